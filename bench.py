@@ -1,0 +1,329 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident fragment-CRC throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], per GPU): 4,194,304 fragments x 4 KiB = 16 GiB,
+device-resident, CRC-32/MPEG-2 (LA-MPI uicrc) of every fragment.  A "step" is one
+lampi_msg_csum launch over the whole batch.  The payload is the SURVEY.md 8(d) synthetic
+stream (seed 2) generated on the device before timing.  With N GPUs each rank owns the
+round-robin shard k = r (mod N) of a global batch of N x 4M fragments (weak scaling, no
+collective on the data path; torch.distributed is used only for the barrier and the
+max-over-ranks time).
+
+Prints ONE JSON line (rank 0):
+  value      = bytes checksummed by all ranks / max-over-ranks wall time of the K steps, GiB/s
+  roofline   = dominant kernel's algorithmic bytes per launch (= 16 GiB payload) / its
+               average launch duration from HIP events on the launch stream, vs 8.0 TB/s
+  cpu_baseline = the reference's uicrc (oracle/_ref, compiled from /root/reference) or the
+               clean-room port, on this host's cores, over a bounded sample of the workload
+  parity     = digest of this rank's results vs the oracle (full digest for the default
+               config, sampled fragments otherwise)
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frags F] [--frag-bytes L]
+       python bench.py --e2e        # host-memory path (config E), for DESIGN.md
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident fragment-CRC GiB/s (batched); % of HBM-read roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = float(1 << 30)
+
+# BASELINE.md oracle digests (CRC XOR, CRC WSUM) of the uniform configs
+GOLDEN = {
+    (2, 4194304, 4096): (0x959621BB, 0xC38D8899),
+    (1, 1048576, 1024): (0xFEB61101, 0x41FADF13),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frags", type=int, default=4194304, help="fragments per GPU")
+    ap.add_argument("--frag-bytes", type=int, default=4096)
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--mode", choices=["crc", "sum"], default="crc")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-bytes", type=int, default=1 << 30)
+    ap.add_argument("--e2e", action="store_true", help="host-memory end-to-end path (config E)")
+    return ap.parse_args()
+
+
+def dist_setup():
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def barrier(world):
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(L: int, seed: int, sample_bytes: int):
+    """Time the reference's uicrc (or the port) on the host cores over a bounded sample."""
+    from oracle.oracle import Reference, Restatement
+
+    port = Restatement()
+    kind, fn, src = "port", port.uicrc_addr(), "oracle/libcsum_ref.so (clean-room restatement)"
+    try:
+        ref = Reference()
+        kind, fn, src = "reference", ref.uicrc_addr(), "oracle/_ref/libref_memfunctions.so (ref MemFunctions.cc)"
+    except (FileNotFoundError, OSError):
+        pass
+    n = max(1, sample_bytes // L)
+    buf = port.stream(seed, 0, n * L)
+    t1, x1 = port.time_crc_fn(fn, buf, n, L, 1)
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
+    tn, xn = port.time_crc_fn(fn, buf, n, L, cores)
+    if x1 != xn:
+        raise RuntimeError("CPU baseline single/multi-thread results differ")
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(n * L / GIB / t1, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
+        "sample": f"{n} x {L} B fragments of stream seed {seed} ({n * L / GIB:.2f} GiB), uicrc init 0xFFFFFFFF, "
+                  f"{src}; timed {t1:.2f} s on 1 core",
+        "all_cores": {"value": round(n * L / GIB / tn, 3), "cores": cores, "seconds": round(tn, 3)},
+        "cpu_model": model,
+    }
+
+
+def read_traffic(config_key: str):
+    """HBM bytes per launch from a committed rocprofv3 PMC run (tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(config_key)
+        return None if e is None else e
+    except (OSError, ValueError):
+        return None
+
+
+def run_device(args):
+    import numpy as np
+    import torch
+
+    from lampi_amd import device as dv
+    from oracle.oracle import Restatement, digest
+
+    rank, world, _ = dist_setup()
+    n, L = args.frags, args.frag_bytes
+    mode = dv.CRC32 if args.mode == "crc" else dv.SUM32
+    stream = torch.cuda.current_stream()
+
+    buf = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    dv.fill_stream_frags(buf, n, L, args.seed, k0=rank, kstep=world)  # shard k = rank (mod world)
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        dv.msg_csum(buf, L, mode=mode, out=out)
+    torch.cuda.synchronize()
+
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(args.steps):
+        dv.msg_csum(buf, L, mode=mode, out=out)
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    wall = max_over_ranks(t1 - t0, world)
+    kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+
+    # parity: this rank's checksums vs the oracle
+    vals = dv.as_u32(out)
+    ref = Restatement()
+    gk = np.arange(n, dtype=np.uint64) * world + rank
+    key = (args.seed, n * world, L)
+    parity = {}
+    if world == 1 and key in GOLDEN and mode == dv.CRC32:
+        x, s = digest(vals, gk)
+        parity = {"check": "full digest vs BASELINE.md", "xor": f"{x:08x}", "wsum": f"{s:08x}",
+                  "ok": (x, s) == GOLDEN[key]}
+    else:
+        rng = np.random.default_rng(rank)
+        idx = np.unique(np.concatenate([np.arange(min(n, 512)), rng.integers(0, n, 512)]))
+        want = np.array([ref.uniform_batch(args.seed, int(gk[i]), 1, L, mode)[0] for i in idx], dtype=np.uint32)
+        parity = {"check": f"{idx.size} sampled fragments vs oracle", "ok": bool(np.array_equal(vals[idx], want))}
+    ok_all = parity["ok"]
+    if world > 1:
+        t = torch.tensor([0 if ok_all else 1], device="cuda")
+        torch.distributed.all_reduce(t)
+        ok_all = int(t.item()) == 0
+
+    bytes_total = float(n) * L * world
+    value = bytes_total / GIB / wall * args.steps
+    achieved = n * L / kern_avg_s / 1e9
+    result = None
+    if rank == 0:
+        cfg_key = f"{'crc' if mode == dv.CRC32 else 'sum'}_{n}x{L}"
+        traffic = read_traffic(cfg_key)
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic: splitmix64 stream seed {args.seed} (SURVEY.md 8(d)), generated on device",
+            "config": {
+                "workload": f"{n} x {L} B fragments per GPU, device-resident, "
+                            f"{'CRC-32/MPEG-2 (uicrc)' if mode == dv.CRC32 else 'uicsum'}, one wavefront per fragment",
+                "fragments_per_gpu": n, "frag_bytes": L, "bytes_per_gpu": n * L,
+                "sharding": "round-robin k = rank (mod N), no collective",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
+                "kernel": "crc_regular_kernel" if mode == dv.CRC32 else "sum_rows_kernel",
+                "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+                "algorithmic_bytes_per_launch": n * L,
+                "traffic_source": None if traffic is None else traffic.get("source"),
+            },
+            "parity": {**parity, "all_ranks_ok": ok_all},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(L, args.seed, args.cpu_sample_bytes)
+        else:
+            result["cpu_baseline"] = None
+    return rank, world, result
+
+
+def run_e2e(args):
+    """Config E: 256 MiB message in pinned host memory -> H2D (copy stream) -> CRC per
+    fragment (compute stream) -> D2H of the u32 array, chunked and overlapped."""
+    import numpy as np
+    import torch
+
+    from lampi_amd import device as dv
+    from oracle.oracle import Restatement
+
+    torch.cuda.set_device(0)
+    msg_bytes = 256 << 20
+    chunk = 16 << 20
+    ref = Restatement()
+    host = torch.empty(msg_bytes, dtype=torch.uint8).pin_memory()
+    host.numpy()[:] = ref.stream(6, 0, msg_bytes)
+    res = {}
+    for L in (4096, 16384, 65456):
+        per_chunk = (chunk // L) * L  # whole fragments per chunk (last fragment of the message may be short)
+        nfr = (msg_bytes + L - 1) // L
+        out_host = torch.empty(nfr, dtype=torch.int32).pin_memory()
+        nbuf = 3
+        dbufs = [torch.empty(per_chunk, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
+        douts = [torch.empty(per_chunk // L + 1, dtype=torch.int32, device="cuda") for _ in range(nbuf)]
+        cp, cs = torch.cuda.Stream(), torch.cuda.Stream()
+        h2d_done = [torch.cuda.Event() for _ in range(nbuf)]
+        crc_done = [torch.cuda.Event() for _ in range(nbuf)]
+
+        def one_pass():
+            off, fi, i = 0, 0, 0
+            while off < msg_bytes:
+                b = i % nbuf
+                nb = min(per_chunk, msg_bytes - off)
+                nf = (nb + L - 1) // L
+                with torch.cuda.stream(cp):
+                    cp.wait_event(crc_done[b])  # buffer b free again
+                    dbufs[b][:nb].copy_(host[off:off + nb], non_blocking=True)
+                    h2d_done[b].record(cp)
+                with torch.cuda.stream(cs):
+                    cs.wait_event(h2d_done[b])
+                    dv.msg_csum(dbufs[b], L, msg_len=nb, out=douts[b], stream=cs)
+                    out_host[fi:fi + nf].copy_(douts[b][:nf], non_blocking=True)
+                    crc_done[b].record(cs)
+                off += nb
+                fi += nf
+                i += 1
+            torch.cuda.synchronize()
+
+        one_pass()
+        reps = 5
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            one_pass()
+        dt = (time.perf_counter() - t0) / reps
+        got = out_host.numpy().view(np.uint32)
+        want = ref.desc_batch(host.numpy(), np.arange(nfr, dtype=np.uint64) * L,
+                              np.minimum(L, msg_bytes - np.arange(nfr) * L).astype(np.uint32), None, 0)
+        res[str(L)] = {"GiB_per_s_incl_h2d_d2h": round(msg_bytes / GIB / dt, 2), "ms_per_256MiB": round(dt * 1e3, 3),
+                       "fragments": int(nfr), "bit_exact": bool(np.array_equal(got, want))}
+    # raw pinned H2D bandwidth for reference
+    d = torch.empty(msg_bytes, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        d.copy_(host, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = msg_bytes * 5 / GIB / (time.perf_counter() - t0)
+    print(json.dumps({"metric": "end-to-end host-memory fragment-CRC (config E, 256 MiB pinned, chunked "
+                                "H2D + CRC + D2H overlapped)", "unit": "GiB/s", "results": res,
+                      "pinned_h2d_GiB_per_s": round(h2d, 2), "chunk_bytes": chunk}))
+
+
+def main():
+    args = parse()
+    if args.e2e:
+        run_e2e(args)
+        return
+    rank, world, result = run_device(args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+/*
+ * lampi_csum.h -- C ABI of the MI355X fragment-checksum engine (liblampi_csum.so).
+ *
+ * Drop-in for LA-MPI's per-fragment data-integrity checksums:
+ *   CRC mode  = uicrc / bcopy_uicrc   (CRC-32/MPEG-2: poly 0x04C11DB7, MSB-first,
+ *               init 0xFFFFFFFF, no reflection, no final XOR)
+ *   SUM mode  = uicsum / bcopy_uicsum (sum mod 2^32 of little-endian 32-bit words,
+ *               trailing partial word zero-padded in its high bytes)
+ * as declared in the reference at src/util/MemFunctions.h:43-65 and applied per
+ * fragment on the send/receive datapath in src/path/{gm,ib,quadrics}.
+ *
+ * All computation runs in hand-written HIP kernels for gfx950.  There is no CPU
+ * fallback: if no GPU is usable the host entry points abort with a message and the
+ * device entry points return a nonzero error code.
+ *
+ * Conventions (mirroring the reference):
+ *   - the caller owns every buffer; nothing is retained after a call returns
+ *     (device entry points: after the stream work completes);
+ *   - checksums are never overloaded as error codes: the scalar host entry points
+ *     return the checksum (as the reference does); the device entry points return
+ *     0 on success or a hipError_t value and write checksums to an output array;
+ *   - chaining state lives with the caller (CRC `partial`, SUM (pint, plen));
+ *   - `stream` is a hipStream_t passed as void* (NULL = the default stream);
+ *     device entry points are stream-ordered, asynchronous, and thread-safe;
+ *   - no global mutable state is visible: the lookup tables are built once per
+ *     device on first use and are read-only afterwards.
+ */
+#ifndef LAMPI_CSUM_H
+#define LAMPI_CSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LAMPI_CRC_POLYNOMIAL      0x04C11DB7u   /* ref src/util/MemFunctions.h:36 */
+#define LAMPI_CRC_INITIAL_REGISTER 0xFFFFFFFFu  /* ref src/util/MemFunctions.h:37 */
+
+/* Checksum mode; the reference selects it at run time with usecrc()
+ * (src/include/internal/state.h:129-132, mpirun -crc). */
+enum lampi_csum_mode {
+    LAMPI_CSUM_CRC32 = 0,   /* uicrc  */
+    LAMPI_CSUM_SUM32 = 1    /* uicsum */
+};
+
+/* ------------------------------------------------------------------------------------
+ * Host-memory, synchronous entry points (same meaning as the reference overloads).
+ * The bytes are moved to the GPU, checksummed (and copied) there, and moved back.
+ * ---------------------------------------------------------------------------------- */
+
+/* replaces unsigned int uicrc(const void*, unsigned long, unsigned int)
+ *   ref src/util/MemFunctions.cc:1331-1367 (mangled _Z5uicrcPKvmj) */
+unsigned int lampi_uicrc(const void *src, unsigned long crclen, unsigned int partial_crc);
+
+/* replaces unsigned int bcopy_uicrc(const void*, void*, unsigned long, unsigned long, unsigned int)
+ *   ref src/util/MemFunctions.cc:1263-1321 (_Z11bcopy_uicrcPKvPvmmj).
+ *   Copies copylen bytes; the CRC covers max(copylen, crclen) bytes of src. */
+unsigned int lampi_bcopy_uicrc(const void *src, void *dst, unsigned long copylen,
+                               unsigned long crclen, unsigned int partial_crc);
+
+/* replaces unsigned int uicsum(const void*, unsigned long, unsigned int*, unsigned int*)
+ *   ref src/util/MemFunctions.cc:1073-1222 (_Z6uicsumPKvmPjS1_).
+ *   Returns the increment to the running sum; (*pint, *plen) is the partial-word state
+ *   (*plen in 0..3; 4 or more is treated as 0, where the reference is undefined). */
+unsigned int lampi_uicsum(const void *src, unsigned long csumlen, unsigned int *pint,
+                          unsigned int *plen);
+
+/* replaces unsigned int bcopy_uicsum(const void*, void*, unsigned long, unsigned long,
+ *                                    unsigned int*, unsigned int*)
+ *   ref src/util/MemFunctions.cc:518-875 (_Z12bcopy_uicsumPKvPvmmPjS2_).
+ *   Copies copylen bytes; the sum covers max(copylen, csumlen) bytes of src. */
+unsigned int lampi_bcopy_uicsum(const void *src, void *dst, unsigned long copylen,
+                                unsigned long csumlen, unsigned int *pint, unsigned int *plen);
+
+/* ------------------------------------------------------------------------------------
+ * Device-resident batched entry points.
+ * ---------------------------------------------------------------------------------- */
+
+/* One fragment.  The descriptor array itself lives in device memory.
+ * Layout is fixed (16 bytes, little-endian): offset 0 addr, 8 length, 12 partial. */
+typedef struct lampi_frag_desc {
+    uint64_t addr;      /* device address of the fragment's first byte (any alignment) */
+    uint32_t length;    /* bytes (0 allowed) */
+    uint32_t partial;   /* CRC mode: CRC register to start from (0xFFFFFFFF = fresh);
+                           SUM mode: ignored (fresh partial-word state) */
+} lampi_frag_desc;
+
+/* out[i] = checksum of fragment d[i] (CRC register or SUM value, as uicrc/uicsum
+ * would return for the same bytes).  One wavefront per fragment.
+ * Replaces the per-fragment loop of gmPath::send / gmSendFragDesc::init
+ * (src/path/gm/path.cc:98-176, src/path/gm/sendFrag.cc:147-155) and the Quadrics
+ * checksum-only send (src/path/quadrics/sendFrag.h:861-872). */
+int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out,
+                          int mode, void *stream);
+
+/* Fragments a contiguous device-resident message the way the path layer does
+ * (fragment k = bytes [k*frag_len, min((k+1)*frag_len, msg_len)),
+ * src/path/gm/path.cc:98-121) and writes ceil(msg_len/frag_len) checksums to d_out.
+ * Every fragment starts from `partial` (CRC mode) or a fresh state (SUM mode). */
+int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t partial,
+                   uint32_t *d_out, int mode, void *stream);
+
+/* ------------------------------------------------------------------------------------
+ * Utilities (bench/test support, device-side).
+ * ---------------------------------------------------------------------------------- */
+
+/* Fill d_dst[0..nbytes) with bytes [byte_off, byte_off + nbytes) of the synthetic
+ * stream of SURVEY.md 8(d): word64[i] = splitmix64(seed + (i+1)*0x9E3779B97F4A7C15), LE. */
+int lampi_fill_stream(void *d_dst, size_t nbytes, uint64_t seed, uint64_t byte_off,
+                      void *stream);
+
+/* Fragment-strided variant: fragment i of d_dst (frag_len bytes, frag_len % 8 == 0,
+ * d_dst 8-byte aligned) holds stream bytes [(k0 + i*kstep)*frag_len, +frag_len), i < n --
+ * the round-robin shard (k = k0 + i*kstep) of a global batch of frag_len-byte fragments. */
+int lampi_fill_stream_frags(void *d_dst, size_t n, size_t frag_len, uint64_t seed, uint64_t k0,
+                            uint64_t kstep, void *stream);
+
+/* Version string of the engine and the gfx target it was built for. */
+const char *lampi_csum_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LAMPI_CSUM_H */

@@ -1,0 +1,77 @@
+"""ctypes binding of liblampi_csum.so (the C ABI declared in include/lampi_csum.h).
+
+The shared library holds the gfx950 kernels; there is no Python or CPU fallback.  If the
+library is missing or cannot be loaded, :func:`lib` raises ``RuntimeError`` -- callers are
+expected to fail loudly, never to compute checksums some other way.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LAMPI_CSUM_LIB", os.path.join(_HERE, "liblampi_csum.so"))
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lampi_csum.h")
+
+CRC32 = 0  # enum lampi_csum_mode (include/lampi_csum.h)
+SUM32 = 1
+CRC_POLYNOMIAL = 0x04C11DB7  # ref src/util/MemFunctions.h:36
+CRC_INITIAL_REGISTER = 0xFFFFFFFF  # ref src/util/MemFunctions.h:37
+
+
+class FragDesc(ctypes.Structure):
+    """struct lampi_frag_desc (16 bytes): addr u64, length u32, partial u32."""
+
+    _fields_ = [("addr", ctypes.c_uint64), ("length", ctypes.c_uint32), ("partial", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(FragDesc) == 16
+
+_lock = threading.Lock()
+_lib = None
+
+c_ulong = ctypes.c_ulong
+c_uint = ctypes.c_uint
+c_void_p = ctypes.c_void_p
+c_size_t = ctypes.c_size_t
+PUINT = ctypes.POINTER(ctypes.c_uint)
+
+# name -> (restype, argtypes); the full exported C ABI.
+PROTOTYPES = {
+    "lampi_uicrc": (c_uint, [c_void_p, c_ulong, c_uint]),
+    "lampi_bcopy_uicrc": (c_uint, [c_void_p, c_void_p, c_ulong, c_ulong, c_uint]),
+    "lampi_uicsum": (c_uint, [c_void_p, c_ulong, PUINT, PUINT]),
+    "lampi_bcopy_uicsum": (c_uint, [c_void_p, c_void_p, c_ulong, c_ulong, PUINT, PUINT]),
+    "lampi_frag_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
+    "lampi_msg_csum": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, c_void_p, ctypes.c_int,
+                                      c_void_p]),
+    "lampi_fill_stream": (ctypes.c_int, [c_void_p, c_size_t, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
+    "lampi_fill_stream_frags": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                               ctypes.c_uint64, c_void_p]),
+    "lampi_csum_version": (ctypes.c_char_p, []),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return liblampi_csum.so with prototypes set; raise if absent."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"liblampi_csum.so not found at {LIB_PATH}: build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in PROTOTYPES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+        return _lib
+
+
+def check(rc: int, what: str) -> None:
+    """Raise on a nonzero hipError_t code returned by a device entry point."""
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError_t {rc}")

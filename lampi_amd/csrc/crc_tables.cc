@@ -1,0 +1,102 @@
+// crc_tables.cc -- see crc_tables.h.
+#include "crc_tables.h"
+
+#include <cstring>
+#include <mutex>
+
+namespace lampi {
+
+namespace {
+uint32_t g_T[256];
+std::once_flag g_T_once;
+
+void build_T() {
+    // entry i: byte i placed in bits 31..24, shifted through 8 polynomial steps
+    // (semantics of ref ulm_initialize_crc_table, MemFunctions.cc:1242-1261)
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t r = i << 24;
+        for (int k = 0; k < 8; ++k) r = (r & 0x80000000u) ? (r << 1) ^ kCrcPoly : (r << 1);
+        g_T[i] = r;
+    }
+}
+
+inline uint32_t zero_byte(uint32_t c) { return (c << 8) ^ g_T[c >> 24]; }
+}  // namespace
+
+const uint32_t *sarwate_table() {
+    std::call_once(g_T_once, build_T);
+    return g_T;
+}
+
+uint32_t crc_bytes(uint32_t crc, const uint8_t *p, size_t n) {
+    const uint32_t *T = sarwate_table();
+    for (size_t i = 0; i < n; ++i) crc = (crc << 8) ^ T[(crc >> 24) ^ p[i]];
+    return crc;
+}
+
+Gf2Mat mat_identity() {
+    Gf2Mat m;
+    for (int b = 0; b < 32; ++b) m.col[b] = 1u << b;
+    return m;
+}
+
+Gf2Mat mat_mul(const Gf2Mat &a, const Gf2Mat &b) {
+    Gf2Mat r;
+    for (int k = 0; k < 32; ++k) r.col[k] = a.apply(b.col[k]);
+    return r;
+}
+
+Gf2Mat shift_matrix(uint64_t nbytes) {
+    sarwate_table();
+    Gf2Mat one;  // one zero byte
+    for (int b = 0; b < 32; ++b) one.col[b] = zero_byte(1u << b);
+    Gf2Mat acc = mat_identity(), sq = one;
+    for (uint64_t n = nbytes; n; n >>= 1) {
+        if (n & 1) acc = mat_mul(sq, acc);
+        sq = mat_mul(sq, sq);
+    }
+    return acc;
+}
+
+Gf2Mat swapped(const Gf2Mat &m) {
+    Gf2Mat r;
+    for (int b = 0; b < 32; ++b) r.col[b] = bswap32(m.apply(bswap32(1u << b)));
+    return r;
+}
+
+void nibble_tables(const Gf2Mat &ms, uint32_t out[128]) {
+    for (int p = 0; p < 8; ++p)
+        for (uint32_t v = 0; v < 16; ++v) out[p * 16 + v] = ms.apply(v << (4 * p));
+}
+
+std::vector<uint32_t> build_table_image() {
+    const uint32_t *T = sarwate_table();
+    std::vector<uint32_t> img(kImgWords, 0);
+
+    // per-lane final shift: lane l's last byte sits 64*(63-l) bytes before the row end
+    const Gf2Mat step = shift_matrix(kLaneBytes);
+    Gf2Mat m = mat_identity();  // m = shift by 64*(63-l), built from l = 63 downwards
+    for (int l = kWave - 1; l >= 0; --l) {
+        uint32_t nt[128];
+        nibble_tables(swapped(m), nt);
+        for (int p = 0; p < 8; ++p)
+            for (int v = 0; v < 16; ++v) img[kImgCombine + p * 1024 + v * 64 + l] = nt[p * 16 + v];
+        m = mat_mul(step, m);
+    }
+
+    // Horner step between rows: the next 64-byte piece of a lane starts 4032 bytes later
+    nibble_tables(swapped(shift_matrix(kRowBytes - kLaneBytes)), &img[kImgHorner]);
+
+    // slicing-by-4 in the swapped domain: for X = C ^ w (w = LE load),
+    //   C' = S_0[X.b0] ^ S_1[X.b1] ^ S_2[X.b2] ^ S_3[X.b3],  S_j = bswap(T_{3-j})
+    uint32_t Tk[4][256];
+    for (int i = 0; i < 256; ++i) {
+        Tk[0][i] = T[i];
+        for (int k = 1; k < 4; ++k) Tk[k][i] = zero_byte(Tk[k - 1][i]);
+    }
+    for (int j = 0; j < 4; ++j)
+        for (int i = 0; i < 256; ++i) img[kImgSlice + j * 256 + i] = bswap32(Tk[3 - j][i]);
+    return img;
+}
+
+}  // namespace lampi

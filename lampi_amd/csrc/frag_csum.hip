@@ -1,0 +1,733 @@
+// frag_csum.hip -- gfx950 kernels for LA-MPI's per-fragment checksums.
+//
+// CRC mode (uicrc, ref src/util/MemFunctions.cc:1331-1367) -- one wavefront per fragment:
+//   * The fragment is right-aligned in a frame of R rows of 4096 bytes (R = ceil(L/4096));
+//     the P = 4096R - L leading frame bytes are zeros.  Leading zeros do not change a CRC
+//     computed from a zero register, so every lane runs the same code.
+//   * The caller's starting register (`partial`, 0xFFFFFFFF fresh) is XORed into the
+//     first four message bytes (crc(s, B) = crc(0, B ^ bytes_BE(s)), |B| >= 4; the
+//     |B| < 4 remainder s << 8|B| is added at the end).
+//   * Lane l owns bytes [64l, 64l+64) of each row: 4 x dwordx4 loads (lane-contiguous,
+//     measured as fast as fully coalesced rows on MI355X), slicing-by-4 CRC from a zero
+//     register, table lookups in LDS addressed by one v_perm each.
+//   * Between rows a lane's register jumps 4032 zero bytes (nibble-table shift, Horner).
+//   * At the end lane l applies its own shift by 64*(63-l) bytes (per-lane nibble
+//     tables, conflict-free) and the 64 registers are XOR-reduced across the wave.
+//   LDS (one 1024-thread workgroup per CU, persistent over fragments):
+//     [0, 32768)      per-lane combine tables  p*4096 + v*256 + 4l   (bank = l % 32)
+//     [32768, 33280)  Horner shift tables      p*64 + 4v             (16 banks, broadcast)
+//     [33280, 98816)  slicing tables, 16 copies: entry i of S_j, copy c at
+//                     i*256 + j*64 + 4c.  Lanes 0-15 and 16-31 of a ds_read_b32 group
+//                     read tables of opposite parity -> 32 distinct banks, no conflicts.
+//
+// SUM mode (uicsum, ref MemFunctions.cc:1073-1222): left-aligned rows, lane-contiguous
+// 64-byte pieces, funnel-shifted to the fragment's own word grid, zero-padded tail,
+// 32-bit adds reduced across the wave.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "crc_tables.h"
+#include "frag_csum_kernels.h"
+
+namespace lampi {
+
+namespace {
+
+constexpr uint32_t kLdsCombine = 0;
+constexpr uint32_t kLdsHorner = 32768;
+constexpr uint32_t kLdsSlice = 33280;
+constexpr uint32_t kLdsBytes = 33280 + 65536;
+constexpr int kBlock = 1024;
+
+// Global-address-space byte pointer: keeps loads as global_load_* (flat loads would force
+// vmcnt(0) + lgkmcnt(0) waits and defeat the prefetch).
+typedef __attribute__((address_space(1))) const uint8_t gbyte;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+typedef __attribute__((address_space(1))) const uint32_t guint;
+
+struct FragInfo {
+    gbyte *addr;
+    uint32_t len;
+    uint32_t partial;
+};
+
+// ---- fragment sources (wave-uniform) ----------------------------------------------
+struct DescSource {
+    const lampi_frag_desc *d;
+    __device__ FragInfo get(size_t f) const {
+        const lampi_frag_desc x = d[f];
+        return {(gbyte *)(uintptr_t)x.addr, x.length, x.partial};
+    }
+};
+
+struct MsgSource {
+    const uint8_t *base;
+    size_t msg_len;
+    size_t frag_len;
+    uint32_t partial;
+    __device__ FragInfo get(size_t f) const {
+        size_t off = f * frag_len;
+        size_t rem = msg_len - off;
+        return {(gbyte *)(base + off), (uint32_t)(rem < frag_len ? rem : frag_len), partial};
+    }
+};
+
+__device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
+}
+
+// ---- loads --------------------------------------------------------------------------
+// Load the 64 bytes at signed offset o (relative to frag) into d[16] as LE words.
+// Bytes at offsets < lo or >= hi read as zero; nothing outside [lo, hi) is dereferenced
+// except within aligned 16-byte chunks that hold at least one byte inside (same page).
+// `mask` selects whether any masking can be needed (wave-uniform).
+__device__ __forceinline__ uint32_t byte_keep_mask(long long ow, long long lo, long long hi) {
+    // keep byte j of the word at offset ow iff lo <= ow + j < hi
+    long long a = lo - ow;  // bytes to drop at the bottom
+    long long b = ow + 4 - hi;  // bytes to drop at the top
+    uint32_t m = 0xFFFFFFFFu;
+    if (a >= 4 || b >= 4) return 0;
+    if (a > 0) m <<= 8 * a;
+    if (b > 0) m &= 0xFFFFFFFFu >> (8 * b);
+    return m;
+}
+
+__device__ __forceinline__ void load64(gbyte *frag, long long o, long long lo, long long hi,
+                                       bool mask, uint32_t s16, uint32_t d[16]) {
+    if (s16 == 0) {
+        // 16-byte aligned chunks
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            long long c = o + 16 * k;
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (!mask || (c + 16 > lo && c < hi))
+                v = *(gu32x4 *)(frag + c);
+            d[4 * k + 0] = v.x;
+            d[4 * k + 1] = v.y;
+            d[4 * k + 2] = v.z;
+            d[4 * k + 3] = v.w;
+        }
+    } else {
+        // not 16-byte aligned: 17 aligned dwords, funnel-shifted by s16 % 4 bytes.  An
+        // aligned dword holding a byte of the fragment never crosses a page.
+        uint32_t a[17];
+        const uint32_t sh = s16 & 3u;
+        const long long c0 = o - (long long)sh;
+#pragma unroll
+        for (int k = 0; k < 17; ++k) {
+            const long long c = c0 + 4 * k;
+            a[k] = (c + 4 > lo && c < hi) ? *(guint *)(frag + c) : 0u;
+        }
+#pragma unroll
+        for (int w = 0; w < 16; ++w) d[w] = __builtin_amdgcn_alignbyte(a[w + 1], a[w], sh);
+    }
+    if (mask) {
+#pragma unroll
+        for (int w = 0; w < 16; ++w) d[w] &= byte_keep_mask(o + 4 * w, lo, hi);
+    }
+}
+
+// ---- CRC pieces -----------------------------------------------------------------------
+struct CrcLane {
+    uint32_t lanec;   // byte t: LDS low byte of table t, copy (lane & 15)
+    uint32_t sel[4];  // v_perm selectors: byte0 <- lanec.byte(j), byte1 <- X.byte(j)
+    uint32_t l4;      // 4 * lane
+};
+
+__device__ __forceinline__ CrcLane make_lane(int lane) {
+    CrcLane k;
+    const uint32_t c4 = (uint32_t)(lane & 15) * 4u;
+    k.lanec = c4 | ((c4 + 64u) << 8) | ((c4 + 128u) << 16) | ((c4 + 192u) << 24);
+    const uint32_t flip = (lane & 16) ? 1u : 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t j = (uint32_t)q ^ flip;
+        k.sel[q] = j | ((4u + j) << 8) | 0x0C0C0000u;
+    }
+    k.l4 = (uint32_t)lane * 4u;
+    return k;
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
+}
+
+// slicing-by-4 lookups of X (swapped domain): one v_perm + one ds_read_b32 each
+struct Look4 {
+    uint32_t t0, t1, t2, t3;
+};
+__device__ __forceinline__ Look4 look4(const uint32_t *lds, const CrcLane &k, uint32_t X) {
+    Look4 r;
+    r.t0 = lds_u32(lds, kLdsSlice + __builtin_amdgcn_perm(X, k.lanec, k.sel[0]));
+    r.t1 = lds_u32(lds, kLdsSlice + __builtin_amdgcn_perm(X, k.lanec, k.sel[1]));
+    r.t2 = lds_u32(lds, kLdsSlice + __builtin_amdgcn_perm(X, k.lanec, k.sel[2]));
+    r.t3 = lds_u32(lds, kLdsSlice + __builtin_amdgcn_perm(X, k.lanec, k.sel[3]));
+    return r;
+}
+
+// register C (swapped domain) through the 16 words of a lane's 64-byte piece:
+// per word 4 v_perm + 4 ds_read_b32 + 2 v_bitop3 (the next word's data XOR is fused)
+__device__ __forceinline__ uint32_t crc_piece(const uint32_t *lds, const CrcLane &k, uint32_t C,
+                                              const uint32_t d[16]) {
+    uint32_t X = C ^ d[0];
+#pragma unroll
+    for (int w = 0; w < 15; ++w) {
+        const Look4 t = look4(lds, k, X);
+        X = xor3(xor3(t.t0, t.t1, t.t2), t.t3, d[w + 1]);
+    }
+    const Look4 t = look4(lds, k, X);
+    return xor3(t.t0, t.t1, t.t2) ^ t.t3;
+}
+
+// shift by 4032 zero bytes (all lanes read the same 16-entry tables: conflict free)
+__device__ __forceinline__ uint32_t horner_shift(const uint32_t *lds, uint32_t C) {
+    uint32_t r = lds_u32(lds, kLdsHorner + ((C << 2) & 0x3Cu));
+#pragma unroll
+    for (int p = 1; p < 8; ++p) r ^= lds_u32(lds, kLdsHorner + p * 64 + ((C >> (4 * p - 2)) & 0x3Cu));
+    return r;
+}
+
+// lane l: shift by 64*(63-l) zero bytes (lane-private tables, bank l % 32)
+__device__ __forceinline__ uint32_t lane_combine(const uint32_t *lds, const CrcLane &k, uint32_t C) {
+    uint32_t r = lds_u32(lds, kLdsCombine + (((C << 8) & 0xF00u) | k.l4));
+    r ^= lds_u32(lds, kLdsCombine + 4096 + (((C << 4) & 0xF00u) | k.l4));
+    r ^= lds_u32(lds, kLdsCombine + 8192 + ((C & 0xF00u) | k.l4));
+#pragma unroll
+    for (int p = 3; p < 8; ++p)
+        r ^= lds_u32(lds, kLdsCombine + p * 4096 + (((C >> (4 * p - 8)) & 0xF00u) | k.l4));
+    return r;
+}
+
+// XOR of v over the 64 lanes: DPP butterflies inside each row of 16, then 4 readlanes.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+    return __builtin_amdgcn_readlane(v, 0) ^ __builtin_amdgcn_readlane(v, 16) ^ __builtin_amdgcn_readlane(v, 32) ^
+           __builtin_amdgcn_readlane(v, 48);
+}
+
+__device__ __forceinline__ uint32_t wave_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+           __builtin_amdgcn_readlane(v, 48);
+}
+
+struct RowGeom {
+    uint32_t R;    // rows
+    uint32_t P;    // frame padding in front of byte 0
+    uint32_t s16;  // (addr - P) mod 16, the chunk misalignment (same for every lane)
+};
+
+__device__ __forceinline__ RowGeom crc_geom(const FragInfo &fi) {
+    RowGeom g;
+    g.R = (fi.len + (kRowBytes - 1)) / kRowBytes;
+    g.P = g.R * kRowBytes - fi.len;
+    g.s16 = (uint32_t)(((uintptr_t)fi.addr - g.P) & 15u);
+    return g;
+}
+
+__device__ __forceinline__ void crc_load_row(const FragInfo &fi, const RowGeom &g, uint32_t r, int lane,
+                                             uint32_t d[16]) {
+    const long long o = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P;
+    // only row 0 of a padded or misaligned frame can touch bytes before the fragment
+    const bool mask = (r == 0) && (g.P != 0 || (((uintptr_t)fi.addr & 15u) != 0));
+    load64(fi.addr, o, 0, (long long)fi.len, mask, g.s16, d);
+}
+
+// XOR bytes_BE(partial) into frame bytes P..P+3 (row 0).
+__device__ __forceinline__ void crc_inject(uint32_t d[16], const RowGeom &g, uint32_t partial, int lane) {
+    const uint32_t v = __builtin_bswap32(partial);  // LE byte j = BE byte j of partial
+    const uint32_t l0 = g.P >> 6;
+    const uint32_t a = (g.P >> 2) & 15u;
+    const uint32_t q = g.P & 3u;
+    const uint32_t m0 = v << (8 * q);
+    const uint32_t m1 = q ? (v >> (32 - 8 * q)) : 0u;
+    const bool own = (uint32_t)lane == l0;
+    const uint32_t mA = own ? m0 : 0u;
+    const uint32_t mB = own ? m1 : 0u;
+    const uint32_t mC = ((uint32_t)lane == l0 + 1 && a == 15u) ? m1 : 0u;
+    d[0] ^= mC;
+#pragma unroll
+    for (uint32_t w = 0; w < 16; ++w) d[w] ^= (w == a) ? mA : ((w == a + 1) ? mB : 0u);
+}
+
+template <class Src>
+__global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, const uint32_t *__restrict__ img,
+                                                          uint32_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+
+    // stage tables: combine + Horner verbatim, slicing tables replicated 16x
+    for (uint32_t i = threadIdx.x; i < kLdsSlice / 4; i += kBlock) lds[i] = img[i];
+    for (uint32_t i = threadIdx.x; i < 16384u; i += kBlock) {
+        const uint32_t e = i >> 6, j = (i >> 4) & 3u;
+        lds[kLdsSlice / 4 + i] = img[kImgSlice + j * 256 + e];
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const CrcLane k = make_lane(lane);
+    const size_t nwaves = (size_t)gridDim.x * (kBlock / 64);
+    size_t f = uniform((uint32_t)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)));
+
+    // skip empty fragments up front
+    auto next_nonempty = [&](size_t x, FragInfo &fi) -> size_t {
+        for (; x < n; x += nwaves) {
+            fi = src.get(x);
+            fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
+            fi.len = uniform(fi.len);
+            fi.partial = uniform(fi.partial);
+            if (fi.len) break;
+            if (lane == 0) out[x] = fi.partial;  // uicrc(p, 0, s) == s
+        }
+        return x;
+    };
+
+    FragInfo cur;
+    f = next_nonempty(f, cur);
+    if (f >= n) return;
+    RowGeom g = crc_geom(cur);
+    uint32_t r = 0;
+    uint32_t d[16];
+    crc_load_row(cur, g, 0, lane, d);
+    uint32_t C = 0;
+
+    for (;;) {
+        // prefetch the next row task
+        FragInfo nfi = cur;
+        RowGeom ng = g;
+        size_t nf = f;
+        uint32_t nr = r + 1;
+        if (nr >= g.R) {
+            nf = next_nonempty(f + nwaves, nfi);
+            nr = 0;
+            if (nf < n) ng = crc_geom(nfi);
+        }
+        const bool more = nf < n;
+        uint32_t nd[16];
+        if (more) crc_load_row(nfi, ng, nr, lane, nd);
+
+        // process the current row
+        if (r == 0) {
+            if (g.P == 0) {
+                C = (lane == 0) ? __builtin_bswap32(cur.partial) : 0u;
+            } else {
+                C = 0;
+                crc_inject(d, g, cur.partial, lane);
+            }
+        } else {
+            C = horner_shift(lds, C);
+            if (r == 1 && g.P > (uint32_t)kRowBytes - 4 && lane == 0)  // register bytes spill into row 1
+                d[0] ^= __builtin_bswap32(cur.partial) >> (8 * (kRowBytes - g.P));
+        }
+        C = crc_piece(lds, k, C, d);
+
+        if (r + 1 == g.R) {
+            C = wave_xor(lane_combine(lds, k, C));
+            if (lane == 0) {
+                uint32_t res = __builtin_bswap32(C);
+                if (cur.len < 4) res ^= cur.partial << (8 * cur.len);
+                out[f] = res;
+            }
+        }
+        if (!more) break;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) d[w] = nd[w];
+        cur = nfi;
+        g = ng;
+        f = nf;
+        r = nr;
+    }
+}
+
+// ---- CRC fast path: regular batches -------------------------------------------------------
+// Fragment f = base + f*frag_len, frag_len = R*4096, base 16-byte aligned (P = 0, no masks).
+// A wave walks its (fragment, row) tasks with two register buffers; the next task's loads
+// are always issued (clamped to the last task) so the hot loop has no load-side branches.
+// One row task of a wave: fragment i (global index f0 + i*nw, first byte at fptr), row r.
+struct RegTask {
+    uint64_t foff;  // wave-uniform byte offset of the fragment's first byte from base
+    uint32_t i, r;
+};
+// Row loads for the regular kernel are issued by inline asm and waited for by an explicit
+// s_waitcnt that takes the destination registers as in/out operands: hipcc's waitcnt pass
+// merges loop-carried load state conservatively (it waited for two rows where one was
+// needed), and an asm load is invisible to it.  Every global load/store the compiler emits
+// in the loop is older than or unrelated to these, so counting only our own loads is exact
+// or conservative (a younger store only makes the wait stricter).
+struct Row {
+    u32x4 q[4];
+};
+
+__device__ __forceinline__ void issue_row(gbyte *p, Row &r) {
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off\n\t"
+        "global_load_dwordx4 %1, %4, off offset:16\n\t"
+        "global_load_dwordx4 %2, %4, off offset:32\n\t"
+        "global_load_dwordx4 %3, %4, off offset:48"
+        : "=&v"(r.q[0]), "=&v"(r.q[1]), "=&v"(r.q[2]), "=&v"(r.q[3])
+        : "v"(p)
+        : "memory");
+}
+
+// wait until at most N of this wave's vector-memory ops are outstanding; r's registers are
+// threaded through so no use of them can be scheduled above the wait
+template <int N>
+__device__ __forceinline__ void wait_row(Row &r) {
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(r.q[0]), "+v"(r.q[1]), "+v"(r.q[2]), "+v"(r.q[3]) : "n"(N) : "memory");
+}
+
+__device__ __forceinline__ void row_words(const Row &r, uint32_t d[16]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        d[4 * k + 0] = r.q[k].x;
+        d[4 * k + 1] = r.q[k].y;
+        d[4 * k + 2] = r.q[k].z;
+        d[4 * k + 3] = r.q[k].w;
+    }
+}
+
+__device__ __forceinline__ void crc_reg_row(const uint32_t *lds, const CrcLane &k, int lane, uint32_t &C,
+                                            const uint32_t d[16], uint32_t r, uint32_t R, uint32_t vinit,
+                                            uint32_t *out, size_t f) {
+    if (r == 0)
+        C = (lane == 0) ? vinit : 0u;
+    else
+        C = horner_shift(lds, C);
+    C = crc_piece(lds, k, C, d);
+    if (r + 1 == R) {
+        const uint32_t x = wave_xor(lane_combine(lds, k, C));
+        if (lane == 0) out[f] = __builtin_bswap32(x);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, size_t n,
+                                                             size_t frag_len, uint32_t partial,
+                                                             const uint32_t *__restrict__ img,
+                                                             uint32_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    for (uint32_t i = threadIdx.x; i < kLdsSlice / 4; i += kBlock) lds[i] = img[i];
+    for (uint32_t i = threadIdx.x; i < 16384u; i += kBlock) {
+        const uint32_t e = i >> 6, j = (i >> 4) & 3u;
+        lds[kLdsSlice / 4 + i] = img[kImgSlice + j * 256 + e];
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const CrcLane k = make_lane(lane);
+    const uint32_t R = (uint32_t)(frag_len / kRowBytes);
+    const uint32_t nw = gridDim.x * (kBlock / 64);
+    const uint32_t f0 = uniform(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+    if (f0 >= n) return;
+    const uint32_t nfr = (uint32_t)((n - f0 + nw - 1) / nw);  // fragments of this wave
+    const uint64_t fstep = (uint64_t)nw * frag_len;
+    const uint32_t vinit = __builtin_bswap32(partial);
+    const uint32_t lane_off = (uint32_t)lane * kLaneBytes;
+    uint32_t C = 0;
+
+    // next task, clamped to the last one (its reload is harmless and keeps loads unconditional)
+    auto advance = [&](RegTask t) -> RegTask {
+        if (t.r + 1 < R) return {t.foff, t.i, t.r + 1};
+        if (t.i + 1 < nfr) return {t.foff + fstep, t.i + 1, 0u};
+        return t;
+    };
+    auto row_ptr = [&](const RegTask &t) -> gbyte * {
+        return (gbyte *)(base + (t.foff + (uint64_t)t.r * kRowBytes + lane_off));
+    };
+    auto is_last = [&](const RegTask &t) -> bool { return t.i + 1 >= nfr && t.r + 1 >= R; };
+    auto process = [&](Row &buf, const RegTask &t) {
+        uint32_t d[16];
+        row_words(buf, d);
+        crc_reg_row(lds, k, lane, C, d, t.r, R, vinit, out, (size_t)f0 + (size_t)t.i * nw);
+    };
+
+    // three row buffers: two rows stay in flight while the third is checksummed
+    RegTask ta{(uint64_t)f0 * frag_len, 0u, 0u};
+    RegTask tb = advance(ta);
+    Row A, B, Cb;
+    issue_row(row_ptr(ta), A);
+    issue_row(row_ptr(tb), B);
+    for (;;) {
+        RegTask tc = advance(tb);
+        issue_row(row_ptr(tc), Cb);
+        wait_row<8>(A);
+        process(A, ta);
+        if (is_last(ta)) break;
+        ta = advance(tc);
+        issue_row(row_ptr(ta), A);
+        wait_row<8>(B);
+        process(B, tb);
+        if (is_last(tb)) break;
+        tb = advance(ta);
+        issue_row(row_ptr(tb), B);
+        wait_row<8>(Cb);
+        process(Cb, tc);
+        if (is_last(tc)) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped re-loads before exit
+}
+
+// ---- SUM -------------------------------------------------------------------------------
+template <class Src>
+__global__ void __launch_bounds__(256) sum_rows_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const size_t nwaves = (size_t)gridDim.x * (256 / 64);
+    for (size_t f = uniform((uint32_t)(blockIdx.x * 4 + (threadIdx.x >> 6))); f < n; f += nwaves) {
+        FragInfo fi = src.get(f);
+        fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
+        fi.len = uniform(fi.len);
+        const uint32_t R = (fi.len + (kRowBytes - 1)) / kRowBytes;
+        const uint32_t s16 = (uint32_t)((uintptr_t)fi.addr & 15u);
+        uint32_t acc = 0;
+        for (uint32_t r = 0; r < R; ++r) {
+            const long long o = (long long)r * kRowBytes + lane * kLaneBytes;
+            const bool mask = (r + 1 == R) && (fi.len % kRowBytes != 0 || s16 != 0);
+            uint32_t d[16];
+            load64(fi.addr, o, 0, (long long)fi.len, mask || s16 != 0, s16, d);
+#pragma unroll
+            for (int w = 0; w < 16; ++w) acc += d[w];
+        }
+        acc = wave_add(acc);
+        if (lane == 0) out[f] = acc;
+    }
+}
+
+// ---- synthetic stream fill ----------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    z *= 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return z;
+}
+__device__ __forceinline__ uint64_t stream_word(uint64_t seed, uint64_t i) {
+    return mix64(seed + (i + 1) * 0x9E3779B97F4A7C15ull);
+}
+
+__global__ void __launch_bounds__(256) fill_stream_kernel(uint8_t *dst, size_t nbytes, uint64_t seed,
+                                                          uint64_t byte_off) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const uint32_t s = (uint32_t)(byte_off & 7u);
+    const uint64_t w0 = byte_off >> 3;
+    const size_t nfull = nbytes / 16;
+    const bool aligned16 = (((uintptr_t)dst) & 15u) == 0;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < nfull; t += stride) {
+        uint64_t a = stream_word(seed, w0 + 2 * t);
+        uint64_t b = stream_word(seed, w0 + 2 * t + 1);
+        uint64_t lo = a, hi = b;
+        if (s) {
+            uint64_t c = stream_word(seed, w0 + 2 * t + 2);
+            lo = (a >> (8 * s)) | (b << (64 - 8 * s));
+            hi = (b >> (8 * s)) | (c << (64 - 8 * s));
+        }
+        if (aligned16) {
+            reinterpret_cast<ulonglong2 *>(dst)[t] = make_ulonglong2(lo, hi);
+        } else {
+            for (int j = 0; j < 8; ++j) dst[16 * t + j] = (uint8_t)(lo >> (8 * j));
+            for (int j = 0; j < 8; ++j) dst[16 * t + 8 + j] = (uint8_t)(hi >> (8 * j));
+        }
+    }
+    // tail bytes
+    const size_t tail0 = nfull * 16;
+    for (size_t i = tail0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += stride) {
+        uint64_t pos = byte_off + i;
+        dst[i] = (uint8_t)(stream_word(seed, pos >> 3) >> (8 * (pos & 7u)));
+    }
+}
+
+// ---- CRC combine over equal-size pieces ---------------------------------------------------
+// vals[0..n): crc(s_k, piece_k) of consecutive pieces of a front-padded message, each
+// piece B bytes (the first may be shorter: leading zeros are free).  Tree over a
+// power-of-two frame padded with zero pieces in front:  (A, B) -> shift_B(A) ^ B.
+// tabs[lvl*128 + p*16 + v]: normal-domain nibble tables of shift by B * 2^lvl.
+__global__ void __launch_bounds__(1024) crc_combine_kernel(const uint32_t *__restrict__ vals, uint32_t n,
+                                                           const uint32_t *__restrict__ tabs, uint32_t npow,
+                                                           uint32_t *__restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t v[];  // 2 * npow words: ping-pong
+    const uint32_t pad = npow - n;
+    for (uint32_t i = threadIdx.x; i < npow; i += blockDim.x) v[i] = (i < pad) ? 0u : vals[i - pad];
+    __syncthreads();
+    uint32_t *src = v, *dst = v + npow;
+    uint32_t lvl = 0;
+    for (uint32_t m = npow; m > 1; m >>= 1, ++lvl) {
+        const uint32_t *t = tabs + lvl * 128;
+        for (uint32_t i = threadIdx.x; i < m / 2; i += blockDim.x) {
+            const uint32_t a = src[2 * i];
+            uint32_t r = src[2 * i + 1];
+#pragma unroll
+            for (int p = 0; p < 8; ++p) r ^= t[p * 16 + ((a >> (4 * p)) & 15u)];
+            dst[i] = r;
+        }
+        __syncthreads();
+        uint32_t *tmp = src;
+        src = dst;
+        dst = tmp;
+    }
+    if (threadIdx.x == 0) out[0] = src[0];
+}
+
+// ---- SUM over a chained stream ------------------------------------------------------------
+// The body [t, t + 4*nb) was summed by sum_rows_kernel in word-aligned pieces (partials);
+// this adds the head (completing the caller's partial word) and the tail partial word and
+// produces the new (pint, plen) state.  out3 = {sum, pint, plen}.
+__global__ void sum_stream_finish_kernel(const uint32_t *__restrict__ partials, uint32_t npart,
+                                         const uint8_t *__restrict__ src, uint64_t len, uint32_t pint,
+                                         uint32_t plen, uint32_t *__restrict__ out3) {
+    __shared__ uint32_t red[256];
+    uint32_t acc = 0;
+    for (uint32_t i = threadIdx.x; i < npart; i += blockDim.x) acc += partials[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    uint32_t sum = red[0];
+    uint32_t k = plen >= 4 ? 0u : plen;
+    uint64_t pos = 0;
+    if (k) {
+        uint32_t w = pint;
+        uint64_t take = 4 - k;
+        if (take > len) take = len;
+        for (uint64_t j = 0; j < take; ++j) {
+            const uint32_t sh = 8u * (uint32_t)(k + j);
+            w = (w & ~(0xFFu << sh)) | ((uint32_t)src[j] << sh);
+        }
+        sum += w - pint;
+        pos = take;
+        if (k + take < 4) {
+            out3[0] = sum;
+            out3[1] = w;
+            out3[2] = k + (uint32_t)take;
+            return;
+        }
+    }
+    const uint64_t body = (len - pos) & ~3ull;
+    const uint64_t r = (len - pos) & 3ull;
+    uint32_t tail = 0;
+    for (uint64_t j = 0; j < r; ++j) tail |= (uint32_t)src[pos + body + j] << (8 * j);
+    out3[0] = sum + tail;
+    out3[1] = tail;
+    out3[2] = (uint32_t)r;
+}
+
+// Fragment-strided stream: fragment i of dst (frag_len bytes, frag_len % 8 == 0) holds stream
+// bytes [(k0 + i*kstep) * frag_len, +frag_len) -- a round-robin shard of a global batch.
+__global__ void __launch_bounds__(256) fill_frags_kernel(uint64_t *dst, size_t n, uint64_t frag_words,
+                                                         uint64_t seed, uint64_t k0, uint64_t kstep) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t total = n * frag_words;
+    for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        const uint64_t i = t / frag_words, j = t - i * frag_words;
+        dst[t] = stream_word(seed, (k0 + i * kstep) * frag_words + j);
+    }
+}
+
+}  // namespace
+
+// ---- launchers ---------------------------------------------------------------------------
+int crc_grid(int device) {
+    static int cu[64] = {0};
+    if (device < 0 || device >= 64) device = 0;
+    if (!cu[device]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0) v = 256;
+        cu[device] = v;
+    }
+    return cu[device];
+}
+
+hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
+                           hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    size_t need = (n + 15) / 16;
+    int g = (int)(need < (size_t)grid ? need : (size_t)grid);
+    hipLaunchKernelGGL(crc_rows_kernel<DescSource>, dim3(g), dim3(kBlock), 0, s, DescSource{d}, n, img, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, size_t n,
+                          uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    size_t need = (n + 15) / 16;
+    int g = (int)(need < (size_t)grid ? need : (size_t)grid);
+    hipLaunchKernelGGL(crc_rows_kernel<MsgSource>, dim3(g), dim3(kBlock), 0, s,
+                       MsgSource{base, msg_len, frag_len, partial}, n, img, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
+                              const uint32_t *img, int grid, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    size_t need = (n + 15) / 16;
+    int g = (int)(need < (size_t)grid ? need : (size_t)grid);
+    hipLaunchKernelGGL(crc_regular_kernel, dim3(g), dim3(kBlock), 0, s, base, n, frag_len, partial, img, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, int grid, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    size_t need = (n + 3) / 4;
+    size_t cap = (size_t)grid * 8;
+    int g = (int)(need < cap ? need : cap);
+    hipLaunchKernelGGL(sum_rows_kernel<DescSource>, dim3(g), dim3(256), 0, s, DescSource{d}, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out, int grid,
+                          hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    size_t need = (n + 3) / 4;
+    size_t cap = (size_t)grid * 8;
+    int g = (int)(need < cap ? need : cap);
+    hipLaunchKernelGGL(sum_rows_kernel<MsgSource>, dim3(g), dim3(256), 0, s,
+                       MsgSource{base, msg_len, frag_len, 0u}, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc_combine(const uint32_t *vals, uint32_t n, const uint32_t *tabs, uint32_t npow,
+                              uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(crc_combine_kernel, dim3(1), dim3(1024), 2 * npow * sizeof(uint32_t), s, vals, n, tabs, npow,
+                       out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_finish(const uint32_t *partials, uint32_t npart, const uint8_t *src, uint64_t len,
+                             uint32_t pint, uint32_t plen, uint32_t *out3, hipStream_t s) {
+    hipLaunchKernelGGL(sum_stream_finish_kernel, dim3(1), dim3(256), 0, s, partials, npart, src, len, pint, plen,
+                       out3);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_frags(uint64_t *dst, size_t n, uint64_t frag_words, uint64_t seed, uint64_t k0,
+                             uint64_t kstep, int grid, hipStream_t s) {
+    if (n == 0 || frag_words == 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_frags_kernel, dim3(grid * 16), dim3(256), 0, s, dst, n, frag_words, seed, k0, kstep);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_stream(uint8_t *dst, size_t nbytes, uint64_t seed, uint64_t byte_off, int grid,
+                              hipStream_t s) {
+    if (nbytes == 0) return hipSuccess;
+    size_t need = (nbytes / 16 + 255) / 256;
+    size_t cap = (size_t)grid * 16;
+    int g = (int)(need < 1 ? 1 : (need < cap ? need : cap));
+    hipLaunchKernelGGL(fill_stream_kernel, dim3(g), dim3(256), 0, s, dst, nbytes, seed, byte_off);
+    return hipGetLastError();
+}
+
+}  // namespace lampi

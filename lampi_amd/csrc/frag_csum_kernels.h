@@ -1,0 +1,33 @@
+// frag_csum_kernels.h -- launchers for the gfx950 kernels in frag_csum.hip (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/lampi_csum.h"
+
+namespace lampi {
+
+// Workgroups for the persistent CRC kernel on `device` (one 1024-thread WG per CU).
+int crc_grid(int device);
+
+hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
+                           hipStream_t s);
+hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, size_t n,
+                          uint32_t *out, const uint32_t *img, int grid, hipStream_t s);
+// Regular batch: frag_len % 4096 == 0, base 16-byte aligned, n full fragments.
+hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
+                              const uint32_t *img, int grid, hipStream_t s);
+hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, int grid, hipStream_t s);
+hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out, int grid,
+                          hipStream_t s);
+hipError_t launch_crc_combine(const uint32_t *vals, uint32_t n, const uint32_t *tabs, uint32_t npow,
+                              uint32_t *out, hipStream_t s);
+hipError_t launch_sum_finish(const uint32_t *partials, uint32_t npart, const uint8_t *src, uint64_t len,
+                             uint32_t pint, uint32_t plen, uint32_t *out3, hipStream_t s);
+hipError_t launch_fill_frags(uint64_t *dst, size_t n, uint64_t frag_words, uint64_t seed, uint64_t k0,
+                             uint64_t kstep, int grid, hipStream_t s);
+hipError_t launch_fill_stream(uint8_t *dst, size_t nbytes, uint64_t seed, uint64_t byte_off, int grid,
+                              hipStream_t s);
+
+}  // namespace lampi

@@ -1,0 +1,331 @@
+// lampi_csum.cc -- C ABI of liblampi_csum.so (see include/lampi_csum.h).
+//
+// Device entry points validate their arguments, make sure the per-device table image
+// exists, and launch the gfx950 kernels on the caller's stream.  Host entry points (the
+// drop-ins for uicrc/bcopy_uicrc/uicsum/bcopy_uicsum) run the same kernels: the bytes go
+// to the GPU, the GPU computes, the checksum (and, for bcopy, the copied bytes) comes back.
+// There is no CPU checksum path in this library.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "../../include/lampi_csum.h"
+#include "crc_tables.h"
+#include "frag_csum_kernels.h"
+
+namespace lampi {
+namespace {
+
+constexpr int kMaxDevices = 64;
+
+struct DeviceTables {
+    std::once_flag once;
+    uint32_t *img = nullptr;
+    hipError_t err = hipSuccess;
+};
+DeviceTables g_tables[kMaxDevices];
+
+hipError_t current_device(int *dev) {
+    hipError_t e = hipGetDevice(dev);
+    if (e != hipSuccess) return e;
+    if (*dev < 0 || *dev >= kMaxDevices) return hipErrorInvalidDevice;
+    return hipSuccess;
+}
+
+// The table image is built on the host (GF(2) algebra, crc_tables.cc) once per process and
+// uploaded once per device; kernels stage it into LDS.
+const std::vector<uint32_t> &host_image() {
+    static const std::vector<uint32_t> img = build_table_image();
+    return img;
+}
+
+hipError_t device_tables(int dev, const uint32_t **out) {
+    DeviceTables &t = g_tables[dev];
+    std::call_once(t.once, [&] {
+        const std::vector<uint32_t> &h = host_image();
+        uint32_t *p = nullptr;
+        t.err = hipMalloc(&p, h.size() * sizeof(uint32_t));
+        if (t.err == hipSuccess) t.err = hipMemcpy(p, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if (t.err == hipSuccess) t.img = p;
+    });
+    *out = t.img;
+    return t.err;
+}
+
+int to_int(hipError_t e) { return (int)e; }
+
+// ------------------------------------------------------------------ host-path context
+[[noreturn]] void die(const char *what, hipError_t e) {
+    std::fprintf(stderr, "liblampi_csum: %s failed: %s (%d); no CPU fallback exists\n", what,
+                 hipGetErrorString(e), (int)e);
+    std::abort();
+}
+
+#define LAMPI_CHECK(call)                      \
+    do {                                       \
+        hipError_t e_ = (call);                \
+        if (e_ != hipSuccess) die(#call, e_);  \
+    } while (0)
+
+// Per-thread staging for the synchronous host entry points.
+struct HostCtx {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    uint8_t *dbuf = nullptr;
+    size_t dcap = 0;
+    uint32_t *dvals = nullptr;  // per-piece checksums + 4 result words
+    size_t vcap = 0;
+    lampi_frag_desc *ddesc = nullptr;
+    size_t desccap = 0;
+    std::vector<lampi_frag_desc> hdesc;
+    std::map<uint64_t, uint32_t *> combine_tabs;  // piece size -> device nibble tables
+};
+
+HostCtx &host_ctx() {
+    thread_local HostCtx ctx;
+    int dev = 0;
+    LAMPI_CHECK(current_device(&dev));
+    if (ctx.dev != dev) {
+        ctx = HostCtx();  // device changed: start over (old buffers belong to the old device)
+        ctx.dev = dev;
+        LAMPI_CHECK(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
+    }
+    return ctx;
+}
+
+template <class T>
+void ensure(T *&p, size_t &cap, size_t n) {
+    if (cap >= n) return;
+    if (p) LAMPI_CHECK(hipFree(p));
+    p = nullptr;
+    size_t c = std::max(n, cap * 2);
+    LAMPI_CHECK(hipMalloc(&p, c * sizeof(T)));
+    cap = c;
+}
+
+constexpr uint64_t kPieceMin = 64 * 1024;  // host path: bytes per fragment piece
+constexpr uint32_t kMaxPieces = 16384;     // combine kernel capacity (LDS ping-pong)
+
+uint64_t piece_size(uint64_t len) {
+    uint64_t b = (len + kMaxPieces - 1) / kMaxPieces;
+    b = (b + 4095) / 4096 * 4096;
+    return std::max<uint64_t>(b, kPieceMin);
+}
+
+uint32_t next_pow2(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// normal-domain nibble tables of shift by B * 2^lvl, lvl = 0..13
+uint32_t *combine_tables(HostCtx &c, uint64_t B) {
+    auto it = c.combine_tabs.find(B);
+    if (it != c.combine_tabs.end()) return it->second;
+    std::vector<uint32_t> h(14 * 128);
+    Gf2Mat m = shift_matrix(B);
+    for (int lvl = 0; lvl < 14; ++lvl) {
+        nibble_tables(m, &h[lvl * 128]);
+        m = mat_mul(m, m);
+    }
+    uint32_t *d = nullptr;
+    LAMPI_CHECK(hipMalloc(&d, h.size() * sizeof(uint32_t)));
+    LAMPI_CHECK(hipMemcpy(d, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c.combine_tabs[B] = d;
+    return d;
+}
+
+// CRC of c.dbuf[0..len) from register `partial`, computed on the GPU.
+uint32_t device_crc(HostCtx &c, uint64_t len, uint32_t partial) {
+    const uint32_t *img = nullptr;
+    LAMPI_CHECK(device_tables(c.dev, &img));
+    const int grid = crc_grid(c.dev);
+    const uint64_t B = piece_size(len);
+    const uint32_t n = (uint32_t)((len + B - 1) / B);
+    // pieces of the front-padded message: piece 0 holds the first len - (n-1)*B bytes
+    const uint64_t first = len - (uint64_t)(n - 1) * B;
+    c.hdesc.resize(n);
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint64_t off = k == 0 ? 0 : first + (uint64_t)(k - 1) * B;
+        c.hdesc[k].addr = (uint64_t)(uintptr_t)(c.dbuf + off);
+        c.hdesc[k].length = (uint32_t)(k == 0 ? first : B);
+        c.hdesc[k].partial = k == 0 ? partial : 0u;
+    }
+    ensure(c.ddesc, c.desccap, n);
+    ensure(c.dvals, c.vcap, (size_t)n + 4);
+    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc.data(), n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
+                               c.stream));
+    LAMPI_CHECK(launch_crc_desc(c.ddesc, n, c.dvals, img, grid, c.stream));
+    uint32_t *res = c.dvals;
+    if (n > 1) {
+        res = c.dvals + n;
+        LAMPI_CHECK(launch_crc_combine(c.dvals, n, combine_tables(c, B), next_pow2(n), res, c.stream));
+    }
+    uint32_t h = 0;
+    LAMPI_CHECK(hipMemcpyAsync(&h, res, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    return h;
+}
+
+// uicsum of c.dbuf[0..len) with chaining state, computed on the GPU.
+uint32_t device_sum(HostCtx &c, uint64_t len, unsigned int *pint, unsigned int *plen) {
+    const int grid = crc_grid(c.dev);
+    const uint32_t k = *plen >= 4 ? 0u : *plen;
+    const uint64_t head = k ? std::min<uint64_t>(4 - k, len) : 0;
+    const uint64_t body = (len - head) & ~3ull;
+    const uint64_t B = piece_size(body ? body : 1);
+    const uint32_t n = (uint32_t)((body + B - 1) / B);
+    c.hdesc.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        c.hdesc[i].addr = (uint64_t)(uintptr_t)(c.dbuf + head + (uint64_t)i * B);
+        c.hdesc[i].length = (uint32_t)std::min<uint64_t>(B, body - (uint64_t)i * B);
+        c.hdesc[i].partial = 0;
+    }
+    ensure(c.ddesc, c.desccap, std::max<uint32_t>(n, 1));
+    ensure(c.dvals, c.vcap, (size_t)n + 4);
+    if (n) {
+        LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc.data(), n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
+                                   c.stream));
+        LAMPI_CHECK(launch_sum_desc(c.ddesc, n, c.dvals, grid, c.stream));
+    }
+    uint32_t *out3 = c.dvals + n;
+    LAMPI_CHECK(launch_sum_finish(c.dvals, n, c.dbuf, len, *pint, *plen, out3, c.stream));
+    uint32_t h[3];
+    LAMPI_CHECK(hipMemcpyAsync(h, out3, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    *pint = h[1];
+    *plen = h[2];
+    return h[0];
+}
+
+void stage_in(HostCtx &c, const void *src, uint64_t len) {
+    ensure(c.dbuf, c.dcap, (size_t)len);
+    LAMPI_CHECK(hipMemcpyAsync(c.dbuf, src, len, hipMemcpyHostToDevice, c.stream));
+}
+
+void stage_out(HostCtx &c, void *dst, uint64_t len) {
+    if (!len) return;
+    LAMPI_CHECK(hipMemcpyAsync(dst, c.dbuf, len, hipMemcpyDeviceToHost, c.stream));
+    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+}
+
+// zero-length uicsum: no bytes, only the state convention of the reference
+// (MemFunctions.cc:1073-1222: an aligned state is reset to (0,0), a partial one is kept)
+uint32_t empty_sum(unsigned int *pint, unsigned int *plen) {
+    if (*plen == 0 || *plen >= 4) {
+        *pint = 0;
+        *plen = 0;
+    }
+    return 0;
+}
+
+}  // namespace
+}  // namespace lampi
+
+using namespace lampi;
+
+extern "C" {
+
+unsigned int lampi_uicrc(const void *src, unsigned long crclen, unsigned int partial_crc) {
+    if (crclen == 0) return partial_crc;  // no bytes: the register is unchanged
+    HostCtx &c = host_ctx();
+    stage_in(c, src, crclen);
+    return device_crc(c, crclen, partial_crc);
+}
+
+unsigned int lampi_bcopy_uicrc(const void *src, void *dst, unsigned long copylen, unsigned long crclen,
+                               unsigned int partial_crc) {
+    const uint64_t n = std::max<uint64_t>(copylen, crclen);
+    if (n == 0) return partial_crc;
+    HostCtx &c = host_ctx();
+    stage_in(c, src, n);
+    const uint32_t r = device_crc(c, n, partial_crc);
+    stage_out(c, dst, copylen);
+    return r;
+}
+
+unsigned int lampi_uicsum(const void *src, unsigned long csumlen, unsigned int *pint, unsigned int *plen) {
+    if (csumlen == 0) return empty_sum(pint, plen);
+    HostCtx &c = host_ctx();
+    stage_in(c, src, csumlen);
+    return device_sum(c, csumlen, pint, plen);
+}
+
+unsigned int lampi_bcopy_uicsum(const void *src, void *dst, unsigned long copylen, unsigned long csumlen,
+                                unsigned int *pint, unsigned int *plen) {
+    const uint64_t n = std::max<uint64_t>(copylen, csumlen);
+    if (n == 0) return empty_sum(pint, plen);
+    HostCtx &c = host_ctx();
+    stage_in(c, src, n);
+    const uint32_t r = device_sum(c, n, pint, plen);
+    stage_out(c, dst, copylen);
+    return r;
+}
+
+int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (n == 0) return 0;
+    if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    hipStream_t s = (hipStream_t)stream;
+    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_desc(d_descs, n, d_out, crc_grid(dev), s));
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s));
+}
+
+int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t partial, uint32_t *d_out, int mode,
+                   void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (frag_len == 0 || frag_len > 0xFFFFFFFFull || !d_out || (msg_len && !d_msg))
+        return to_int(hipErrorInvalidValue);
+    // a zero-length message is one empty fragment (the path layer still sends a header)
+    const size_t n = msg_len ? (msg_len + frag_len - 1) / frag_len : 1;
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    hipStream_t s = (hipStream_t)stream;
+    const uint8_t *base = (const uint8_t *)d_msg;
+    const int grid = crc_grid(dev);
+    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_msg(base, msg_len, frag_len, n, d_out, grid, s));
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    const bool regular = msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 &&
+                         ((uintptr_t)base & 15u) == 0;
+    if (regular) return to_int(launch_crc_regular(base, n, frag_len, partial, d_out, img, grid, s));
+    return to_int(launch_crc_msg(base, msg_len, frag_len, partial, n, d_out, img, grid, s));
+}
+
+int lampi_fill_stream(void *d_dst, size_t nbytes, uint64_t seed, uint64_t byte_off, void *stream) {
+    if (nbytes == 0) return 0;
+    if (!d_dst) return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_fill_stream((uint8_t *)d_dst, nbytes, seed, byte_off, crc_grid(dev), (hipStream_t)stream));
+}
+
+int lampi_fill_stream_frags(void *d_dst, size_t n, size_t frag_len, uint64_t seed, uint64_t k0, uint64_t kstep,
+                            void *stream) {
+    if (n == 0) return 0;
+    if (!d_dst || frag_len == 0 || frag_len % 8 != 0 || ((uintptr_t)d_dst & 7u)) return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_fill_frags((uint64_t *)d_dst, n, frag_len / 8, seed, k0, kstep, crc_grid(dev),
+                                    (hipStream_t)stream));
+}
+
+const char *lampi_csum_version(void) { return "lampi-frag-csum 0.1 (gfx950, CDNA4)"; }
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+"""Device-resident batched checksums over torch CUDA tensors (HIP on ROCm).
+
+PyTorch is only plumbing here: it owns HBM buffers and streams.  Every checksum is
+computed by the gfx950 kernels behind the C ABI (lampi_frag_csum_batch, lampi_msg_csum).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ._lib import CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
+
+__all__ = ["CRC32", "SUM32", "frag_csum_batch", "msg_csum", "fill_stream", "fill_stream_frags", "make_descs",
+           "as_u32"]
+
+
+def _stream_handle(stream: torch.cuda.Stream | None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _require_cuda(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{what} must be a device (cuda) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{what} must be contiguous")
+
+
+def as_u32(t: torch.Tensor) -> np.ndarray:
+    """Checksum tensor (int32 storage) -> numpy uint32 on the host."""
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+def make_descs(base: torch.Tensor, offsets, lengths, partials=None) -> torch.Tensor:
+    """Build a device array of ``lampi_frag_desc`` (n x 16 bytes, int64 [n, 2] storage)."""
+    _require_cuda(base, "base")
+    off = np.asarray(offsets, dtype=np.uint64)
+    ln = np.asarray(lengths, dtype=np.uint64)
+    n = off.size
+    if ln.size != n:
+        raise ValueError("offsets and lengths differ in size")
+    if n and int((off + ln).max()) > base.numel() * base.element_size():
+        raise ValueError("a fragment extends past the end of the base tensor")
+    if n and int(ln.max()) > 0xFFFFFFFF:
+        raise ValueError("fragment length exceeds 32 bits")
+    pt = (np.full(n, CRC_INITIAL_REGISTER, dtype=np.uint64) if partials is None
+          else np.asarray(partials, dtype=np.uint64) & 0xFFFFFFFF)
+    host = np.empty((n, 2), dtype=np.uint64)
+    host[:, 0] = np.uint64(base.data_ptr()) + off
+    host[:, 1] = ln | (pt << np.uint64(32))
+    return torch.from_numpy(host.view(np.int64)).to(base.device)
+
+
+def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
+                    stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """out[i] = checksum of fragment descs[i]; one wavefront per fragment."""
+    _require_cuda(descs, "descs")
+    count = descs.numel() * descs.element_size() // 16 if n is None else int(n)
+    if out is None:
+        out = torch.empty(count, dtype=torch.int32, device=descs.device)
+    _require_cuda(out, "out")
+    if out.numel() < count:
+        raise ValueError("out is too small")
+    check(lib().lampi_frag_csum_batch(descs.data_ptr(), count, out.data_ptr(), mode, _stream_handle(stream)),
+          "lampi_frag_csum_batch")
+    return out
+
+
+def msg_csum(msg: torch.Tensor, frag_len: int, partial: int = CRC_INITIAL_REGISTER, mode: int = CRC32,
+             msg_len: int | None = None, out: torch.Tensor | None = None,
+             stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Checksums of the fragments of a contiguous device message (src/path/gm/path.cc:98-121)."""
+    _require_cuda(msg, "msg")
+    nbytes = msg.numel() * msg.element_size() if msg_len is None else int(msg_len)
+    if nbytes > msg.numel() * msg.element_size():
+        raise ValueError("msg_len exceeds the tensor")
+    n = (nbytes + frag_len - 1) // frag_len if nbytes else 1
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=msg.device)
+    _require_cuda(out, "out")
+    if out.numel() < n:
+        raise ValueError("out is too small")
+    check(lib().lampi_msg_csum(msg.data_ptr(), nbytes, frag_len, partial & 0xFFFFFFFF, out.data_ptr(), mode,
+                               _stream_handle(stream)), "lampi_msg_csum")
+    return out
+
+
+def fill_stream(dst: torch.Tensor, seed: int, byte_off: int = 0, nbytes: int | None = None,
+                stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Write the SURVEY.md 8(d) synthetic stream (splitmix64 words, LE) into ``dst`` on device."""
+    _require_cuda(dst, "dst")
+    n = dst.numel() * dst.element_size() if nbytes is None else int(nbytes)
+    check(lib().lampi_fill_stream(dst.data_ptr(), n, seed & (2**64 - 1), byte_off, _stream_handle(stream)),
+          "lampi_fill_stream")
+    return dst
+
+
+def fill_stream_frags(dst: torch.Tensor, n: int, frag_len: int, seed: int, k0: int = 0, kstep: int = 1,
+                      stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Round-robin shard of a global batch: fragment i of ``dst`` = global fragment k0 + i*kstep."""
+    _require_cuda(dst, "dst")
+    if n * frag_len > dst.numel() * dst.element_size():
+        raise ValueError("dst is too small")
+    check(lib().lampi_fill_stream_frags(dst.data_ptr(), n, frag_len, seed & (2**64 - 1), k0, kstep,
+                                        _stream_handle(stream)), "lampi_fill_stream_frags")
+    return dst

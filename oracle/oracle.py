@@ -1,0 +1,187 @@
+"""oracle.py -- ctypes access to the TEST-ONLY checkers.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product (lampi_amd/).
+
+* :class:`Restatement` -- oracle/libcsum_ref.so, the clean-room C restatement (csum_ref.c).
+  Travels to the GPU box; it is the parity checker there and the timed CPU baseline.
+* :class:`Reference` -- oracle/_ref/libref_memfunctions.so, the reference's own
+  src/util/MemFunctions.cc compiled unmodified (oracle/Makefile).  Exists only where
+  /root/reference was present at build time; bound by the C++ mangled names of
+  SURVEY.md 8(b).
+
+Parity status: pinned (tests/golden/ fixtures generated from Reference, checked against
+Restatement by tests/test_oracle.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+RESTATEMENT_SO = os.path.join(HERE, "libcsum_ref.so")
+REFERENCE_SO = os.path.join(HERE, "_ref", "libref_memfunctions.so")
+
+CRC_INIT = 0xFFFFFFFF
+_u = ctypes.c_uint
+_ul = ctypes.c_ulong
+_vp = ctypes.c_void_p
+_pu = ctypes.POINTER(ctypes.c_uint)
+
+
+def _buf(b):
+    arr = np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray) else b.view(np.uint8).reshape(-1)
+    return arr.ctypes.data, arr
+
+
+class _Api:
+    """Common Python surface: uicrc / bcopy_uicrc / uicsum / bcopy_uicsum."""
+
+    def uicrc(self, data, n=None, partial=CRC_INIT):
+        p, a = _buf(data)
+        return int(self._uicrc(p, a.size if n is None else n, partial & 0xFFFFFFFF))
+
+    def bcopy_uicrc(self, src, dst, copylen, crclen, partial=CRC_INIT):
+        ps, _ = _buf(src)
+        pd, _ = _buf(dst)
+        return int(self._bcopy_uicrc(ps, pd, copylen, crclen, partial & 0xFFFFFFFF))
+
+    def uicsum(self, data, n=None, pint=0, plen=0):
+        """Returns (sum_increment, pint', plen')."""
+        p, a = _buf(data)
+        pi, pl = _u(pint), _u(plen)
+        r = self._uicsum(p, a.size if n is None else n, ctypes.byref(pi), ctypes.byref(pl))
+        return int(r), pi.value, pl.value
+
+    def bcopy_uicsum(self, src, dst, copylen, csumlen, pint=0, plen=0):
+        ps, _ = _buf(src)
+        pd, _ = _buf(dst)
+        pi, pl = _u(pint), _u(plen)
+        r = self._bcopy_uicsum(ps, pd, copylen, csumlen, ctypes.byref(pi), ctypes.byref(pl))
+        return int(r), pi.value, pl.value
+
+
+class Restatement(_Api):
+    def __init__(self, path: str = RESTATEMENT_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        L = ctypes.CDLL(path)
+        self.lib = L
+        self._uicrc = L.oracle_uicrc
+        self._uicrc.restype, self._uicrc.argtypes = _u, [_vp, ctypes.c_size_t, _u]
+        self._bcopy_uicrc = L.oracle_bcopy_uicrc
+        self._bcopy_uicrc.restype = _u
+        self._bcopy_uicrc.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _u]
+        self._uicsum = L.oracle_uicsum
+        self._uicsum.restype, self._uicsum.argtypes = _u, [_vp, ctypes.c_size_t, _pu, _pu]
+        self._bcopy_uicsum = L.oracle_bcopy_uicsum
+        self._bcopy_uicsum.restype = _u
+        self._bcopy_uicsum.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _pu, _pu]
+        L.oracle_fill_stream.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t]
+        L.oracle_uniform_batch.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_size_t,
+                                           ctypes.c_int, ctypes.c_int, _vp]
+        L.oracle_uniform_digest.argtypes = [ctypes.c_uint64, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp]
+        L.oracle_desc_batch.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _vp]
+        L.oracle_time_uniform.restype = ctypes.c_double
+        L.oracle_time_uniform.argtypes = [ctypes.c_uint64, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.c_int, _vp]
+        L.oracle_time_fn.restype = ctypes.c_double
+        L.oracle_time_fn.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, _vp]
+        L.oracle_header_checksum.restype = _u
+        L.oracle_header_checksum.argtypes = [_vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+
+    # ---- batch helpers -------------------------------------------------------------
+    def stream(self, seed: int, byte_off: int, n: int) -> np.ndarray:
+        out = np.empty(n, dtype=np.uint8)
+        self.lib.oracle_fill_stream(out.ctypes.data, seed, byte_off, n)
+        return out
+
+    def uniform_batch(self, seed: int, k0: int, n: int, L: int, mode: int, nthreads: int = 0) -> np.ndarray:
+        out = np.empty(n, dtype=np.uint32)
+        self.lib.oracle_uniform_batch(seed, k0, n, L, mode, nthreads, out.ctypes.data)
+        return out
+
+    def uniform_digest(self, seed: int, n: int, L: int, mode: int, nshard: int = 1, shard: int = 0,
+                       nthreads: int = 0) -> tuple[int, int]:
+        dig = np.zeros(2, dtype=np.uint32)
+        self.lib.oracle_uniform_digest(seed, n, L, mode, nshard, shard, nthreads, dig.ctypes.data)
+        return int(dig[0]), int(dig[1])
+
+    def desc_batch(self, base: np.ndarray, offsets, lengths, partials=None, mode: int = 0,
+                   nthreads: int = 0) -> np.ndarray:
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        pt = None if partials is None else np.ascontiguousarray(partials, dtype=np.uint32)
+        out = np.empty(off.size, dtype=np.uint32)
+        self.lib.oracle_desc_batch(base.ctypes.data, off.ctypes.data, ln.ctypes.data,
+                                   None if pt is None else pt.ctypes.data, off.size, mode, nthreads,
+                                   out.ctypes.data)
+        return out
+
+    def time_uniform(self, seed: int, n: int, L: int, mode: int, nthreads: int) -> tuple[float, int]:
+        x = ctypes.c_uint(0)
+        t = self.lib.oracle_time_uniform(seed, n, L, mode, nthreads, ctypes.byref(x))
+        return float(t), x.value
+
+    def time_crc_fn(self, fn_addr: int, buf: np.ndarray, n: int, L: int, nthreads: int) -> tuple[float, int]:
+        """Seconds for `fn` (uicrc-shaped C function address) over n fragments of L bytes."""
+        x = ctypes.c_uint(0)
+        t = self.lib.oracle_time_fn(fn_addr, buf.ctypes.data, n, L, nthreads, ctypes.byref(x))
+        return float(t), x.value
+
+    def uicrc_addr(self) -> int:
+        return ctypes.cast(self.lib.oracle_uicrc, ctypes.c_void_p).value
+
+    def header_checksum(self, hdr, crclen: int, word_count: int, usecrc: bool) -> int:
+        p, _ = _buf(hdr)
+        return int(self.lib.oracle_header_checksum(p, crclen, word_count, 1 if usecrc else 0))
+
+
+class Reference(_Api):
+    """The reference's MemFunctions.cc, compiled unmodified (C++ linkage, mangled names)."""
+
+    def uicrc_addr(self) -> int:
+        return ctypes.cast(self._uicrc, ctypes.c_void_p).value
+
+    def __init__(self, path: str = REFERENCE_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing (built only where /root/reference exists)")
+        L = ctypes.CDLL(path)
+        self.lib = L
+        self._uicrc = getattr(L, "_Z5uicrcPKvmj")
+        self._uicrc.restype, self._uicrc.argtypes = _u, [_vp, _ul, _u]
+        self._bcopy_uicrc = getattr(L, "_Z11bcopy_uicrcPKvPvmmj")
+        self._bcopy_uicrc.restype, self._bcopy_uicrc.argtypes = _u, [_vp, _vp, _ul, _ul, _u]
+        self._uicsum = getattr(L, "_Z6uicsumPKvmPjS1_")
+        self._uicsum.restype, self._uicsum.argtypes = _u, [_vp, _ul, _pu, _pu]
+        self._bcopy_uicsum = getattr(L, "_Z12bcopy_uicsumPKvPvmmPjS2_")
+        self._bcopy_uicsum.restype, self._bcopy_uicsum.argtypes = _u, [_vp, _vp, _ul, _ul, _pu, _pu]
+
+
+def splitmix_stream(seed: int, byte_off: int, n: int) -> np.ndarray:
+    """numpy generator of the SURVEY.md 8(d) stream (same bytes as oracle_fill_stream)."""
+    w0 = byte_off // 8
+    w1 = (byte_off + n + 7) // 8
+    idx = np.arange(w0, w1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (idx + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z ^= z >> np.uint64(30)
+        z *= np.uint64(0xBF58476D1CE4E5B9)
+        z ^= z >> np.uint64(27)
+        z *= np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    b = z.view(np.uint8)
+    s = byte_off - 8 * w0
+    return b[s:s + n].copy()
+
+
+def digest(vals: np.ndarray, k_index: np.ndarray | None = None) -> tuple[int, int]:
+    """(XOR, sum c_k*(2k+1) mod 2^32) of per-fragment checksums."""
+    v = np.asarray(vals, dtype=np.uint64)
+    k = np.arange(v.size, dtype=np.uint64) if k_index is None else np.asarray(k_index, dtype=np.uint64)
+    x = int(np.bitwise_xor.reduce(v.astype(np.uint32))) if v.size else 0
+    s = int(((v * (2 * k + 1)) & np.uint64(0xFFFFFFFF)).sum() & 0xFFFFFFFF) if v.size else 0
+    return x, s

@@ -1,0 +1,226 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) vs the oracle, bit-exact.
+
+Sizes the oracle finishes in seconds are compared fragment by fragment; the BASELINE
+config B (4M x 4 KiB, 16 GiB device-resident) is compared through its committed digests
+(computed by the reference-pinned oracle).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EDGE_LENS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 63, 64, 65, 127, 1023, 1024, 1025, 1976, 2047, 2048, 4092,
+             4095, 4096, 4097, 8191, 8192, 12288, 16383, 16384, 16385, 65455, 65456, 65536]
+
+
+def _dv():
+    from lampi_amd import device as dv
+
+    return dv
+
+
+def test_stream_generator_matches_oracle(cuda, oracle):
+    import torch
+
+    dv = _dv()
+    for seed, off, n in [(2, 0, 1 << 16), (7, 13, 99999), (1, 5, 17)]:
+        t = torch.empty(n, dtype=torch.uint8, device=cuda)
+        dv.fill_stream(t, seed, byte_off=off)
+        assert np.array_equal(t.cpu().numpy(), oracle.stream(seed, off, n))
+    t = torch.empty(6 * 4096, dtype=torch.uint8, device=cuda)
+    dv.fill_stream_frags(t, 6, 4096, seed=3, k0=5, kstep=8)
+    want = np.concatenate([oracle.stream(3, (5 + 8 * i) * 4096, 4096) for i in range(6)])
+    assert np.array_equal(t.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("L", [64, 1024, 1976, 4096, 16384, 65456])
+def test_uniform_batches(cuda, oracle, mode, L):
+    import torch
+
+    dv = _dv()
+    n = max(8, (8 << 20) // L)
+    buf = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=2)
+    got = dv.as_u32(dv.msg_csum(buf, L, mode=mode))
+    want = oracle.uniform_batch(2, 0, n, L, mode)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_message_with_short_last_fragment(cuda, oracle, mode):
+    import torch
+
+    dv = _dv()
+    for msg_len, L in [(1 << 20, 65456), (1000003, 4096), (5, 4096), (4096 * 7 + 1, 4096)]:
+        buf = torch.empty(msg_len, dtype=torch.uint8, device=cuda)
+        dv.fill_stream(buf, seed=11)
+        got = dv.as_u32(dv.msg_csum(buf, L, partial=0x12345678, mode=mode))
+        host = buf.cpu().numpy()
+        nf = (msg_len + L - 1) // L
+        offs = np.arange(nf, dtype=np.uint64) * L
+        lens = np.minimum(L, msg_len - offs.astype(np.int64)).astype(np.uint32)
+        want = oracle.desc_batch(host, offs, lens, np.full(nf, 0x12345678, np.uint32) if mode == 0 else None, mode)
+        assert np.array_equal(got, want), (msg_len, L)
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_descriptor_batch_edges_and_alignment(cuda, oracle, mode):
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(1234)
+    base = torch.empty(4 << 20, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=21)
+    host = base.cpu().numpy()
+    lens, offs = [], []
+    for L in EDGE_LENS:
+        for a in range(0, 17):  # every alignment mod 16 plus one
+            lens.append(L)
+            offs.append(int(rng.integers(0, (4 << 20) - 70000)) // 64 * 64 + a)
+    lens = np.array(lens, dtype=np.uint64)
+    offs = np.array(offs, dtype=np.uint64)
+    parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
+    parts[::3] = 0xFFFFFFFF
+    descs = dv.make_descs(base, offs, lens, parts)
+    got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
+    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+
+
+def test_descriptor_batch_random(cuda, oracle):
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(99)
+    base = torch.empty(64 << 20, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=33)
+    host = base.cpu().numpy()
+    n = 20000
+    lens = rng.integers(0, 70000, size=n).astype(np.uint64)
+    offs = rng.integers(0, (64 << 20) - 70000, size=n).astype(np.uint64)
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    descs = dv.make_descs(base, offs, lens, parts)
+    for mode in (0, 1):
+        got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
+        want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
+        assert np.array_equal(got, want)
+
+
+def test_kat_check_values(cuda):
+    import torch
+
+    dv = _dv()
+    t = torch.tensor(list(b"123456789"), dtype=torch.uint8, device=cuda)
+    assert dv.as_u32(dv.msg_csum(t, 4096))[0] == 0x0376E6E7
+    assert dv.as_u32(dv.msg_csum(t, 4096, mode=dv.SUM32))[0] == 0x6C6A689F
+    z = torch.zeros(65536, dtype=torch.uint8, device=cuda)
+    assert dv.as_u32(dv.msg_csum(z, 65536))[0] == 0x288E1614  # uicrc(Z, 65536)
+    f = torch.full((4096,), 0xFF, dtype=torch.uint8, device=cuda)
+    assert dv.as_u32(dv.msg_csum(f, 4096))[0] == 0xAF19D570
+    r = torch.arange(1976, dtype=torch.int32, device=cuda).to(torch.uint8)
+    assert dv.as_u32(dv.msg_csum(r, 1976))[0] == 0x092CD62F
+    assert dv.as_u32(dv.msg_csum(r, 1976, mode=dv.SUM32))[0] == 0x677786AC
+
+
+def test_config_b_full_digest(cuda):
+    """BASELINE config B: 4M x 4 KiB device-resident; digests from BASELINE.md."""
+    import torch
+
+    from oracle.oracle import digest
+
+    dv = _dv()
+    n, L = 4194304, 4096
+    buf = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=2)
+    crc = dv.as_u32(dv.msg_csum(buf, L))
+    assert [f"{v:08x}" for v in crc[:4]] == ["9aff1c82", "cf9217cf", "84a13b32", "66922667"]
+    assert digest(crc) == (0x959621BB, 0xC38D8899)
+    s = dv.as_u32(dv.msg_csum(buf, L, mode=dv.SUM32))
+    sx = int(np.sum(s, dtype=np.uint64) & 0xFFFFFFFF)
+    assert (sx, digest(s)[1]) == (0x190D78D3, 0x88569035)
+    del buf
+    torch.cuda.empty_cache()
+
+
+def test_config_d_shard_digest_sample(cuda, oracle):
+    """Config D layout (16 KiB fragments, GPU g owns k = g mod 8): a 1 GiB slice of shard 3."""
+    import torch
+
+    dv = _dv()
+    n, L, g = 65536, 16384, 3
+    buf = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    dv.fill_stream_frags(buf, n, L, seed=3, k0=g, kstep=8)
+    got = dv.as_u32(dv.msg_csum(buf, L))
+    idx = np.r_[0:256, n - 256:n]
+    want = np.array([oracle.uniform_batch(3, g + 8 * int(i), 1, L, 0)[0] for i in idx], dtype=np.uint32)
+    assert np.array_equal(got[idx], want)
+    if g == 3:
+        assert got[0] == oracle.uniform_batch(3, 3, 1, L, 0)[0]
+
+
+def test_host_api_matches_reference_semantics(cuda, oracle):
+    """lampi_amd.memfunctions (host entry points, computed on the GPU) vs the oracle."""
+    import lampi_amd as la
+
+    rng = np.random.default_rng(7)
+    data = rng.integers(0, 256, size=3 << 20, dtype=np.uint8)
+    for n in [0, 1, 3, 4, 5, 100, 4096, 65456, 65537, 1 << 20, (3 << 20) - 5]:
+        for off in (0, 1, 3):
+            src = data[off:off + n]
+            p = int(rng.integers(0, 2**32))
+            assert la.uicrc(src, n, p) == oracle.uicrc(src, n, p)
+            assert la.uicrc(src, n) == oracle.uicrc(src, n)
+            for plen in (0, 1, 2, 3):
+                pint = int(rng.integers(0, 2**32)) & ((1 << (8 * plen)) - 1)
+                st = la.PartialState(pint, plen)
+                got = la.uicsum(src, n, st)
+                want = oracle.uicsum(src, n, pint, plen)
+                assert (got, st.pint, st.plen) == want, (n, off, plen)
+    # bcopy with copylen < crclen, = and >
+    src = data[:200000]
+    for copylen, clen in [(100, 100), (50, 100), (100, 50), (0, 77), (65456, 65456), (70000, 100000)]:
+        d1 = np.zeros(200000, np.uint8)
+        d2 = np.zeros(200000, np.uint8)
+        assert la.bcopy_uicrc(src, d1, copylen, clen) == oracle.bcopy_uicrc(src, d2, copylen, clen)
+        assert np.array_equal(d1, d2)
+        st = la.PartialState()
+        got = la.bcopy_uicsum(src, d1, copylen, clen, st)
+        assert (got, st.pint, st.plen) == oracle.bcopy_uicsum(src, d2, copylen, clen)
+        assert np.array_equal(d1, d2)
+
+
+def test_host_api_chaining(cuda, oracle):
+    """Chained pieces (the non-contiguous typemap pattern, src/path/gm/sendFrag.cc:157-217)."""
+    import lampi_amd as la
+
+    rng = np.random.default_rng(3)
+    msg = rng.integers(0, 256, size=300000, dtype=np.uint8)
+    for _ in range(20):
+        cuts = np.sort(rng.integers(0, msg.size, size=int(rng.integers(1, 8))))
+        pieces = np.split(msg, cuts)
+        crc = la.CRC_INITIAL_REGISTER
+        total = 0
+        st = la.PartialState()
+        for p in pieces:
+            crc = la.uicrc(p, p.size, crc)
+            total = (total + la.uicsum(p, p.size, st)) & 0xFFFFFFFF
+        assert crc == oracle.uicrc(msg)
+        assert total == oracle.uicsum(msg)[0]
+
+
+def test_header_checksum_residue(cuda, oracle):
+    """CRC(header || stored headerChecksum) == 0 (receiver check, src/path/gm/path.cc:379-384)."""
+    import lampi_amd as la
+
+    rng = np.random.default_rng(8)
+    for hl, words in ((72, 18), (128, 32)):
+        for _ in range(5):
+            hdr = rng.integers(0, 256, size=hl, dtype=np.uint8)
+            c = la.header_checksum(hdr, hl - 4, words, usecrc=True)
+            assert c == oracle.header_checksum(hdr, hl - 4, words, True)
+            hdr[hl - 4:] = np.frombuffer(c.to_bytes(4, "little"), np.uint8)
+            assert la.uicrc(hdr, hl) == 0
+            assert la.header_checksum(hdr, hl - 4, words, usecrc=False) == oracle.header_checksum(
+                hdr, hl - 4, words, False)

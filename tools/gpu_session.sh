@@ -1,0 +1,44 @@
+#!/usr/bin/env bash
+# tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
+# Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
+#   smoke | tests | bench | prof | pmc | e2e | bench16k | microbench
+# A test failure (exit 1) lets later steps run; a fault, abort, segfault, timeout or
+# kill (exit >= 124, 134, 139, ...) ends the session immediately.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name exit=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then
+    echo "!!! $name ended with $rc: stopping the session"
+    exit $rc
+  fi
+  return 0
+}
+
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    bench) run bench 600 python bench.py ;;
+    bench16k) run bench16k 600 python bench.py --frags 1048576 --frag-bytes 16384 --no-cpu-baseline ;;
+    benchsum) run benchsum 600 python bench.py --mode sum --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
+            -- python3 bench.py --steps 10 --no-cpu-baseline ;;
+    pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \
+            -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline &&
+         run pmc_ea 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv \
+            -d gpurun_out/pmc_ea -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    e2e) run e2e 600 python bench.py --e2e ;;
+    microbench) run microbench 300 tools/microbench/readbw ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "=== session done"
