@@ -69,33 +69,37 @@ void nibble_tables(const Gf2Mat &ms, uint32_t out[128]) {
         for (uint32_t v = 0; v < 16; ++v) out[p * 16 + v] = ms.apply(v << (4 * p));
 }
 
-std::vector<uint32_t> build_table_image() {
+void slice_tables(uint32_t S[4][256]) {
     const uint32_t *T = sarwate_table();
-    std::vector<uint32_t> img(kImgWords, 0);
-
-    // per-lane final shift: lane l's last byte sits 64*(63-l) bytes before the row end
-    const Gf2Mat step = shift_matrix(kLaneBytes);
-    Gf2Mat m = mat_identity();  // m = shift by 64*(63-l), built from l = 63 downwards
-    for (int l = kWave - 1; l >= 0; --l) {
-        uint32_t nt[128];
-        nibble_tables(swapped(m), nt);
-        for (int p = 0; p < 8; ++p)
-            for (int v = 0; v < 16; ++v) img[kImgCombine + p * 1024 + v * 64 + l] = nt[p * 16 + v];
-        m = mat_mul(step, m);
-    }
-
-    // Horner step between rows: the next 64-byte piece of a lane starts 4032 bytes later
-    nibble_tables(swapped(shift_matrix(kRowBytes - kLaneBytes)), &img[kImgHorner]);
-
-    // slicing-by-4 in the swapped domain: for X = C ^ w (w = LE load),
-    //   C' = S_0[X.b0] ^ S_1[X.b1] ^ S_2[X.b2] ^ S_3[X.b3],  S_j = bswap(T_{3-j})
     uint32_t Tk[4][256];
     for (int i = 0; i < 256; ++i) {
         Tk[0][i] = T[i];
         for (int k = 1; k < 4; ++k) Tk[k][i] = zero_byte(Tk[k - 1][i]);
     }
     for (int j = 0; j < 4; ++j)
-        for (int i = 0; i < 256; ++i) img[kImgSlice + j * 256 + i] = bswap32(Tk[3 - j][i]);
+        for (int i = 0; i < 256; ++i) S[j][i] = bswap32(Tk[3 - j][i]);
+}
+
+std::vector<uint32_t> build_table_image() {
+    std::vector<uint32_t> img(kImgWords, 0);
+
+    uint32_t S[4][256];
+    slice_tables(S);
+    for (int i = 0; i < 256; ++i)
+        for (int j = 0; j < 4; ++j) img[kImgSliceT + 4 * i + j] = S[j][i];
+
+    // per-lane final shift: lane l's last byte sits 64*(63-l) bytes before the row end
+    const Gf2Mat step = shift_matrix(kLaneBytes);
+    Gf2Mat m = mat_identity();  // shift by 64*(63-l), built from l = 63 downwards
+    for (int l = kWave - 1; l >= 0; --l) {
+        const Gf2Mat ms = swapped(m);
+        for (int b = 0; b < 32; ++b) img[kImgCombineCols + l * 32 + b] = ms.col[b];
+        m = mat_mul(step, m);
+    }
+
+    // Horner step between rows: the next 64-byte piece of a lane starts 4032 bytes later
+    const Gf2Mat h = swapped(shift_matrix(kRowBytes - kLaneBytes));
+    for (int b = 0; b < 32; ++b) img[kImgHornerCols + b] = h.col[b];
     return img;
 }
 

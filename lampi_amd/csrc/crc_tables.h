@@ -25,16 +25,17 @@ constexpr int kWave = 64;
 constexpr int kLaneBytes = 64;
 constexpr int kRowBytes = kWave * kLaneBytes;  // 4096
 
-// Layout of the device table image (u32 words) -- copied into LDS by the kernels.
-//   [kImgCombine, +8192)  per-lane final shift by 64*(63-l) bytes, nibble tables,
-//                         word index p*1024 + v*64 + l  (LDS byte addr p*4096 + v*256 + 4l:
-//                         lane l always hits bank l%32 -> conflict free)
-//   [kImgHorner, +128)    shift by kRowBytes-kLaneBytes (4032) bytes, p*16 + v
-//   [kImgSlice, +1024)    slicing-by-4 tables S_j[i] at j*256 + i (replicated in LDS)
-constexpr size_t kImgCombine = 0;
-constexpr size_t kImgHorner = 8192;
-constexpr size_t kImgSlice = 8192 + 128;
-constexpr size_t kImgWords = 8192 + 128 + 1024;
+// Layout of the device basis image (u32 words); each workgroup expands it into its LDS
+// tables (frag_csum.hip, stage_tables):
+//   [kImgSliceT, +1024)      slicing-by-4 tables transposed: word 4i + j = S_j[i]
+//   [kImgCombineCols, +2048) per-lane final shift by 64*(63-l) bytes (swapped domain), as
+//                            matrix columns: word l*32 + b = M_l(1 << b)
+//   [kImgHornerCols, +32)    shift by kRowBytes - kLaneBytes = 4032 bytes, columns b
+// Nibble tables are XORs of four columns: M(v << 4p) = XOR_{bit b of v} col[4p + b].
+constexpr size_t kImgSliceT = 0;
+constexpr size_t kImgCombineCols = 1024;
+constexpr size_t kImgHornerCols = 1024 + 2048;
+constexpr size_t kImgWords = 1024 + 2048 + 32;
 
 inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -60,7 +61,11 @@ uint32_t crc_bytes(uint32_t crc, const uint8_t *p, size_t n);  // host scalar (t
 // Nibble tables of a swapped-domain linear map m: out[p*16 + v] = m(v << 4p).
 void nibble_tables(const Gf2Mat &m_swapped, uint32_t out[128]);
 
-// Full device table image, kImgWords words.
+// Slicing tables S_j[i], j = 0..3 (swapped domain): for X = C ^ w (w a little-endian
+// 32-bit load), C' = S_0[X.b0] ^ S_1[X.b1] ^ S_2[X.b2] ^ S_3[X.b3].
+void slice_tables(uint32_t S[4][256]);
+
+// Device basis image, kImgWords words.
 std::vector<uint32_t> build_table_image();
 
 }  // namespace lampi

@@ -12,13 +12,25 @@
 //     register, table lookups in LDS addressed by one v_perm each.
 //   * Between rows a lane's register jumps 4032 zero bytes (nibble-table shift, Horner).
 //   * At the end lane l applies its own shift by 64*(63-l) bytes (per-lane nibble
-//     tables, conflict-free) and the 64 registers are XOR-reduced across the wave.
-//   LDS (one 1024-thread workgroup per CU, persistent over fragments):
-//     [0, 32768)      per-lane combine tables  p*4096 + v*256 + 4l   (bank = l % 32)
-//     [32768, 33280)  Horner shift tables      p*64 + 4v             (16 banks, broadcast)
-//     [33280, 98816)  slicing tables, 16 copies: entry i of S_j, copy c at
-//                     i*256 + j*64 + 4c.  Lanes 0-15 and 16-31 of a ds_read_b32 group
-//                     read tables of opposite parity -> 32 distinct banks, no conflicts.
+//     tables, conflict-free) and the 64 registers are XOR-reduced across the wave (DPP).
+//
+// Scheduling (measured, tools/microbench/readocc.hip, readdyn.hip, crc_sched.hip): HBM reads
+// run fastest when the chip sweeps memory as one compact window in address order.  So the
+// grid is NOT persistent: 256-thread workgroups (4 waves) each own 4*fpw consecutive
+// fragments and wave w takes fragments w, w+4, w+8, ...; the hardware dispatcher keeps the
+// window compact and balances the load.  Persistent grids (static or atomic work queues)
+// and 512/1024-thread workgroups measured 3-10% slower on raw reads.
+//
+// LDS (66048 B per workgroup -> two workgroups per CU), tables built per workgroup from a
+// 12 KiB basis image (crc_tables.cc):
+//   row e = 0..255 at e*256:
+//     [0,128)    slicing tables, entry e of S_j, copy c = 0..7 at j*32 + 4c.  Lane octet g
+//                (lanes 8g..8g+7 of a 32-lane ds_read_b32 group) reads table q^g in
+//                instruction q -> 32 distinct banks, conflict-free; one v_perm forms the
+//                address (byte0 = j*32+4c, byte1 = byte j of X).
+//     [128,256)  per-lane combine tables: (p*16 + v)*2 + (l >> 5) is the row, lane l & 31
+//                the word -> bank l % 32, conflict-free.
+//   [65536, 66048)  Horner nibble tables (shift by 4032 bytes), p*64 + 4v (broadcast reads).
 //
 // SUM mode (uicsum, ref MemFunctions.cc:1073-1222): left-aligned rows, lane-contiguous
 // 64-byte pieces, funnel-shifted to the fragment's own word grid, zero-padded tail,
@@ -33,11 +45,10 @@ namespace lampi {
 
 namespace {
 
-constexpr uint32_t kLdsCombine = 0;
-constexpr uint32_t kLdsHorner = 32768;
-constexpr uint32_t kLdsSlice = 33280;
-constexpr uint32_t kLdsBytes = 33280 + 65536;
-constexpr int kBlock = 1024;
+constexpr uint32_t kLdsHorner = 65536;
+constexpr uint32_t kLdsBytes = 65536 + 512;
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;  // waves per workgroup
 
 // Global-address-space byte pointer: keeps loads as global_load_* (flat loads would force
 // vmcnt(0) + lgkmcnt(0) waits and defeat the prefetch).
@@ -82,6 +93,106 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t *lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
+}
+
+// ---- asm-issued loads ----------------------------------------------------------------
+// Hot-loop loads are issued by inline asm and waited for by an explicit s_waitcnt that
+// threads the destination registers through as in/out operands, so no use can be
+// scheduled above the wait.  hipcc's waitcnt pass merges loop-carried load state
+// conservatively (it waited for two rows where one was needed) and cannot see asm loads;
+// the loads the compiler emits itself are older than or independent of these, and a
+// younger compiler store only makes a wait stricter, never unsafe.
+struct Row {
+    u32x4 q[4];
+};
+
+__device__ __forceinline__ void issue_row(gbyte *p, Row &r) {
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off\n\t"
+        "global_load_dwordx4 %1, %4, off offset:16\n\t"
+        "global_load_dwordx4 %2, %4, off offset:32\n\t"
+        "global_load_dwordx4 %3, %4, off offset:48"
+        : "=&v"(r.q[0]), "=&v"(r.q[1]), "=&v"(r.q[2]), "=&v"(r.q[3])
+        : "v"(p)
+        : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_row(Row &r) {
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(r.q[0]), "+v"(r.q[1]), "+v"(r.q[2]), "+v"(r.q[3]) : "n"(N) : "memory");
+}
+
+__device__ __forceinline__ u32x4 issue_b128(gbyte *p) {
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+__device__ __forceinline__ void row_words(const Row &r, uint32_t d[16]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        d[4 * k + 0] = r.q[k].x;
+        d[4 * k + 1] = r.q[k].y;
+        d[4 * k + 2] = r.q[k].z;
+        d[4 * k + 3] = r.q[k].w;
+    }
+}
+
+// ---- LDS table staging --------------------------------------------------------------
+// Loads the basis image with asm loads, lets `pre` issue kPre more asm loads (the first
+// rows of the workgroup, so their HBM latency overlaps the staging), then waits for the
+// basis only (vmcnt(kPre)) and builds the tables.  Ends with an LDS-only barrier: a
+// __syncthreads() would also wait for the row loads.
+template <int kPre, class Pre>
+__device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__restrict__ img, Pre pre) {
+    const uint32_t t = threadIdx.x;  // 256 threads
+    gbyte *g = (gbyte *)img;
+    // slicing: thread t builds row e = t from S_0..3[t]
+    u32x4 s01 = issue_b128(g + 4 * (kImgSliceT + 4 * t));  // {S0..S3}[t], transposed in the image
+    // combine: lane l = t & 63, nibble positions p0 = t >> 6 and p0 + 4 (4 columns each)
+    const uint32_t l = t & 63u, p0 = t >> 6;
+    u32x4 ca = issue_b128(g + 4 * (kImgCombineCols + l * 32 + 4 * p0));
+    u32x4 cb = issue_b128(g + 4 * (kImgCombineCols + l * 32 + 4 * (p0 + 4)));
+    // Horner: threads 0..127, p = t >> 4 (loads beyond 127 re-read a valid column)
+    u32x4 hc = issue_b128(g + 4 * (kImgHornerCols + 4 * ((t >> 4) & 7u)));
+    pre();
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(s01), "+v"(ca), "+v"(cb), "+v"(hc) : "n"(kPre) : "memory");
+
+    char *b = reinterpret_cast<char *>(lds);
+    // row t, bytes [0,128): S_j replicated 8x at j*32 + 4c
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t v = j == 0 ? s01.x : j == 1 ? s01.y : j == 2 ? s01.z : s01.w;
+        const u32x4 r4 = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(b + t * 256 + j * 32) = r4;
+        *reinterpret_cast<u32x4 *>(b + t * 256 + j * 32 + 16) = r4;
+    }
+    // combine entries (l, p, v) = XOR of columns 4p+bit for the set bits of v
+    const uint32_t lane_base = (l >> 5) * 256 + 128 + (l & 31u) * 4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const u32x4 c = h ? cb : ca;
+        const uint32_t p = p0 + 4 * h;
+#pragma unroll
+        for (uint32_t v = 0; v < 16; ++v) {
+            uint32_t e = 0;
+            if (v & 1) e ^= c.x;
+            if (v & 2) e ^= c.y;
+            if (v & 4) e ^= c.z;
+            if (v & 8) e ^= c.w;
+            *reinterpret_cast<uint32_t *>(b + p * 8192 + v * 512 + lane_base) = e;
+        }
+    }
+    if (t < 128) {
+        const uint32_t v = t & 15u;
+        uint32_t e = 0;
+        if (v & 1) e ^= hc.x;
+        if (v & 2) e ^= hc.y;
+        if (v & 4) e ^= hc.z;
+        if (v & 8) e ^= hc.w;
+        *reinterpret_cast<uint32_t *>(b + kLdsHorner + (t >> 4) * 64 + v * 4) = e;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // ---- loads --------------------------------------------------------------------------
@@ -137,22 +248,22 @@ __device__ __forceinline__ void load64(gbyte *frag, long long o, long long lo, l
 
 // ---- CRC pieces -----------------------------------------------------------------------
 struct CrcLane {
-    uint32_t lanec;   // byte t: LDS low byte of table t, copy (lane & 15)
-    uint32_t sel[4];  // v_perm selectors: byte0 <- lanec.byte(j), byte1 <- X.byte(j)
-    uint32_t l4;      // 4 * lane
+    uint32_t lanec;      // byte j: j*32 + 4c, the low LDS address byte of table j, copy c = lane & 7
+    uint32_t sel[4];     // v_perm selectors: byte0 <- lanec.byte(j), byte1 <- X.byte(j), j = q ^ octet
+    uint32_t comb_base;  // (l >> 5)*256 + 128 + 4*(l & 31): this lane's combine-table column
 };
 
 __device__ __forceinline__ CrcLane make_lane(int lane) {
     CrcLane k;
-    const uint32_t c4 = (uint32_t)(lane & 15) * 4u;
-    k.lanec = c4 | ((c4 + 64u) << 8) | ((c4 + 128u) << 16) | ((c4 + 192u) << 24);
-    const uint32_t flip = (lane & 16) ? 1u : 0u;
+    const uint32_t c4 = (uint32_t)(lane & 7) * 4u;
+    k.lanec = c4 | ((c4 + 32u) << 8) | ((c4 + 64u) << 16) | ((c4 + 96u) << 24);
+    const uint32_t g = (uint32_t)(lane >> 3) & 3u;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        uint32_t j = (uint32_t)q ^ flip;
+        const uint32_t j = (uint32_t)q ^ g;
         k.sel[q] = j | ((4u + j) << 8) | 0x0C0C0000u;
     }
-    k.l4 = (uint32_t)lane * 4u;
+    k.comb_base = ((uint32_t)lane >> 5) * 256u + 128u + ((uint32_t)lane & 31u) * 4u;
     return k;
 }
 
@@ -166,10 +277,10 @@ struct Look4 {
 };
 __device__ __forceinline__ Look4 look4(const uint32_t *lds, const CrcLane &k, uint32_t X) {
     Look4 r;
-    r.t0 = lds_u32(lds, kLdsSlice + __builtin_amdgcn_perm(X, k.lanec, k.sel[0]));
-    r.t1 = lds_u32(lds, kLdsSlice + __builtin_amdgcn_perm(X, k.lanec, k.sel[1]));
-    r.t2 = lds_u32(lds, kLdsSlice + __builtin_amdgcn_perm(X, k.lanec, k.sel[2]));
-    r.t3 = lds_u32(lds, kLdsSlice + __builtin_amdgcn_perm(X, k.lanec, k.sel[3]));
+    r.t0 = lds_u32(lds, __builtin_amdgcn_perm(X, k.lanec, k.sel[0]));
+    r.t1 = lds_u32(lds, __builtin_amdgcn_perm(X, k.lanec, k.sel[1]));
+    r.t2 = lds_u32(lds, __builtin_amdgcn_perm(X, k.lanec, k.sel[2]));
+    r.t3 = lds_u32(lds, __builtin_amdgcn_perm(X, k.lanec, k.sel[3]));
     return r;
 }
 
@@ -189,20 +300,20 @@ __device__ __forceinline__ uint32_t crc_piece(const uint32_t *lds, const CrcLane
 
 // shift by 4032 zero bytes (all lanes read the same 16-entry tables: conflict free)
 __device__ __forceinline__ uint32_t horner_shift(const uint32_t *lds, uint32_t C) {
-    uint32_t r = lds_u32(lds, kLdsHorner + ((C << 2) & 0x3Cu));
+    uint32_t r = lds_u32(lds, kLdsHorner | ((C << 2) & 0x3Cu));
 #pragma unroll
-    for (int p = 1; p < 8; ++p) r ^= lds_u32(lds, kLdsHorner + p * 64 + ((C >> (4 * p - 2)) & 0x3Cu));
+    for (int p = 1; p < 8; ++p) r ^= lds_u32(lds, (kLdsHorner | ((C >> (4 * p - 2)) & 0x3Cu)) + p * 64);
     return r;
 }
 
-// lane l: shift by 64*(63-l) zero bytes (lane-private tables, bank l % 32)
+// lane l: shift by 64*(63-l) zero bytes (lane-private nibble tables, bank l % 32)
 __device__ __forceinline__ uint32_t lane_combine(const uint32_t *lds, const CrcLane &k, uint32_t C) {
-    uint32_t r = lds_u32(lds, kLdsCombine + (((C << 8) & 0xF00u) | k.l4));
-    r ^= lds_u32(lds, kLdsCombine + 4096 + (((C << 4) & 0xF00u) | k.l4));
-    r ^= lds_u32(lds, kLdsCombine + 8192 + ((C & 0xF00u) | k.l4));
+    const uint32_t b = k.comb_base;
+    uint32_t r = lds_u32(lds, ((C << 9) & 0x1E00u) | b);
+    r ^= lds_u32(lds, (((C << 5) & 0x1E00u) | b) + 8192);
+    r ^= lds_u32(lds, (((C << 1) & 0x1E00u) | b) + 2 * 8192);
 #pragma unroll
-    for (int p = 3; p < 8; ++p)
-        r ^= lds_u32(lds, kLdsCombine + p * 4096 + (((C >> (4 * p - 8)) & 0xF00u) | k.l4));
+    for (int p = 3; p < 8; ++p) r ^= lds_u32(lds, (((C >> (4 * p - 9)) & 0x1E00u) | b) + p * 8192);
     return r;
 }
 
@@ -223,6 +334,11 @@ __device__ __forceinline__ uint32_t wave_add(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
            __builtin_amdgcn_readlane(v, 48);
+}
+
+// Fragments of a workgroup: wave w of workgroup b takes fragments b*4*fpw + w + 4i, i < fpw.
+__device__ __forceinline__ uint32_t wg_first(uint32_t fpw) {
+    return uniform(blockIdx.x * kWaves * fpw + (threadIdx.x >> 6));
 }
 
 struct RowGeom {
@@ -264,39 +380,34 @@ __device__ __forceinline__ void crc_inject(uint32_t d[16], const RowGeom &g, uin
     for (uint32_t w = 0; w < 16; ++w) d[w] ^= (w == a) ? mA : ((w == a + 1) ? mB : 0u);
 }
 
+// ---- CRC, general fragments (descriptor batches, ragged messages) -----------------------
 template <class Src>
-__global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, const uint32_t *__restrict__ img,
+__global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uint32_t fpw,
+                                                          const uint32_t *__restrict__ img,
                                                           uint32_t *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
-
-    // stage tables: combine + Horner verbatim, slicing tables replicated 16x
-    for (uint32_t i = threadIdx.x; i < kLdsSlice / 4; i += kBlock) lds[i] = img[i];
-    for (uint32_t i = threadIdx.x; i < 16384u; i += kBlock) {
-        const uint32_t e = i >> 6, j = (i >> 4) & 3u;
-        lds[kLdsSlice / 4 + i] = img[kImgSlice + j * 256 + e];
-    }
-    __syncthreads();
+    stage_tables<0>(lds, img, [] {});
 
     const int lane = threadIdx.x & 63;
     const CrcLane k = make_lane(lane);
-    const size_t nwaves = (size_t)gridDim.x * (kBlock / 64);
-    size_t f = uniform((uint32_t)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)));
+    const size_t f0 = wg_first(fpw);
+    const size_t fend = f0 + (size_t)kWaves * fpw;  // exclusive, stride kWaves
 
-    // skip empty fragments up front
+    // next non-empty fragment at or after x (stride kWaves); empty ones are answered directly
     auto next_nonempty = [&](size_t x, FragInfo &fi) -> size_t {
-        for (; x < n; x += nwaves) {
+        for (; x < n && x < fend; x += kWaves) {
             fi = src.get(x);
             fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
             fi.len = uniform(fi.len);
             fi.partial = uniform(fi.partial);
-            if (fi.len) break;
+            if (fi.len) return x;
             if (lane == 0) out[x] = fi.partial;  // uicrc(p, 0, s) == s
         }
-        return x;
+        return n;
     };
 
     FragInfo cur;
-    f = next_nonempty(f, cur);
+    size_t f = next_nonempty(f0, cur);
     if (f >= n) return;
     RowGeom g = crc_geom(cur);
     uint32_t r = 0;
@@ -311,7 +422,7 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, con
         size_t nf = f;
         uint32_t nr = r + 1;
         if (nr >= g.R) {
-            nf = next_nonempty(f + nwaves, nfi);
+            nf = next_nonempty(f + kWaves, nfi);
             nr = 0;
             if (nf < n) ng = crc_geom(nfi);
         }
@@ -354,125 +465,165 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, con
 
 // ---- CRC fast path: regular batches -------------------------------------------------------
 // Fragment f = base + f*frag_len, frag_len = R*4096, base 16-byte aligned (P = 0, no masks).
-// A wave walks its (fragment, row) tasks with two register buffers; the next task's loads
-// are always issued (clamped to the last task) so the hot loop has no load-side branches.
-// One row task of a wave: fragment i (global index f0 + i*nw, first byte at fptr), row r.
-struct RegTask {
-    uint64_t foff;  // wave-uniform byte offset of the fragment's first byte from base
-    uint32_t i, r;
-};
-// Row loads for the regular kernel are issued by inline asm and waited for by an explicit
-// s_waitcnt that takes the destination registers as in/out operands: hipcc's waitcnt pass
-// merges loop-carried load state conservatively (it waited for two rows where one was
-// needed), and an asm load is invisible to it.  Every global load/store the compiler emits
-// in the loop is older than or unrelated to these, so counting only our own loads is exact
-// or conservative (a younger store only makes the wait stricter).
-struct Row {
-    u32x4 q[4];
+// A wave checksums TWO of its fragments at once (two independent lookup chains interleaved:
+// with two waves per SIMD a single chain's LDS latency, ~1 us per row, is too close to the
+// ~1.3 us of HBM time per row).  Steps (a pair of rows) flow through three register buffers
+// -- two steps in flight while one is checksummed -- and the next loads are always issued
+// (clamped to the last step), so the hot loop has no load-side branches.
+struct PairTask {
+    uint32_t i, r;  // fragments 2i and 2i+1 of this wave's list, row r
 };
 
-__device__ __forceinline__ void issue_row(gbyte *p, Row &r) {
-    asm volatile(
-        "global_load_dwordx4 %0, %4, off\n\t"
-        "global_load_dwordx4 %1, %4, off offset:16\n\t"
-        "global_load_dwordx4 %2, %4, off offset:32\n\t"
-        "global_load_dwordx4 %3, %4, off offset:48"
-        : "=&v"(r.q[0]), "=&v"(r.q[1]), "=&v"(r.q[2]), "=&v"(r.q[3])
-        : "v"(p)
-        : "memory");
+struct Rows2 {
+    Row a, b;
+};
+
+__device__ __forceinline__ void issue_rows2(gbyte *pa, gbyte *pb, Rows2 &x) {
+    issue_row(pa, x.a);
+    issue_row(pb, x.b);
 }
 
-// wait until at most N of this wave's vector-memory ops are outstanding; r's registers are
-// threaded through so no use of them can be scheduled above the wait
 template <int N>
-__device__ __forceinline__ void wait_row(Row &r) {
-    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(r.q[0]), "+v"(r.q[1]), "+v"(r.q[2]), "+v"(r.q[3]) : "n"(N) : "memory");
+__device__ __forceinline__ void wait_rows2(Rows2 &x) {
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(x.a.q[0]), "+v"(x.a.q[1]), "+v"(x.a.q[2]), "+v"(x.a.q[3]), "+v"(x.b.q[0]), "+v"(x.b.q[1]),
+                   "+v"(x.b.q[2]), "+v"(x.b.q[3])
+                 : "n"(N)
+                 : "memory");
 }
 
-__device__ __forceinline__ void row_words(const Row &r, uint32_t d[16]) {
+// two registers through their 16-word pieces, chains interleaved
+__device__ __forceinline__ void crc_piece2(const uint32_t *lds, const CrcLane &k, uint32_t &C0, uint32_t &C1,
+                                           const uint32_t d0[16], const uint32_t d1[16]) {
+    uint32_t X0 = C0 ^ d0[0], X1 = C1 ^ d1[0];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        d[4 * k + 0] = r.q[k].x;
-        d[4 * k + 1] = r.q[k].y;
-        d[4 * k + 2] = r.q[k].z;
-        d[4 * k + 3] = r.q[k].w;
+    for (int w = 0; w < 15; ++w) {
+        const Look4 t = look4(lds, k, X0);
+        const Look4 u = look4(lds, k, X1);
+        X0 = xor3(xor3(t.t0, t.t1, t.t2), t.t3, d0[w + 1]);
+        X1 = xor3(xor3(u.t0, u.t1, u.t2), u.t3, d1[w + 1]);
     }
+    const Look4 t = look4(lds, k, X0);
+    const Look4 u = look4(lds, k, X1);
+    C0 = xor3(t.t0, t.t1, t.t2) ^ t.t3;
+    C1 = xor3(u.t0, u.t1, u.t2) ^ u.t3;
 }
 
-__device__ __forceinline__ void crc_reg_row(const uint32_t *lds, const CrcLane &k, int lane, uint32_t &C,
-                                            const uint32_t d[16], uint32_t r, uint32_t R, uint32_t vinit,
-                                            uint32_t *out, size_t f) {
-    if (r == 0)
-        C = (lane == 0) ? vinit : 0u;
-    else
-        C = horner_shift(lds, C);
-    C = crc_piece(lds, k, C, d);
-    if (r + 1 == R) {
-        const uint32_t x = wave_xor(lane_combine(lds, k, C));
-        if (lane == 0) out[f] = __builtin_bswap32(x);
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, size_t n,
-                                                             size_t frag_len, uint32_t partial,
+// kAblate (tools/microbench/crc_ablation.hip only; the product launches 0):
+//   1 = loads only (words XOR-folded, no table lookups), 2 = lookups only (no global loads)
+template <int kAblate>
+__global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
+                                                             uint32_t fpw, size_t frag_len, uint32_t partial,
                                                              const uint32_t *__restrict__ img,
                                                              uint32_t *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
-    for (uint32_t i = threadIdx.x; i < kLdsSlice / 4; i += kBlock) lds[i] = img[i];
-    for (uint32_t i = threadIdx.x; i < 16384u; i += kBlock) {
-        const uint32_t e = i >> 6, j = (i >> 4) & 3u;
-        lds[kLdsSlice / 4 + i] = img[kImgSlice + j * 256 + e];
-    }
-    __syncthreads();
-
     const int lane = threadIdx.x & 63;
-    const CrcLane k = make_lane(lane);
     const uint32_t R = (uint32_t)(frag_len / kRowBytes);
-    const uint32_t nw = gridDim.x * (kBlock / 64);
-    const uint32_t f0 = uniform(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
-    if (f0 >= n) return;
-    const uint32_t nfr = (uint32_t)((n - f0 + nw - 1) / nw);  // fragments of this wave
-    const uint64_t fstep = (uint64_t)nw * frag_len;
-    const uint32_t vinit = __builtin_bswap32(partial);
+    const uint32_t f0 = wg_first(fpw);
+    // fragments of this wave: f0 + kWaves*j, j < nfr; processed in pairs (2i, 2i+1)
+    const uint32_t nfr = f0 < n ? min(fpw, (n - f0 + kWaves - 1) / kWaves) : 0u;
+    const uint32_t npair = (nfr + 1) / 2;
     const uint32_t lane_off = (uint32_t)lane * kLaneBytes;
-    uint32_t C = 0;
+    const uint32_t vinit = __builtin_bswap32(partial);
 
-    // next task, clamped to the last one (its reload is harmless and keeps loads unconditional)
-    auto advance = [&](RegTask t) -> RegTask {
-        if (t.r + 1 < R) return {t.foff, t.i, t.r + 1};
-        if (t.i + 1 < nfr) return {t.foff + fstep, t.i + 1, 0u};
+    auto advance = [&](PairTask t) -> PairTask {
+        if (t.r + 1 < R) return {t.i, t.r + 1};
+        if (t.i + 1 < npair) return {t.i + 1, 0u};
         return t;
     };
-    auto row_ptr = [&](const RegTask &t) -> gbyte * {
-        return (gbyte *)(base + (t.foff + (uint64_t)t.r * kRowBytes + lane_off));
+    auto is_last = [&](const PairTask &t) -> bool { return t.i + 1 >= npair && t.r + 1 >= R; };
+    // fragment slot s of pair i; a missing second fragment re-reads the first (no output)
+    auto frag = [&](uint32_t i, uint32_t s) -> uint32_t {
+        const uint32_t j = 2 * i + s;
+        return f0 + kWaves * (j < nfr ? j : 2 * i);
     };
-    auto is_last = [&](const RegTask &t) -> bool { return t.i + 1 >= nfr && t.r + 1 >= R; };
-    auto process = [&](Row &buf, const RegTask &t) {
-        uint32_t d[16];
-        row_words(buf, d);
-        crc_reg_row(lds, k, lane, C, d, t.r, R, vinit, out, (size_t)f0 + (size_t)t.i * nw);
+    auto row_ptr = [&](uint32_t f, uint32_t r) -> gbyte * {
+        return (gbyte *)(base + ((uint64_t)(nfr ? f : 0u) * frag_len + (uint64_t)r * kRowBytes + lane_off));
+    };
+    auto issue = [&](const PairTask &t, Rows2 &x) {
+        issue_rows2(row_ptr(frag(t.i, 0), t.r), row_ptr(frag(t.i, 1), t.r), x);
     };
 
-    // three row buffers: two rows stay in flight while the third is checksummed
-    RegTask ta{(uint64_t)f0 * frag_len, 0u, 0u};
-    RegTask tb = advance(ta);
-    Row A, B, Cb;
-    issue_row(row_ptr(ta), A);
-    issue_row(row_ptr(tb), B);
+    PairTask ta{0u, 0u};
+    PairTask tb = advance(ta);
+    Rows2 A, B, Cb;
+    if (kAblate != 2) {
+        stage_tables<16>(lds, img, [&] {
+            issue(ta, A);
+            issue(tb, B);
+        });
+    } else {
+        stage_tables<0>(lds, img, [] {});
+    }
+    if (nfr == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return;
+    }
+    const CrcLane k = make_lane(lane);
+    uint32_t C0 = 0, C1 = 0;
+    auto process = [&](Rows2 &x, const PairTask &t) {
+        uint32_t d0[16], d1[16];
+        row_words(x.a, d0);
+        row_words(x.b, d1);
+        const bool has1 = 2 * t.i + 1 < nfr;
+        if (kAblate == 1) {
+            uint32_t y0 = C0, y1 = C1;
+#pragma unroll
+            for (int w = 0; w < 16; ++w) {
+                y0 ^= d0[w];
+                y1 ^= d1[w];
+            }
+            C0 = y0;
+            C1 = y1;
+            if (t.r + 1 == R && lane == 0) {
+                out[frag(t.i, 0)] = C0;
+                if (has1) out[frag(t.i, 1)] = C1;
+            }
+            return;
+        }
+        if (t.r == 0) {
+            C0 = C1 = (lane == 0) ? vinit : 0u;
+        } else {
+            C0 = horner_shift(lds, C0);
+            C1 = horner_shift(lds, C1);
+        }
+        crc_piece2(lds, k, C0, C1, d0, d1);
+        if (t.r + 1 == R) {
+            const uint32_t x0 = wave_xor(lane_combine(lds, k, C0));
+            const uint32_t x1 = wave_xor(lane_combine(lds, k, C1));
+            if (lane == 0) {
+                out[frag(t.i, 0)] = __builtin_bswap32(x0);
+                if (has1) out[frag(t.i, 1)] = __builtin_bswap32(x1);
+            }
+        }
+    };
+    if (kAblate == 2) {  // same lookups on register data, no HBM traffic
+        for (int w = 0; w < 4; ++w) {
+            A.a.q[w] = u32x4{lane_off + w, lane_off ^ 0x5A5Au, 7u * w, f0};
+            A.b.q[w] = u32x4{lane_off + 3 * w, lane_off ^ 0xA5A5u, 5u * w, f0 + 1};
+        }
+        for (PairTask t = ta;; t = advance(t)) {
+            process(A, t);
+            A.a.q[0].x ^= C0;
+            A.b.q[0].x ^= C1;
+            if (is_last(t)) break;
+        }
+        return;
+    }
     for (;;) {
-        RegTask tc = advance(tb);
-        issue_row(row_ptr(tc), Cb);
-        wait_row<8>(A);
+        PairTask tc = advance(tb);
+        issue(tc, Cb);
+        wait_rows2<16>(A);
         process(A, ta);
         if (is_last(ta)) break;
         ta = advance(tc);
-        issue_row(row_ptr(ta), A);
-        wait_row<8>(B);
+        issue(ta, A);
+        wait_rows2<16>(B);
         process(B, tb);
         if (is_last(tb)) break;
         tb = advance(ta);
-        issue_row(row_ptr(tb), B);
-        wait_row<8>(Cb);
+        issue(tb, B);
+        wait_rows2<16>(Cb);
         process(Cb, tc);
         if (is_last(tc)) break;
     }
@@ -481,10 +632,11 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
 
 // ---- SUM -------------------------------------------------------------------------------
 template <class Src>
-__global__ void __launch_bounds__(256) sum_rows_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
+__global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uint32_t fpw, uint32_t *__restrict__ out) {
     const int lane = threadIdx.x & 63;
-    const size_t nwaves = (size_t)gridDim.x * (256 / 64);
-    for (size_t f = uniform((uint32_t)(blockIdx.x * 4 + (threadIdx.x >> 6))); f < n; f += nwaves) {
+    const size_t f0 = wg_first(fpw);
+    const size_t fend = f0 + (size_t)kWaves * fpw;
+    for (size_t f = f0; f < n && f < fend; f += kWaves) {
         FragInfo fi = src.get(f);
         fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
         fi.len = uniform(fi.len);
@@ -651,51 +803,62 @@ int crc_grid(int device) {
     return cu[device];
 }
 
+// fragments per wave for the non-persistent grids: enough work per workgroup to amortise the
+// 64.5 KiB table staging, small enough to keep the chip's read window compact
+static uint32_t pick_fpw(size_t n, uint32_t R) {
+    uint32_t fpw = R >= 4 ? 8u : 32u;
+    while (fpw > 1 && (size_t)kWaves * fpw * 512 > n) fpw >>= 1;  // small batches: more workgroups
+    return fpw;
+}
+
+static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size_t)kWaves * fpw - 1) / ((size_t)kWaves * fpw))); }
+
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
                            hipStream_t s) {
+    (void)grid;
     if (n == 0) return hipSuccess;
-    size_t need = (n + 15) / 16;
-    int g = (int)(need < (size_t)grid ? need : (size_t)grid);
-    hipLaunchKernelGGL(crc_rows_kernel<DescSource>, dim3(g), dim3(kBlock), 0, s, DescSource{d}, n, img, out);
+    const uint32_t fpw = pick_fpw(n, 1);
+    hipLaunchKernelGGL(crc_rows_kernel<DescSource>, grid_for(n, fpw), dim3(kBlock), 0, s, DescSource{d}, n, fpw, img,
+                       out);
     return hipGetLastError();
 }
 
 hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, size_t n,
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
+    (void)grid;
     if (n == 0) return hipSuccess;
-    size_t need = (n + 15) / 16;
-    int g = (int)(need < (size_t)grid ? need : (size_t)grid);
-    hipLaunchKernelGGL(crc_rows_kernel<MsgSource>, dim3(g), dim3(kBlock), 0, s,
-                       MsgSource{base, msg_len, frag_len, partial}, n, img, out);
+    const uint32_t fpw = pick_fpw(n, (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes));
+    hipLaunchKernelGGL(crc_rows_kernel<MsgSource>, grid_for(n, fpw), dim3(kBlock), 0, s,
+                       MsgSource{base, msg_len, frag_len, partial}, n, fpw, img, out);
     return hipGetLastError();
 }
 
 hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
                               const uint32_t *img, int grid, hipStream_t s) {
+    (void)grid;
     if (n == 0) return hipSuccess;
-    size_t need = (n + 15) / 16;
-    int g = (int)(need < (size_t)grid ? need : (size_t)grid);
-    hipLaunchKernelGGL(crc_regular_kernel, dim3(g), dim3(kBlock), 0, s, base, n, frag_len, partial, img, out);
+    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t fpw = pick_fpw(n, (uint32_t)(frag_len / kRowBytes));
+    hipLaunchKernelGGL(crc_regular_kernel<0>, grid_for(n, fpw), dim3(kBlock), 0, s, base, (uint32_t)n, fpw, frag_len,
+                       partial, img, out);
     return hipGetLastError();
 }
 
 hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, int grid, hipStream_t s) {
+    (void)grid;
     if (n == 0) return hipSuccess;
-    size_t need = (n + 3) / 4;
-    size_t cap = (size_t)grid * 8;
-    int g = (int)(need < cap ? need : cap);
-    hipLaunchKernelGGL(sum_rows_kernel<DescSource>, dim3(g), dim3(256), 0, s, DescSource{d}, n, out);
+    const uint32_t fpw = pick_fpw(n, 1);
+    hipLaunchKernelGGL(sum_rows_kernel<DescSource>, grid_for(n, fpw), dim3(kBlock), 0, s, DescSource{d}, n, fpw, out);
     return hipGetLastError();
 }
 
 hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out, int grid,
                           hipStream_t s) {
+    (void)grid;
     if (n == 0) return hipSuccess;
-    size_t need = (n + 3) / 4;
-    size_t cap = (size_t)grid * 8;
-    int g = (int)(need < cap ? need : cap);
-    hipLaunchKernelGGL(sum_rows_kernel<MsgSource>, dim3(g), dim3(256), 0, s,
-                       MsgSource{base, msg_len, frag_len, 0u}, n, out);
+    const uint32_t fpw = pick_fpw(n, 1);
+    hipLaunchKernelGGL(sum_rows_kernel<MsgSource>, grid_for(n, fpw), dim3(kBlock), 0, s,
+                       MsgSource{base, msg_len, frag_len, 0u}, n, fpw, out);
     return hipGetLastError();
 }
 

@@ -16,6 +16,20 @@
 
 using namespace lampi;
 
+// nibble-table application of a linear map given by its 32 columns (as the kernels'
+// LDS tables hold it: entry (p, v) = XOR of columns 4p + set bits of v)
+static uint32_t nib(const uint32_t *cols, uint32_t C) {
+    uint32_t r = 0;
+    for (int p = 0; p < 8; ++p) {
+        const uint32_t v = (C >> (4 * p)) & 15u;
+        uint32_t e = 0;
+        for (int b = 0; b < 4; ++b)
+            if (v >> b & 1u) e ^= cols[4 * p + b];
+        r ^= e;
+    }
+    return r;
+}
+
 static uint32_t emulate(const std::vector<uint32_t> &img, const uint8_t *msg, uint32_t L, uint32_t partial) {
     if (L == 0) return partial;
     const uint32_t R = (L + kRowBytes - 1) / kRowBytes;
@@ -25,11 +39,7 @@ static uint32_t emulate(const std::vector<uint32_t> &img, const uint8_t *msg, ui
     for (int lane = 0; lane < kWave; ++lane) {
         uint32_t C = 0;
         for (uint32_t r = 0; r < R; ++r) {
-            if (r) {  // Horner: 8 nibble lookups
-                uint32_t x = 0;
-                for (int p = 0; p < 8; ++p) x ^= img[kImgHorner + p * 16 + ((C >> (4 * p)) & 15u)];
-                C = x;
-            }
+            if (r) C = nib(&img[kImgHornerCols], C);  // Horner: 8 nibble lookups
             for (int w = 0; w < 16; ++w) {
                 // frame position of this word, real offset
                 const long long fp = (long long)r * kRowBytes + lane * kLaneBytes + 4 * w;
@@ -43,13 +53,11 @@ static uint32_t emulate(const std::vector<uint32_t> &img, const uint8_t *msg, ui
                     word |= byte << (8 * j);
                 }
                 const uint32_t X = C ^ word;
-                C = img[kImgSlice + 0 * 256 + (X & 255u)] ^ img[kImgSlice + 1 * 256 + ((X >> 8) & 255u)] ^
-                    img[kImgSlice + 2 * 256 + ((X >> 16) & 255u)] ^ img[kImgSlice + 3 * 256 + (X >> 24)];
+                C = img[kImgSliceT + 4 * (X & 255u) + 0] ^ img[kImgSliceT + 4 * ((X >> 8) & 255u) + 1] ^
+                    img[kImgSliceT + 4 * ((X >> 16) & 255u) + 2] ^ img[kImgSliceT + 4 * (X >> 24) + 3];
             }
         }
-        uint32_t x = 0;  // lane combine
-        for (int p = 0; p < 8; ++p) x ^= img[kImgCombine + p * 1024 + ((C >> (4 * p)) & 15u) * 64 + lane];
-        total ^= x;
+        total ^= nib(&img[kImgCombineCols + lane * 32], C);  // lane combine
     }
     uint32_t res = bswap32(total);
     if (L < 4) res ^= partial << (8 * L);
