@@ -143,12 +143,20 @@ __device__ __forceinline__ void row_words(const Row &r, uint32_t d[16]) {
 // rows of the workgroup, so their HBM latency overlaps the staging), then waits for the
 // basis only (vmcnt(kPre)) and builds the tables.  Ends with an LDS-only barrier: a
 // __syncthreads() would also wait for the row loads.
-template <int kPre, class Pre>
+// kParts (diagnostics only, tools/microbench/crc_ablation.hip): bit 0 slicing, bit 1 combine,
+// bit 2 Horner tables; the product always builds all three.
+template <int kPre, class Pre, int kParts = 7>
 __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__restrict__ img, Pre pre) {
     const uint32_t t = threadIdx.x;  // 256 threads
     gbyte *g = (gbyte *)img;
-    // slicing: thread t builds row e = t from S_0..3[t]
-    u32x4 s01 = issue_b128(g + 4 * (kImgSliceT + 4 * t));  // {S0..S3}[t], transposed in the image
+    // slicing: thread t fills 16-byte slot t & 7 of rows (t >> 3) + 32k, k = 0..7, i.e. table
+    // j = (t & 7) >> 1; consecutive lanes write consecutive slots (a thread-per-row fill put
+    // every lane of a ds_write_b128 on the same banks: 1.2 us per workgroup, measured)
+    const uint32_t sj = (t & 7u) >> 1, r0 = t >> 3;
+    uint32_t sv[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+        asm volatile("global_load_dword %0, %1, off" : "=&v"(sv[kk]) : "v"(g + 4 * (kImgSliceT + 4 * (r0 + 32 * kk) + sj)) : "memory");
     // combine: lane l = t & 63, nibble positions p0 = t >> 6 and p0 + 4 (4 columns each)
     const uint32_t l = t & 63u, p0 = t >> 6;
     u32x4 ca = issue_b128(g + 4 * (kImgCombineCols + l * 32 + 4 * p0));
@@ -156,21 +164,21 @@ __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__re
     // Horner: threads 0..127, p = t >> 4 (loads beyond 127 re-read a valid column)
     u32x4 hc = issue_b128(g + 4 * (kImgHornerCols + 4 * ((t >> 4) & 7u)));
     pre();
-    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(s01), "+v"(ca), "+v"(cb), "+v"(hc) : "n"(kPre) : "memory");
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(ca), "+v"(cb), "+v"(hc), "+v"(sv[0]) : "n"(kPre) : "memory");
+    asm volatile("" : "+v"(sv[1]), "+v"(sv[2]), "+v"(sv[3]), "+v"(sv[4]), "+v"(sv[5]), "+v"(sv[6]), "+v"(sv[7]));
 
     char *b = reinterpret_cast<char *>(lds);
-    // row t, bytes [0,128): S_j replicated 8x at j*32 + 4c
+    // rows r0 + 32k, slot t & 7 (bytes 16*(t&7) .. +16 = copies 4*(t&1) .. +3 of S_sj)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t v = j == 0 ? s01.x : j == 1 ? s01.y : j == 2 ? s01.z : s01.w;
+    for (int kk = 0; kk < ((kParts & 1) ? 8 : 0); ++kk) {
+        const uint32_t v = sv[kk];
         const u32x4 r4 = {v, v, v, v};
-        *reinterpret_cast<u32x4 *>(b + t * 256 + j * 32) = r4;
-        *reinterpret_cast<u32x4 *>(b + t * 256 + j * 32 + 16) = r4;
+        *reinterpret_cast<u32x4 *>(b + (r0 + 32 * kk) * 256 + (t & 7u) * 16) = r4;
     }
     // combine entries (l, p, v) = XOR of columns 4p+bit for the set bits of v
     const uint32_t lane_base = (l >> 5) * 256 + 128 + (l & 31u) * 4;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < ((kParts & 2) ? 2 : 0); ++h) {
         const u32x4 c = h ? cb : ca;
         const uint32_t p = p0 + 4 * h;
 #pragma unroll
@@ -183,7 +191,7 @@ __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__re
             *reinterpret_cast<uint32_t *>(b + p * 8192 + v * 512 + lane_base) = e;
         }
     }
-    if (t < 128) {
+    if ((kParts & 4) && t < 128) {
         const uint32_t v = t & 15u;
         uint32_t e = 0;
         if (v & 1) e ^= hc.x;
@@ -465,90 +473,109 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
 
 // ---- CRC fast path: regular batches -------------------------------------------------------
 // Fragment f = base + f*frag_len, frag_len = R*4096, base 16-byte aligned (P = 0, no masks).
-// A wave checksums TWO of its fragments at once (two independent lookup chains interleaved:
-// with two waves per SIMD a single chain's LDS latency, ~1 us per row, is too close to the
-// ~1.3 us of HBM time per row).  Steps (a pair of rows) flow through three register buffers
+// A wave checksums kChains of its fragments at once (independent lookup chains interleaved:
+// with two waves per SIMD one chain's LDS latency, ~1 us per row, is too close to the
+// ~1.3 us of HBM time per row).  Steps (kChains rows) flow through three register buffers
 // -- two steps in flight while one is checksummed -- and the next loads are always issued
 // (clamped to the last step), so the hot loop has no load-side branches.
-struct PairTask {
-    uint32_t i, r;  // fragments 2i and 2i+1 of this wave's list, row r
+struct GroupTask {
+    uint32_t i, r;  // fragments kChains*i .. kChains*i + kChains-1 of this wave's list, row r
 };
 
-struct Rows2 {
-    Row a, b;
+template <int K>
+struct RowsK {
+    Row x[K];
 };
 
-__device__ __forceinline__ void issue_rows2(gbyte *pa, gbyte *pb, Rows2 &x) {
-    issue_row(pa, x.a);
-    issue_row(pb, x.b);
+template <int N, int K>
+__device__ __forceinline__ void wait_rows(RowsK<K> &b) {
+    if constexpr (K == 2) {
+        asm volatile("s_waitcnt vmcnt(%8)"
+                     : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
+                       "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3])
+                     : "n"(N)
+                     : "memory");
+    } else {
+        static_assert(K == 4, "kChains is 2 or 4");
+        asm volatile("s_waitcnt vmcnt(%16)"
+                     : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
+                       "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3]),
+                       "+v"(b.x[2].q[0]), "+v"(b.x[2].q[1]), "+v"(b.x[2].q[2]), "+v"(b.x[2].q[3]),
+                       "+v"(b.x[3].q[0]), "+v"(b.x[3].q[1]), "+v"(b.x[3].q[2]), "+v"(b.x[3].q[3])
+                     : "n"(N)
+                     : "memory");
+    }
 }
 
-template <int N>
-__device__ __forceinline__ void wait_rows2(Rows2 &x) {
-    asm volatile("s_waitcnt vmcnt(%8)"
-                 : "+v"(x.a.q[0]), "+v"(x.a.q[1]), "+v"(x.a.q[2]), "+v"(x.a.q[3]), "+v"(x.b.q[0]), "+v"(x.b.q[1]),
-                   "+v"(x.b.q[2]), "+v"(x.b.q[3])
-                 : "n"(N)
-                 : "memory");
+__device__ __forceinline__ uint32_t row_word(const Row &r, int w) {
+    const u32x4 v = r.q[w >> 2];
+    return (w & 3) == 0 ? v.x : (w & 3) == 1 ? v.y : (w & 3) == 2 ? v.z : v.w;
 }
 
-// two registers through their 16-word pieces, chains interleaved
-__device__ __forceinline__ void crc_piece2(const uint32_t *lds, const CrcLane &k, uint32_t &C0, uint32_t &C1,
-                                           const uint32_t d0[16], const uint32_t d1[16]) {
-    uint32_t X0 = C0 ^ d0[0], X1 = C1 ^ d1[0];
+// K registers through their 16-word pieces, chains interleaved
+template <int K>
+__device__ __forceinline__ void crc_pieces(const uint32_t *lds, const CrcLane &k, uint32_t (&C)[K],
+                                           const RowsK<K> &b) {
+    uint32_t X[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) X[c] = C[c] ^ row_word(b.x[c], 0);
 #pragma unroll
     for (int w = 0; w < 15; ++w) {
-        const Look4 t = look4(lds, k, X0);
-        const Look4 u = look4(lds, k, X1);
-        X0 = xor3(xor3(t.t0, t.t1, t.t2), t.t3, d0[w + 1]);
-        X1 = xor3(xor3(u.t0, u.t1, u.t2), u.t3, d1[w + 1]);
+        Look4 t[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) t[c] = look4(lds, k, X[c]);
+#pragma unroll
+        for (int c = 0; c < K; ++c) X[c] = xor3(xor3(t[c].t0, t[c].t1, t[c].t2), t[c].t3, row_word(b.x[c], w + 1));
     }
-    const Look4 t = look4(lds, k, X0);
-    const Look4 u = look4(lds, k, X1);
-    C0 = xor3(t.t0, t.t1, t.t2) ^ t.t3;
-    C1 = xor3(u.t0, u.t1, u.t2) ^ u.t3;
+    Look4 t[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) t[c] = look4(lds, k, X[c]);
+#pragma unroll
+    for (int c = 0; c < K; ++c) C[c] = xor3(t[c].t0, t[c].t1, t[c].t2) ^ t[c].t3;
 }
 
 // kAblate (tools/microbench/crc_ablation.hip only; the product launches 0):
 //   1 = loads only (words XOR-folded, no table lookups), 2 = lookups only (no global loads)
-template <int kAblate>
+template <int kAblate, int kChains>
 __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
                                                              uint32_t fpw, size_t frag_len, uint32_t partial,
                                                              const uint32_t *__restrict__ img,
                                                              uint32_t *__restrict__ out) {
+    constexpr int K = kChains;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
     const uint32_t R = (uint32_t)(frag_len / kRowBytes);
     const uint32_t f0 = wg_first(fpw);
-    // fragments of this wave: f0 + kWaves*j, j < nfr; processed in pairs (2i, 2i+1)
+    // fragments of this wave: f0 + kWaves*j, j < nfr; processed in groups of K
     const uint32_t nfr = f0 < n ? min(fpw, (n - f0 + kWaves - 1) / kWaves) : 0u;
-    const uint32_t npair = (nfr + 1) / 2;
+    const uint32_t ngrp = (nfr + K - 1) / K;
     const uint32_t lane_off = (uint32_t)lane * kLaneBytes;
     const uint32_t vinit = __builtin_bswap32(partial);
 
-    auto advance = [&](PairTask t) -> PairTask {
+    auto advance = [&](GroupTask t) -> GroupTask {
         if (t.r + 1 < R) return {t.i, t.r + 1};
-        if (t.i + 1 < npair) return {t.i + 1, 0u};
+        if (t.i + 1 < ngrp) return {t.i + 1, 0u};
         return t;
     };
-    auto is_last = [&](const PairTask &t) -> bool { return t.i + 1 >= npair && t.r + 1 >= R; };
-    // fragment slot s of pair i; a missing second fragment re-reads the first (no output)
+    auto is_last = [&](const GroupTask &t) -> bool { return t.i + 1 >= ngrp && t.r + 1 >= R; };
+    // fragment of slot s in group i; missing fragments (past nfr) re-read slot 0 (no output)
     auto frag = [&](uint32_t i, uint32_t s) -> uint32_t {
-        const uint32_t j = 2 * i + s;
-        return f0 + kWaves * (j < nfr ? j : 2 * i);
+        const uint32_t j = K * i + s;
+        return f0 + kWaves * (j < nfr ? j : K * i);
     };
     auto row_ptr = [&](uint32_t f, uint32_t r) -> gbyte * {
         return (gbyte *)(base + ((uint64_t)(nfr ? f : 0u) * frag_len + (uint64_t)r * kRowBytes + lane_off));
     };
-    auto issue = [&](const PairTask &t, Rows2 &x) {
-        issue_rows2(row_ptr(frag(t.i, 0), t.r), row_ptr(frag(t.i, 1), t.r), x);
+    auto issue = [&](const GroupTask &t, RowsK<K> &b) {
+#pragma unroll
+        for (int c = 0; c < K; ++c) issue_row(row_ptr(frag(t.i, c), t.r), b.x[c]);
     };
 
-    PairTask ta{0u, 0u};
-    PairTask tb = advance(ta);
-    Rows2 A, B, Cb;
+    GroupTask ta{0u, 0u};
+    GroupTask tb = advance(ta);
+    RowsK<K> A, B, Cb;
     if (kAblate != 2) {
-        stage_tables<16>(lds, img, [&] {
+        stage_tables<8 * K>(lds, img, [&] {
             issue(ta, A);
             issue(tb, B);
         });
@@ -560,70 +587,72 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
         return;
     }
     const CrcLane k = make_lane(lane);
-    uint32_t C0 = 0, C1 = 0;
-    auto process = [&](Rows2 &x, const PairTask &t) {
-        uint32_t d0[16], d1[16];
-        row_words(x.a, d0);
-        row_words(x.b, d1);
-        const bool has1 = 2 * t.i + 1 < nfr;
-        if (kAblate == 1) {
-            uint32_t y0 = C0, y1 = C1;
+    uint32_t C[K];
 #pragma unroll
-            for (int w = 0; w < 16; ++w) {
-                y0 ^= d0[w];
-                y1 ^= d1[w];
+    for (int c = 0; c < K; ++c) C[c] = 0;
+    auto process = [&](RowsK<K> &b, const GroupTask &t) {
+        if (kAblate == 1) {
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                uint32_t y = C[c];
+#pragma unroll
+                for (int w = 0; w < 16; ++w) y ^= row_word(b.x[c], w);
+                C[c] = y;
             }
-            C0 = y0;
-            C1 = y1;
             if (t.r + 1 == R && lane == 0) {
-                out[frag(t.i, 0)] = C0;
-                if (has1) out[frag(t.i, 1)] = C1;
+#pragma unroll
+                for (int c = 0; c < K; ++c)
+                    if (K * t.i + c < nfr) out[frag(t.i, c)] = C[c];
             }
             return;
         }
         if (t.r == 0) {
-            C0 = C1 = (lane == 0) ? vinit : 0u;
+#pragma unroll
+            for (int c = 0; c < K; ++c) C[c] = (lane == 0) ? vinit : 0u;
         } else {
-            C0 = horner_shift(lds, C0);
-            C1 = horner_shift(lds, C1);
+#pragma unroll
+            for (int c = 0; c < K; ++c) C[c] = horner_shift(lds, C[c]);
         }
-        crc_piece2(lds, k, C0, C1, d0, d1);
+        crc_pieces<K>(lds, k, C, b);
         if (t.r + 1 == R) {
-            const uint32_t x0 = wave_xor(lane_combine(lds, k, C0));
-            const uint32_t x1 = wave_xor(lane_combine(lds, k, C1));
+            uint32_t x[K];
+#pragma unroll
+            for (int c = 0; c < K; ++c) x[c] = lane_combine(lds, k, C[c]);
+#pragma unroll
+            for (int c = 0; c < K; ++c) x[c] = wave_xor(x[c]);
             if (lane == 0) {
-                out[frag(t.i, 0)] = __builtin_bswap32(x0);
-                if (has1) out[frag(t.i, 1)] = __builtin_bswap32(x1);
+#pragma unroll
+                for (int c = 0; c < K; ++c)
+                    if (K * t.i + c < nfr) out[frag(t.i, c)] = __builtin_bswap32(x[c]);
             }
         }
     };
     if (kAblate == 2) {  // same lookups on register data, no HBM traffic
-        for (int w = 0; w < 4; ++w) {
-            A.a.q[w] = u32x4{lane_off + w, lane_off ^ 0x5A5Au, 7u * w, f0};
-            A.b.q[w] = u32x4{lane_off + 3 * w, lane_off ^ 0xA5A5u, 5u * w, f0 + 1};
-        }
-        for (PairTask t = ta;; t = advance(t)) {
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+            for (int w = 0; w < 4; ++w) A.x[c].q[w] = u32x4{lane_off + w + 7u * c, lane_off ^ 0x5A5Au, 7u * w, f0 + c};
+        for (GroupTask t = ta;; t = advance(t)) {
             process(A, t);
-            A.a.q[0].x ^= C0;
-            A.b.q[0].x ^= C1;
+#pragma unroll
+            for (int c = 0; c < K; ++c) A.x[c].q[0].x ^= C[c];
             if (is_last(t)) break;
         }
         return;
     }
     for (;;) {
-        PairTask tc = advance(tb);
+        GroupTask tc = advance(tb);
         issue(tc, Cb);
-        wait_rows2<16>(A);
+        wait_rows<16 * K / 2, K>(A);
         process(A, ta);
         if (is_last(ta)) break;
         ta = advance(tc);
         issue(ta, A);
-        wait_rows2<16>(B);
+        wait_rows<16 * K / 2, K>(B);
         process(B, tb);
         if (is_last(tb)) break;
         tb = advance(ta);
         issue(tb, B);
-        wait_rows2<16>(Cb);
+        wait_rows<16 * K / 2, K>(Cb);
         process(Cb, tc);
         if (is_last(tc)) break;
     }
@@ -811,6 +840,8 @@ static uint32_t pick_fpw(size_t n, uint32_t R) {
     return fpw;
 }
 
+constexpr int kRegularChains = 2;
+
 static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size_t)kWaves * fpw - 1) / ((size_t)kWaves * fpw))); }
 
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
@@ -839,8 +870,8 @@ hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, ui
     if (n == 0) return hipSuccess;
     if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const uint32_t fpw = pick_fpw(n, (uint32_t)(frag_len / kRowBytes));
-    hipLaunchKernelGGL(crc_regular_kernel<0>, grid_for(n, fpw), dim3(kBlock), 0, s, base, (uint32_t)n, fpw, frag_len,
-                       partial, img, out);
+    hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains>), grid_for(n, fpw), dim3(kBlock), 0, s, base, (uint32_t)n,
+                       fpw, frag_len, partial, img, out);
     return hipGetLastError();
 }
 

@@ -20,6 +20,29 @@
 
 using namespace lampi;
 
+struct NoPre {
+    __device__ void operator()() const {}
+};
+
+// staging cost probes: kind 0 = full stage_tables, 1 = launch + one LDS write (floor)
+template <int kKind>
+__global__ void __launch_bounds__(kBlock) stage_only(const uint32_t *__restrict__ img, uint32_t *out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    if (kKind == 0) {
+        stage_tables<0>(lds, img, [] {});
+    } else if (kKind == 2) {
+        stage_tables<0, NoPre, 0>(lds, img, NoPre{});  // basis loads + barrier only
+    } else if (kKind == 3) {
+        stage_tables<0, NoPre, 1>(lds, img, NoPre{});  // + slicing tables
+    } else if (kKind == 4) {
+        stage_tables<0, NoPre, 2>(lds, img, NoPre{});  // + combine tables only
+    } else {
+        lds[threadIdx.x] = threadIdx.x;
+        __syncthreads();
+    }
+    if (lds[(threadIdx.x * 97) & 16383] == 0x9E3779B9u) out[0] = 1;
+}
+
 int main(int argc, char **argv) {
     const size_t bytes = argc > 1 ? strtoull(argv[1], 0, 0) : (16ull << 30);
     std::vector<uint32_t> img = build_table_image();
@@ -35,21 +58,42 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const char *names[3] = {"product", "loads-only", "lookups-only"};
+    for (int kind = 0; kind < 5; ++kind) {
+        for (int nwg : {65536}) {
+            auto go = [&] {
+                if (kind == 0) hipLaunchKernelGGL(stage_only<0>, dim3(nwg), dim3(kBlock), 0, 0, dimg, out);
+                else if (kind == 1) hipLaunchKernelGGL(stage_only<1>, dim3(nwg), dim3(kBlock), 0, 0, dimg, out);
+                else if (kind == 2) hipLaunchKernelGGL(stage_only<2>, dim3(nwg), dim3(kBlock), 0, 0, dimg, out);
+                else if (kind == 3) hipLaunchKernelGGL(stage_only<3>, dim3(nwg), dim3(kBlock), 0, 0, dimg, out);
+                else hipLaunchKernelGGL(stage_only<4>, dim3(nwg), dim3(kBlock), 0, 0, dimg, out);
+            };
+            go();
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0));
+            for (int r = 0; r < 10; ++r) go();
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("stage_only kind=%d wgs=%d: %.3f ms per launch = %.2f us per WG-slot (512 slots)\n", kind, nwg,
+                   ms / 10, ms / 10 * 1e3 * 512 / nwg);
+        }
+    }
+    if (argc > 2) return 0;  // probes only
     for (size_t L : {4096ul, 16384ul}) {
         const uint32_t n = (uint32_t)(bytes / L);
-        for (uint32_t fpw : {8u, 16u, 32u, 64u}) {
+        for (int chains : {2, 4})
+        for (uint32_t fpw : {8u, 16u, 32u}) {
             const dim3 grid((n + kWaves * fpw - 1) / (kWaves * fpw));
             for (int v = 0; v < 3; ++v) {
                 auto launch = [&] {
-                    if (v == 0)
-                        hipLaunchKernelGGL(crc_regular_kernel<0>, grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu,
-                                           dimg, out);
-                    else if (v == 1)
-                        hipLaunchKernelGGL(crc_regular_kernel<1>, grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu,
-                                           dimg, out);
-                    else
-                        hipLaunchKernelGGL(crc_regular_kernel<2>, grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu,
-                                           dimg, out);
+#define LK(V, K) hipLaunchKernelGGL((crc_regular_kernel<V, K>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu, dimg, out)
+                    if (chains == 2) {
+                        if (v == 0) LK(0, 2); else if (v == 1) LK(1, 2); else LK(2, 2);
+                    } else {
+                        if (v == 0) LK(0, 4); else if (v == 1) LK(1, 4); else LK(2, 4);
+                    }
+#undef LK
                 };
                 launch();
                 CK(hipDeviceSynchronize());
@@ -61,9 +105,10 @@ int main(int argc, char **argv) {
                 float ms;
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 const double s = ms / 1e3 / reps;
-                printf("L=%5zu fpw=%2u %-13s grid=%6u  %8.3f ms  %8.1f GB/s  %5.1f%% of 8 TB/s\n", L, fpw, names[v],
+                printf("K=%d L=%5zu fpw=%2u %-13s grid=%6u  %8.3f ms  %8.1f GB/s  %5.1f%% of 8 TB/s\n", chains, L, fpw, names[v],
                        grid.x, s * 1e3, bytes / s / 1e9, bytes / s / 8e12 * 100);
                 fflush(stdout);
+                (void)0;
             }
         }
     }

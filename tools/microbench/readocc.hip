@@ -46,6 +46,34 @@ __global__ void rd_il(const u32x4 *__restrict__ p, unsigned nfrag, unsigned fpw,
     if (acc == 0x9E3779B9u) out[0] = acc + lds[0];
 }
 
+// XCD-grouped: workgroups 8g..8g+7 (one per XCD under round-robin dispatch) read adjacent
+// 16 KiB blocks at every step; step i of workgroup b reads block (b>>3)*8*fpw + 8i + (b&7)
+template <int kDepth>
+__global__ void rd_xg(const u32x4 *__restrict__ p, unsigned nfrag, unsigned fpw, unsigned *out) {
+    extern __shared__ unsigned lds[];
+    const unsigned lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+    if (threadIdx.x == 0) lds[0] = blockIdx.x;
+    unsigned acc = 0;
+    const unsigned b = blockIdx.x;
+    const unsigned blk0 = (b >> 3) * 8 * fpw + (b & 7);
+    for (unsigned i = 0; i < fpw; i += kDepth) {
+        u32x4 v[kDepth][4];
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d) {
+            unsigned f = (blk0 + 8 * (i + d)) * 4 + wib;
+            if (f >= nfrag || i + d >= fpw) f = 0;
+            const u32x4 *q = p + (size_t)f * 256 + lane * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[d][k] = q[k];
+        }
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc ^= v[d][k].x ^ v[d][k].y ^ v[d][k].z ^ v[d][k].w;
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc + lds[0];
+}
+
 template <int kDepth>
 __global__ void rd(const u32x4 *__restrict__ p, unsigned nfrag, unsigned fpw, unsigned *out) {
     extern __shared__ unsigned lds[];
@@ -92,18 +120,29 @@ int main(int argc, char **argv) {
         int depth;
         bool il;
         bool nt;
+        bool xg;
     };
     const Cfg cfgs[] = {
-        {256, 1, 0, 1, false, false},     {256, 16, 40960, 2, true, false}, {256, 16, 40960, 2, true, true},
-        {256, 1, 0, 1, true, true},       {256, 4, 40960, 1, true, true},   {256, 16, 40960, 1, true, true},
-        {256, 32, 40960, 2, true, true},  {256, 16, 65536, 2, true, true},  {256, 16, 65536, 3, true, true},
-        {256, 16, 65536, 4, true, true},  {256, 16, 65536, 3, true, false}, {256, 16, 32768, 2, true, true},
-        {256, 16, 53248, 3, true, true},  {192, 16, 40960, 2, true, true},  {320, 16, 40960, 2, true, true},
+        {256, 1, 0, 1, false, false, false},     {256, 1, 65536, 1, false, false, false},
+        {256, 1, 40960, 1, false, false, false}, {128, 1, 0, 1, false, false, false},
+        {256, 2, 65536, 2, true, false, false},  {256, 2, 0, 2, true, false, false},
+        {256, 4, 65536, 4, true, false, false},  {256, 4, 0, 4, true, false, false},
+        {256, 8, 65536, 4, true, false, false},  {256, 16, 65536, 2, true, false, false},
+        {256, 16, 65536, 4, true, false, false}, {512, 4, 65536, 4, true, false, false},
     };
     for (const Cfg &c : cfgs) {
         const unsigned wpb = c.block / 64;
         const unsigned grid = (nfrag + wpb * c.fpw - 1) / (wpb * c.fpw);
         auto launch = [&] {
+            if (c.xg) {
+                if (c.depth == 2)
+                    hipLaunchKernelGGL(rd_xg<2>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
+                else if (c.depth == 3)
+                    hipLaunchKernelGGL(rd_xg<3>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
+                else
+                    hipLaunchKernelGGL(rd_xg<4>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
+                return;
+            }
             if (c.il && c.nt) {
                 if (c.depth == 1)
                     hipLaunchKernelGGL((rd_il<1, true>), dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
@@ -120,8 +159,10 @@ int main(int argc, char **argv) {
                     hipLaunchKernelGGL(rd_il<1>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
                 else if (c.depth == 2)
                     hipLaunchKernelGGL(rd_il<2>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
-                else
+                else if (c.depth == 3)
                     hipLaunchKernelGGL(rd_il<3>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
+                else
+                    hipLaunchKernelGGL(rd_il<4>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
                 return;
             }
             if (c.depth == 1)
@@ -141,7 +182,7 @@ int main(int argc, char **argv) {
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double s = ms / 1e3 / reps;
-        printf("%s%s block=%4d fpw=%3u lds=%6d depth=%d grid=%7u  %7.3f ms  %7.1f GB/s (%5.1f%%)\n", c.il ? "IL " : "SEQ", c.nt ? "nt" : "  ",
+        printf("%s%s block=%4d fpw=%3u lds=%6d depth=%d grid=%7u  %7.3f ms  %7.1f GB/s (%5.1f%%)\n", c.xg ? "XG " : c.il ? "IL " : "SEQ", c.nt ? "nt" : "  ",
                c.block, c.fpw, c.lds, c.depth, grid, s * 1e3, bytes / s / 1e9, bytes / s / 8e10);
         fflush(stdout);
     }
