@@ -40,7 +40,10 @@ GIB = float(1 << 30)
 GOLDEN = {
     (2, 4194304, 4096): (0x959621BB, 0xC38D8899),
     (1, 1048576, 1024): (0xFEB61101, 0x41FADF13),
+    (3, 33554432, 16384): (0xF2A5DDAD, 0x3383EB2F),
 }
+# CRC XOR of GPU g's shard (k = g mod 8), 8 GPUs
+CONFIG_D_SHARD_XOR = [0x54862C49, 0x046DA633, 0x53ABB493, 0xEB1A2E44, 0xB9EACC67, 0x0BEC3926, 0x937B2402, 0x3B821C43]
 
 
 def parse():
@@ -54,6 +57,9 @@ def parse():
     ap.add_argument("--mode", choices=["crc", "sum"], default="crc")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-bytes", type=int, default=1 << 30)
+    ap.add_argument("--config", choices=["B", "D"], default="B",
+                    help="B: 4M x 4 KiB per GPU, seed 2 (default, weak scaling); "
+                         "D: 32M x 16 KiB over N GPUs, seed 3 (BASELINE config D, N >= 2)")
     ap.add_argument("--e2e", action="store_true", help="host-memory end-to-end path (config E)")
     return ap.parse_args()
 
@@ -144,10 +150,14 @@ def run_device(args):
     import torch
 
     from lampi_amd import device as dv
-    from oracle.oracle import Restatement, digest
+    from oracle.oracle import Restatement
 
     rank, world, _ = dist_setup()
     n, L = args.frags, args.frag_bytes
+    if args.config == "D":
+        if world < 2:
+            raise SystemExit("config D (512 GiB) needs N >= 2 GPUs")
+        n, L, args.seed = 33554432 // world, 16384, 3
     mode = dv.CRC32 if args.mode == "crc" else dv.SUM32
     stream = torch.cuda.current_stream()
 
@@ -181,10 +191,16 @@ def run_device(args):
     gk = np.arange(n, dtype=np.uint64) * world + rank
     key = (args.seed, n * world, L)
     parity = {}
-    if world == 1 and key in GOLDEN and mode == dv.CRC32:
-        x, s = digest(vals, gk)
-        parity = {"check": "full digest vs BASELINE.md", "xor": f"{x:08x}", "wsum": f"{s:08x}",
-                  "ok": (x, s) == GOLDEN[key]}
+    if key in GOLDEN and mode == dv.CRC32:
+        from lampi_amd import shard
+
+        local = shard.digest(vals, gk)
+        whole = shard.allreduce_digest(local) if world > 1 else local
+        ok = whole == GOLDEN[key]
+        if args.config == "D" and world == 8:
+            ok = ok and local[0] == CONFIG_D_SHARD_XOR[rank]
+        parity = {"check": "full digest vs BASELINE.md" + (" (per-GPU shard XOR too)" if world == 8 else ""),
+                  "xor": f"{whole[0]:08x}", "wsum": f"{whole[1]:08x}", "ok": ok}
     else:
         rng = np.random.default_rng(rank)
         idx = np.unique(np.concatenate([np.arange(min(n, 512)), rng.integers(0, n, 512)]))

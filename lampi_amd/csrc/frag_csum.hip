@@ -685,6 +685,37 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
     }
 }
 
+// SUM fast path for regular batches (frag_len % 4096 == 0, 16-byte aligned base): no tables,
+// hence no staging, so it uses the fastest measured read shape -- one fragment per wave,
+// short-lived 256-thread workgroups in address order, up to four rows (16 x dwordx4 per
+// lane) in flight at once.
+__global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
+                                                             size_t frag_len, uint32_t *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t f = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
+    if (f >= n) return;
+    const uint32_t R = (uint32_t)(frag_len / kRowBytes);
+    gbyte *p = (gbyte *)(base + (uint64_t)f * frag_len + (uint64_t)lane * kLaneBytes);
+    uint32_t acc = 0;
+    uint32_t r = 0;
+    for (; r + 4 <= R; r += 4) {
+        u32x4 v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)(r + k / 4) * kRowBytes + 16 * (k & 3));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+    }
+    for (; r < R; ++r) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)r * kRowBytes + 16 * k);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+    }
+    acc = wave_add(acc);
+    if (lane == 0) out[f] = acc;
+}
+
 // ---- synthetic stream fill ----------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z ^= z >> 30;
@@ -887,6 +918,12 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
                           hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
+    if (msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 && ((uintptr_t)base & 15u) == 0 &&
+        n <= 0xFFFFFFFFull) {
+        hipLaunchKernelGGL(sum_regular_kernel, dim3((unsigned)((n + kWaves - 1) / kWaves)), dim3(kBlock), 0, s, base,
+                           (uint32_t)n, frag_len, out);
+        return hipGetLastError();
+    }
     const uint32_t fpw = pick_fpw(n, 1);
     hipLaunchKernelGGL(sum_rows_kernel<MsgSource>, grid_for(n, fpw), dim3(kBlock), 0, s,
                        MsgSource{base, msg_len, frag_len, 0u}, n, fpw, out);

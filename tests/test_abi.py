@@ -88,3 +88,40 @@ def test_host_entry_points_fail_loudly_without_gpu():
     if r.returncode == 0:
         pytest.fail(f"host path returned without a GPU: {r.stdout!r}")
     assert "no CPU fallback" in r.stderr or r.returncode != 0
+
+
+def test_reference_callers_compile_against_dropin_header(tmp_path):
+    """Code written against the reference's MemFunctions.h overloads compiles and links
+    against include/lampi/MemFunctions.h + liblampi_csum.so."""
+    import lampi_amd
+
+    src = tmp_path / "caller.cc"
+    src.write_text(r'''
+#include "lampi/MemFunctions.h"
+// the shapes of the src/path call sites (gm/sendFrag.cc:147-217, gm/recvFrag.h:165-182)
+unsigned int send_contig(const void *s, void *d, unsigned long n) { return bcopy_uicrc(s, d, n, n); }
+unsigned int send_typemap(const void *s, void *d, unsigned long n) {
+    unsigned int csum = 0, ui1 = 0, ui2 = 0;
+    csum = bcopy_uicrc(s, d, n, n, CRC_INITIAL_REGISTER);
+    csum += bcopy_uicsum(s, d, n, n, &ui1, &ui2);
+    return csum + uicsum(s, n) + uicsum(s, n, &ui1, &ui2) + uicrc(s, n) + uicrc(s, n, csum) +
+           bcopy_uicsum(s, d, n, n);
+}
+int main(int argc, char **) { return argc > 5 ? (int)send_contig(0, 0, 0) : 0; }
+''')
+    c_src = tmp_path / "caller.c"
+    c_src.write_text(r'''
+#include "lampi_csum.h"
+int main(void) {
+    lampi_frag_desc d = {0, 0, LAMPI_CRC_INITIAL_REGISTER};
+    (void)d;
+    return (int)(sizeof(lampi_frag_desc) != 16);
+}
+''')
+    libdir = os.path.dirname(lampi_amd._lib.LIB_PATH)
+    inc = os.path.join(ROOT, "include")
+    subprocess.run(["g++", "-std=c++11", "-Wall", "-Werror", "-I", inc, str(src), "-L", libdir, "-llampi_csum",
+                    "-o", str(tmp_path / "caller")], check=True)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", inc, str(c_src), "-o", str(tmp_path / "cc")],
+                   check=True)
+    assert subprocess.run([str(tmp_path / "cc")]).returncode == 0
