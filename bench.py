@@ -57,8 +57,9 @@ def parse():
     ap.add_argument("--mode", choices=["crc", "sum"], default="crc")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-bytes", type=int, default=1 << 30)
-    ap.add_argument("--config", choices=["B", "D"], default="B",
+    ap.add_argument("--config", choices=["B", "C", "D"], default="B",
                     help="B: 4M x 4 KiB per GPU, seed 2 (default, weak scaling); "
+                         "C: mixed 64 B - 64 KiB Zipf sizes, >= 4 GiB, seed 5 (1 GPU, descriptor batch); "
                          "D: 32M x 16 KiB over N GPUs, seed 3 (BASELINE config D, N >= 2)")
     ap.add_argument("--e2e", action="store_true", help="host-memory end-to-end path (config E)")
     return ap.parse_args()
@@ -256,6 +257,57 @@ def run_device(args):
     return rank, world, result
 
 
+def run_mixed(args):
+    """Config C: one descriptor batch of Zipf-sized fragments packed back to back (seed 5)."""
+    import numpy as np
+    import torch
+
+    from lampi_amd import device as dv
+    from oracle.oracle import Restatement, digest
+
+    rank, world, _ = dist_setup()
+    if world != 1:
+        raise SystemExit("config C is a single-GPU configuration")
+    ref = Restatement()
+    lens = ref.zipf_lengths(4 << 30)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum(dtype=np.uint64))
+    buf = torch.empty(total, dtype=torch.uint8, device="cuda")
+    dv.fill_stream(buf, seed=5)
+    descs = dv.make_descs(buf, offs, lens)
+    out = torch.empty(lens.size, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        dv.frag_csum_batch(descs, mode=dv.CRC32, out=out)
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(args.steps):
+        dv.frag_csum_batch(descs, mode=dv.CRC32, out=out)
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_avg_s = sum(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) / args.steps / 1e3
+    with open(os.path.join(ROOT, "tests", "golden", "fixtures.json")) as f:
+        gold = json.load(f)["digests"]["C"]
+    got = digest(dv.as_u32(out))
+    achieved = total / kern_avg_s / 1e9
+    print(json.dumps({
+        "metric": METRIC, "value": round(total / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: splitmix64 stream seed 5, Zipf(1.1) lengths 64 B..64 KiB (SURVEY.md 8(d))",
+        "config": {"workload": f"config C: {lens.size} mixed fragments, {total} B, descriptor batch, "
+                               "one wavefront per fragment", "fragments": int(lens.size), "bytes": total},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "crc_rows_kernel",
+                     "kernel_avg_ms": round(kern_avg_s * 1e3, 4), "algorithmic_bytes_per_launch": total},
+        "parity": {"check": "full digest vs tests/golden/fixtures.json (config C)", "xor": f"{got[0]:08x}",
+                   "wsum": f"{got[1]:08x}", "ok": got == (gold["crc_xor"], gold["crc_wsum"])},
+        "cpu_baseline": None}))
+
+
 def run_e2e(args):
     """Config E: 256 MiB message in pinned host memory -> H2D (copy stream) -> CRC per
     fragment (compute stream) -> D2H of the u32 array, chunked and overlapped."""
@@ -331,6 +383,9 @@ def main():
     args = parse()
     if args.e2e:
         run_e2e(args)
+        return
+    if args.config == "C":
+        run_mixed(args)
         return
     rank, world, result = run_device(args)
     if rank == 0:

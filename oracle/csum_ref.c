@@ -10,6 +10,7 @@
 #include <string.h>
 #include <time.h>
 #include <stdlib.h>
+#include <math.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -287,4 +288,42 @@ double oracle_time_fn(void *fn, const uint8_t *buf, size_t n, size_t L, int nthr
     double t1 = now_s();
     if (xor_out) *xor_out = x;
     return t1 - t0;
+}
+
+/* ---- config C: mixed fragment sizes ---------------------------------------
+ * Length of fragment k = 64*r bytes, r in [1, 1024] drawn Zipf(s = 1.1) by inverse CDF from
+ * the counter-based uniform u_k = (mix(0x5A1F + k) >> 11) * 2^-53.  Fragments are packed
+ * back to back (64-byte aligned, since every length is a multiple of 64) until the total
+ * reaches min_total bytes.  Returns the number of fragments; writes up to cap lengths. */
+size_t oracle_zipf_lengths(uint64_t min_total, size_t cap, uint32_t *len_out)
+{
+    static double cdf[1025];
+    static int ready = 0;
+    if (!ready) {
+        double z = 0.0;
+        for (int r = 1; r <= 1024; ++r) z += pow((double)r, -1.1);
+        double acc = 0.0;
+        cdf[0] = 0.0;
+        for (int r = 1; r <= 1024; ++r) {
+            acc += pow((double)r, -1.1) / z;
+            cdf[r] = acc;
+        }
+        cdf[1024] = 1.0;
+        ready = 1;
+    }
+    uint64_t total = 0;
+    size_t k = 0;
+    while (total < min_total) {
+        double u = (double)(mix64(0x5A1Full + k) >> 11) * (1.0 / 9007199254740992.0);
+        int lo = 1, hi = 1024;  /* smallest r with cdf[r] > u */
+        while (lo < hi) {
+            int mid = (lo + hi) / 2;
+            if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+        }
+        uint32_t L = 64u * (uint32_t)lo;
+        if (k < cap && len_out) len_out[k] = L;
+        total += L;
+        ++k;
+    }
+    return k;
 }

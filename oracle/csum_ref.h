@@ -79,6 +79,10 @@ void oracle_desc_batch(const uint8_t *base, const uint64_t *off, const uint32_t 
 double oracle_time_uniform(uint64_t seed, size_t n, size_t L, int mode, int nthreads,
                            uint32_t *xor_out);
 
+/* Config C: Zipf(1.1) lengths 64*r, r in [1,1024], from u_k = mix(0x5A1F+k)>>11,
+ * packed until the total reaches min_total.  Returns the count; writes up to cap lengths. */
+size_t oracle_zipf_lengths(uint64_t min_total, size_t cap, uint32_t *len_out);
+
 /* Time a uicrc-shaped function pointer over n fragments of L bytes of buf (see .c). */
 double oracle_time_fn(void *fn, const uint8_t *buf, size_t n, size_t L, int nthreads, uint32_t *xor_out);
 

@@ -90,6 +90,8 @@ class Restatement(_Api):
                                           ctypes.c_int, _vp]
         L.oracle_time_fn.restype = ctypes.c_double
         L.oracle_time_fn.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, _vp]
+        L.oracle_zipf_lengths.restype = ctypes.c_size_t
+        L.oracle_zipf_lengths.argtypes = [ctypes.c_uint64, ctypes.c_size_t, _vp]
         L.oracle_header_checksum.restype = _u
         L.oracle_header_checksum.argtypes = [_vp, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
 
@@ -134,6 +136,13 @@ class Restatement(_Api):
 
     def uicrc_addr(self) -> int:
         return ctypes.cast(self.lib.oracle_uicrc, ctypes.c_void_p).value
+
+    def zipf_lengths(self, min_total: int) -> np.ndarray:
+        """Config C fragment lengths, packed until the total >= min_total."""
+        n = int(self.lib.oracle_zipf_lengths(min_total, 0, None))
+        out = np.empty(n, dtype=np.uint32)
+        self.lib.oracle_zipf_lengths(min_total, n, out.ctypes.data)
+        return out
 
     def header_checksum(self, hdr, crclen: int, word_count: int, usecrc: bool) -> int:
         p, _ = _buf(hdr)

@@ -160,6 +160,27 @@ def main():
                           "D per-GPU shard XORs are BASELINE.md's (not regenerated here)")
     fx["config_d_shard_xor"] = [0x54862C49, 0x046DA633, 0x53ABB493, 0xEB1A2E44, 0xB9EACC67, 0x0BEC3926,
                                 0x937B2402, 0x3B821C43]
+    # config C (mixed Zipf sizes, seed 5, >= 4 GiB) and config E (256 MiB message, seed 6):
+    # restatement-generated (its parity with the reference is pinned by everything above)
+    lens = port.zipf_lengths(4 << 30)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(lens.sum(dtype=np.uint64))
+    stream = port.stream(5, 0, total)
+    crc_c = port.desc_batch(stream, offs, lens, None, 0)
+    sum_c = port.desc_batch(stream, offs, lens, None, 1)
+    del stream
+    cx, cw = digest(crc_c)
+    digs["C"] = {"seed": 5, "n": int(lens.size), "total_bytes": total, "crc_xor": cx, "crc_wsum": cw,
+                 "sum_total": int(np.sum(sum_c, dtype=np.uint64) & 0xFFFFFFFF), "sum_wsum": digest(sum_c)[1],
+                 "len_sum_check": int(lens[:1000].sum()), "crc_first4": [int(v) for v in crc_c[:4]]}
+    msg = port.stream(6, 0, 256 << 20)
+    digs["E"] = {"seed": 6, "msg_bytes": 256 << 20}
+    for L in (4096, 16384, 65456):
+        nf = ((256 << 20) + L - 1) // L
+        o = np.arange(nf, dtype=np.uint64) * L
+        ln = np.minimum(L, (256 << 20) - o).astype(np.uint32)
+        v = port.desc_batch(msg, o, ln, None, 0)
+        digs["E"][str(L)] = {"n": int(nf), "crc_xor": digest(v)[0], "crc_wsum": digest(v)[1]}
     print(f"digests in {time.time() - t0:.1f}s")
 
     with open(OUT, "w") as f:

@@ -224,3 +224,51 @@ def test_header_checksum_residue(cuda, oracle):
             assert la.uicrc(hdr, hl) == 0
             assert la.header_checksum(hdr, hl - 4, words, usecrc=False) == oracle.header_checksum(
                 hdr, hl - 4, words, False)
+
+
+def test_config_c_mixed_sizes_full_digest(cuda, oracle):
+    """BASELINE config C: 659,114 Zipf-sized fragments (64 B..64 KiB, 4 GiB) as one descriptor
+    batch; digest from tests/golden/fixtures.json (restatement, pinned to the reference)."""
+    import json
+    import os
+
+    import torch
+
+    from oracle.oracle import digest
+
+    dv = _dv()
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fixtures.json")) as f:
+        gold = json.load(f)["digests"]["C"]
+    lens = oracle.zipf_lengths(4 << 30)
+    assert lens.size == gold["n"] and int(lens.sum(dtype=np.uint64)) == gold["total_bytes"]
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    buf = torch.empty(gold["total_bytes"], dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=5)
+    descs = dv.make_descs(buf, offs, lens)
+    crc = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.CRC32))
+    assert [int(v) for v in crc[:4]] == gold["crc_first4"]
+    assert digest(crc) == (gold["crc_xor"], gold["crc_wsum"])
+    s = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.SUM32))
+    assert (int(np.sum(s, dtype=np.uint64) & 0xFFFFFFFF), digest(s)[1]) == (gold["sum_total"], gold["sum_wsum"])
+    del buf
+    torch.cuda.empty_cache()
+
+
+def test_config_e_message_digests(cuda):
+    """BASELINE config E: 256 MiB message (seed 6) fragmented at 4 KiB, 16 KiB and the GM payload size."""
+    import json
+    import os
+
+    import torch
+
+    from oracle.oracle import digest
+
+    dv = _dv()
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fixtures.json")) as f:
+        gold = json.load(f)["digests"]["E"]
+    msg = torch.empty(256 << 20, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(msg, seed=6)
+    for L in (4096, 16384, 65456):
+        crc = dv.as_u32(dv.msg_csum(msg, L))
+        assert crc.size == gold[str(L)]["n"]
+        assert digest(crc) == (gold[str(L)]["crc_xor"], gold[str(L)]["crc_wsum"]), L

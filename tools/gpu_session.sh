@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
-#   smoke | tests | bench | prof | pmc | e2e | bench16k | microbench
+#   smoke | tests | bench | bench16k | benchsum | benchC | prof | pmc | e2e | microbench
 # A test failure (exit 1) lets later steps run; a fault, abort, segfault, timeout or
 # kill (exit >= 124, 134, 139, ...) ends the session immediately.
 set -u
@@ -30,6 +30,7 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     bench16k) run bench16k 600 python bench.py --frags 1048576 --frag-bytes 16384 --no-cpu-baseline ;;
     benchsum) run benchsum 600 python bench.py --mode sum --no-cpu-baseline ;;
+    benchC) run benchC 600 python bench.py --config C --steps 10 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
             -- python3 bench.py --steps 10 --no-cpu-baseline ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \

@@ -74,6 +74,32 @@ __global__ void rd_xg(const u32x4 *__restrict__ p, unsigned nfrag, unsigned fpw,
     if (acc == 0x9E3779B9u) out[0] = acc + lds[0];
 }
 
+// grid-stride non-persistent: step i of workgroup b reads 16 KiB chunk b + i*gridDim.x
+template <int kDepth>
+__global__ void rd_gs(const u32x4 *__restrict__ p, unsigned nfrag, unsigned fpw, unsigned *out) {
+    extern __shared__ unsigned lds[];
+    const unsigned lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+    if (threadIdx.x == 0) lds[0] = blockIdx.x;
+    unsigned acc = 0;
+    const unsigned wpb = blockDim.x >> 6;
+    for (unsigned i = 0; i < fpw; i += kDepth) {
+        u32x4 v[kDepth][4];
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d) {
+            unsigned f = (blockIdx.x + (i + d) * gridDim.x) * wpb + wib;
+            if (f >= nfrag || i + d >= fpw) f = 0;
+            const u32x4 *q = p + (size_t)f * 256 + lane * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[d][k] = q[k];
+        }
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc ^= v[d][k].x ^ v[d][k].y ^ v[d][k].z ^ v[d][k].w;
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc + lds[0];
+}
+
 template <int kDepth>
 __global__ void rd(const u32x4 *__restrict__ p, unsigned nfrag, unsigned fpw, unsigned *out) {
     extern __shared__ unsigned lds[];
@@ -123,17 +149,23 @@ int main(int argc, char **argv) {
         bool xg;
     };
     const Cfg cfgs[] = {
-        {256, 1, 0, 1, false, false, false},     {256, 1, 65536, 1, false, false, false},
-        {256, 1, 40960, 1, false, false, false}, {128, 1, 0, 1, false, false, false},
-        {256, 2, 65536, 2, true, false, false},  {256, 2, 0, 2, true, false, false},
-        {256, 4, 65536, 4, true, false, false},  {256, 4, 0, 4, true, false, false},
-        {256, 8, 65536, 4, true, false, false},  {256, 16, 65536, 2, true, false, false},
-        {256, 16, 65536, 4, true, false, false}, {512, 4, 65536, 4, true, false, false},
+        {256, 1, 0, 1, false, false, false},      {256, 1, 65536, 1, false, false, false},
+        {256, 16, 65536, 4, true, false, false},  {256, 32, 65536, 4, true, false, false},
+        {256, 8, 65536, 4, false, true, false},   {256, 16, 65536, 4, false, true, false},
+        {256, 32, 65536, 4, false, true, false},  {256, 64, 65536, 4, false, true, false},
+        {256, 32, 65536, 2, false, true, false},  {256, 16, 0, 4, false, true, false},
     };
     for (const Cfg &c : cfgs) {
         const unsigned wpb = c.block / 64;
         const unsigned grid = (nfrag + wpb * c.fpw - 1) / (wpb * c.fpw);
         auto launch = [&] {
+            if (!c.il && c.nt) {
+                if (c.depth == 2)
+                    hipLaunchKernelGGL(rd_gs<2>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
+                else
+                    hipLaunchKernelGGL(rd_gs<4>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
+                return;
+            }
             if (c.xg) {
                 if (c.depth == 2)
                     hipLaunchKernelGGL(rd_xg<2>, dim3(grid), dim3(c.block), c.lds, 0, (const u32x4 *)buf, nfrag, c.fpw, out);
@@ -182,7 +214,7 @@ int main(int argc, char **argv) {
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double s = ms / 1e3 / reps;
-        printf("%s%s block=%4d fpw=%3u lds=%6d depth=%d grid=%7u  %7.3f ms  %7.1f GB/s (%5.1f%%)\n", c.xg ? "XG " : c.il ? "IL " : "SEQ", c.nt ? "nt" : "  ",
+        printf("%s%s block=%4d fpw=%3u lds=%6d depth=%d grid=%7u  %7.3f ms  %7.1f GB/s (%5.1f%%)\n", c.xg ? "XG " : c.il ? "IL " : (c.nt ? "GS " : "SEQ"), (c.il && c.nt) ? "nt" : "  ",
                c.block, c.fpw, c.lds, c.depth, grid, s * 1e3, bytes / s / 1e9, bytes / s / 8e10);
         fflush(stdout);
     }
