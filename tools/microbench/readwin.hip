@@ -104,6 +104,49 @@ __global__ void __launch_bounds__(256) rd_tk(const u32x4 *__restrict__ p, unsign
     if (acc == 0x9E3779B9u) out[0] = acc + lds[0];
 }
 
+// per-wave tickets, kLook grabs in flight: ticket = `cpw` consecutive fragments; queue q
+// (the wave's XCD) hands out chunks q, q+8, ... so all XCDs sweep one window together
+template <int kLook>
+__global__ void __launch_bounds__(256) rd_tw(const u32x4 *__restrict__ p, unsigned nfrag, unsigned cpw, unsigned *q,
+                                             unsigned *out) {
+    extern __shared__ unsigned lds[];
+    const unsigned lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) lds[0] = blockIdx.x;
+    const unsigned nchunk = (nfrag + cpw - 1) / cpw;
+    const unsigned home = xcc_id();
+    unsigned tk[kLook];
+#pragma unroll
+    for (int i = 0; i < kLook; ++i) {
+        unsigned g = 0;
+        if (lane == 0) g = take(q, nchunk, home);
+        tk[i] = __builtin_amdgcn_readfirstlane(g);
+    }
+    unsigned acc = 0;
+    for (;;) {
+        const unsigned cur = tk[0];
+        if (cur >= nchunk) break;
+#pragma unroll
+        for (int i = 0; i + 1 < kLook; ++i) tk[i] = tk[i + 1];
+        unsigned g = 0;
+        if (lane == 0) g = take(q, nchunk, home);
+        tk[kLook - 1] = __builtin_amdgcn_readfirstlane(g);
+        const unsigned f0 = cur * cpw;
+        for (unsigned i = 0; i < cpw; i += 2) {
+            unsigned fa = f0 + i, fb = f0 + i + 1;
+            if (fa >= nfrag) fa = f0;
+            if (fb >= nfrag || i + 1 >= cpw) fb = fa;
+            u32x4 v[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = p[(size_t)fa * 256 + lane * 4 + k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[4 + k] = p[(size_t)fb * 256 + lane * 4 + k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+        }
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc + lds[0];
+}
+
 int main(int argc, char **argv) {
     const size_t bytes = argc > 1 ? strtoull(argv[1], 0, 0) : (16ull << 30);
     const unsigned nfrag = (unsigned)(bytes / 4096);
@@ -124,13 +167,20 @@ int main(int argc, char **argv) {
         unsigned cpw;
         int wg_per_cu;
     };
-    const Cfg cfgs[] = {{'P', 4, 2}, {'P', 8, 2}, {'P', 16, 2}, {'P', 4, 1}, {'T', 4, 2},
-                        {'T', 8, 2}, {'T', 16, 2}, {'T', 32, 2}, {'T', 4, 1}};
+    const Cfg cfgs[] = {{'P', 8, 2}, {'2', 4, 2}, {'2', 8, 2}, {'2', 16, 2}, {'4', 4, 2},
+                        {'4', 8, 2}, {'4', 16, 2}, {'4', 8, 8}, {'2', 8, 4}};
     for (const Cfg &c : cfgs) {
         const int grid = cus * c.wg_per_cu;
         auto launch = [&] {
             if (c.mode == 'P') {
                 hipLaunchKernelGGL(rd_ps, dim3(grid), dim3(256), 65536, 0, (const u32x4 *)buf, nfrag, c.cpw, out);
+            } else if (c.mode == '2' || c.mode == '4') {
+                CK(hipMemsetAsync(q, 0, 8 * 32 * 4, 0));
+                const int lds = c.wg_per_cu <= 2 ? 65536 : (c.wg_per_cu <= 4 ? 32768 : 0);
+                if (c.mode == '2')
+                    hipLaunchKernelGGL(rd_tw<2>, dim3(grid), dim3(256), lds, 0, (const u32x4 *)buf, nfrag, c.cpw, q, out);
+                else
+                    hipLaunchKernelGGL(rd_tw<4>, dim3(grid), dim3(256), lds, 0, (const u32x4 *)buf, nfrag, c.cpw, q, out);
             } else {
                 CK(hipMemsetAsync(q, 0, 8 * 32 * 4, 0));
                 hipLaunchKernelGGL(rd_tk, dim3(grid), dim3(256), 65536, 0, (const u32x4 *)buf, nfrag, c.cpw, q, out);
