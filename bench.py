@@ -62,6 +62,8 @@ def parse():
                          "C: mixed 64 B - 64 KiB Zipf sizes, >= 4 GiB, seed 5 (1 GPU, descriptor batch); "
                          "D: 32M x 16 KiB over N GPUs, seed 3 (BASELINE config D, N >= 2)")
     ap.add_argument("--e2e", action="store_true", help="host-memory end-to-end path (config E)")
+    ap.add_argument("--bcopy", action="store_true",
+                    help="fused copy + checksum batch (lampi_frag_bcopy_batch) on the config B shape")
     return ap.parse_args()
 
 
@@ -379,8 +381,96 @@ def run_e2e(args):
                       "pinned_h2d_GiB_per_s": round(h2d, 2), "chunk_bytes": chunk}))
 
 
+def run_bcopy(args):
+    """copy n fragments into a staging array with the checksum fused
+    (bcopy_uicrc / bcopy_uicsum of every fragment).  Roofline bytes = L read + L written.
+    Timed: lampi_msg_bcopy (the value), the same work as a descriptor batch
+    (lampi_frag_bcopy_batch) and torch's own device copy of the bytes (copy reference)."""
+    import numpy as np
+    import torch
+
+    from lampi_amd import device as dv
+    from lampi_amd import shard
+
+    rank, world, _ = dist_setup()
+    if world != 1:
+        raise SystemExit("--bcopy is a single-GPU measurement")
+    n, L = args.frags, args.frag_bytes
+    mode = dv.CRC32 if args.mode == "crc" else dv.SUM32
+    src = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    dv.fill_stream_frags(src, n, L, args.seed)
+    dst = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+    offs = np.arange(n, dtype=np.uint64) * L
+    descs = dv.make_copy_descs(src, offs, dst, offs, np.full(n, L), np.full(n, L))
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        t0 = time.perf_counter()
+        evs[0].record(stream)
+        for i in range(args.steps):
+            fn()
+            evs[i + 1].record(stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        return wall, sum(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) / args.steps / 1e3
+
+    def check(tag):
+        vals = dv.as_u32(out)
+        copy_ok = bool(torch.equal(src, dst))
+        key = (args.seed, n, L)
+        if key in GOLDEN and mode == dv.CRC32:
+            got = shard.digest(vals, np.arange(n, dtype=np.uint64))
+            return {"check": f"{tag}: full digest vs BASELINE.md + copy == source", "xor": f"{got[0]:08x}",
+                    "ok": got == GOLDEN[key] and copy_ok}
+        from oracle.oracle import Restatement
+
+        idx = np.unique(np.random.default_rng(0).integers(0, n, 512))
+        want = np.array([Restatement().uniform_batch(args.seed, int(i), 1, L, mode)[0] for i in idx], np.uint32)
+        return {"check": f"{tag}: {idx.size} sampled fragments vs oracle + copy == source",
+                "ok": bool(np.array_equal(vals[idx], want)) and copy_ok}
+
+    wall, kern = timed(lambda: dv.msg_bcopy(src, L, dst, L, mode=mode, out=out))
+    parity = check("msg_bcopy")
+    dst.zero_()
+    _, kern_desc = timed(lambda: dv.frag_bcopy_batch(descs, mode=mode, out=out))
+    parity_desc = check("frag_bcopy_batch")
+    _, kern_copy = timed(lambda: dst.copy_(src))
+    moved = 2.0 * n * L
+    achieved = moved / kern / 1e9
+    kname = ("crc_regular_kernel<copy>" if mode == dv.CRC32 else "sum_regular_kernel<copy>")
+    print(json.dumps({
+        "metric": "device-resident fused copy+checksum GiB/s of payload (bcopy); % of HBM roofline",
+        "value": round(n * L / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic: splitmix64 stream seed {args.seed} (SURVEY.md 8(d)), generated on device",
+        "config": {"workload": f"{n} x {L} B fragments copied into a staging array with the "
+                               f"{'CRC' if mode == dv.CRC32 else 'sum'} fused (lampi_msg_bcopy)",
+                   "fragments": n, "frag_bytes": L},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                     "kernel_avg_ms": round(kern * 1e3, 4), "algorithmic_bytes_per_launch": int(moved),
+                     "note": "algorithmic bytes = payload read + payload written"},
+        "descriptor_batch": {"kernel_avg_ms": round(kern_desc * 1e3, 4),
+                             "achieved_GBs": round(moved / kern_desc / 1e9, 1)},
+        "copy_reference": {"what": "torch dst.copy_(src), same bytes, no checksum",
+                           "kernel_avg_ms": round(kern_copy * 1e3, 4),
+                           "achieved_GBs": round(moved / kern_copy / 1e9, 1)},
+        "parity": {**parity, "descriptor_batch": parity_desc,
+                   "ok_all": bool(parity["ok"] and parity_desc["ok"])},
+        "cpu_baseline": None}))
+
+
 def main():
     args = parse()
+    if args.bcopy:
+        run_bcopy(args)
+        return
     if args.e2e:
         run_e2e(args)
         return

@@ -95,6 +95,35 @@ typedef struct lampi_frag_desc {
 int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out,
                           int mode, void *stream);
 
+/* One fused copy + checksum (32 bytes, little-endian): offset 0 src, 8 dst, 16 copylen,
+ * 20 csumlen, 24 partial, 28 reserved. */
+typedef struct lampi_copy_desc {
+    uint64_t src;       /* device address of the source fragment (any alignment) */
+    uint64_t dst;       /* device address of the copy (any alignment; must not overlap src) */
+    uint32_t copylen;   /* bytes copied src -> dst */
+    uint32_t csumlen;   /* the checksum covers max(copylen, csumlen) source bytes; the residue
+                           beyond copylen is checksummed but not copied (ref :1266, :1314-1317) */
+    uint32_t partial;   /* CRC mode: starting register; SUM mode: ignored (fresh state) */
+    uint32_t reserved;  /* 0 */
+} lampi_copy_desc;
+
+/* Fused copy + checksum per descriptor: d[i].dst gets the first copylen bytes of d[i].src
+ * (no other destination byte is written) and out[i] the checksum bcopy_uicrc / bcopy_uicsum
+ * would return.  One wavefront per fragment, every source byte read from HBM once.
+ * Replaces the per-fragment bcopy_uicrc/bcopy_uicsum of the send side
+ * (src/path/gm/sendFrag.cc:147-155, ref src/util/MemFunctions.cc:1263-1321, 518-875) and
+ * the receive-side CopyFunction (src/path/gm/recvFrag.h:165-205, copylen < crclen at :174). */
+int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d_out, int mode,
+                           void *stream);
+
+/* Fragments a contiguous device-resident message like lampi_msg_csum and copies fragment k
+ * to d_dst + k*dst_stride (dst_stride >= frag_len; e.g. frag_len for a plain copy, or the
+ * slot size of a staging ring) with its checksum fused: bcopy_uicrc / bcopy_uicsum of every
+ * fragment (copylen = crclen = the fragment length), ref src/path/gm/sendFrag.cc:147-155.
+ * Source and destination must not overlap. */
+int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_dst, size_t dst_stride,
+                    uint32_t partial, uint32_t *d_out, int mode, void *stream);
+
 /* Fragments a contiguous device-resident message the way the path layer does
  * (fragment k = bytes [k*frag_len, min((k+1)*frag_len, msg_len)),
  * src/path/gm/path.cc:98-121) and writes ceil(msg_len/frag_len) checksums to d_out.

@@ -28,6 +28,16 @@ class FragDesc(ctypes.Structure):
 
 assert ctypes.sizeof(FragDesc) == 16
 
+
+class CopyDesc(ctypes.Structure):
+    """struct lampi_copy_desc (32 bytes): src u64, dst u64, copylen, csumlen, partial, reserved u32."""
+
+    _fields_ = [("src", ctypes.c_uint64), ("dst", ctypes.c_uint64), ("copylen", ctypes.c_uint32),
+                ("csumlen", ctypes.c_uint32), ("partial", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(CopyDesc) == 32
+
 _lock = threading.Lock()
 _lib = None
 
@@ -44,6 +54,9 @@ PROTOTYPES = {
     "lampi_uicsum": (c_uint, [c_void_p, c_ulong, PUINT, PUINT]),
     "lampi_bcopy_uicsum": (c_uint, [c_void_p, c_void_p, c_ulong, c_ulong, PUINT, PUINT]),
     "lampi_frag_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
+    "lampi_frag_bcopy_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
+    "lampi_msg_bcopy": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, ctypes.c_uint32, c_void_p,
+                                       ctypes.c_int, c_void_p]),
     "lampi_msg_csum": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, c_void_p, ctypes.c_int,
                                       c_void_p]),
     "lampi_fill_stream": (ctypes.c_int, [c_void_p, c_size_t, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),

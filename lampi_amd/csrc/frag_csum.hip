@@ -57,22 +57,42 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 typedef __attribute__((address_space(1))) const uint32_t guint;
 
+typedef __attribute__((address_space(1))) uint8_t gwbyte;
+typedef __attribute__((address_space(1))) uint32_t gwuint;
+typedef __attribute__((address_space(1))) u32x4 gwu32x4;
+
 struct FragInfo {
     gbyte *addr;
-    uint32_t len;
+    uint32_t len;      // bytes checksummed
     uint32_t partial;
+    uint8_t *dst;      // copy sources only: destination of the first copylen bytes
+    uint32_t copylen;
 };
 
 // ---- fragment sources (wave-uniform) ----------------------------------------------
 struct DescSource {
+    static constexpr bool kCopy = false;
     const lampi_frag_desc *d;
     __device__ FragInfo get(size_t f) const {
         const lampi_frag_desc x = d[f];
-        return {(gbyte *)(uintptr_t)x.addr, x.length, x.partial};
+        return {(gbyte *)(uintptr_t)x.addr, x.length, x.partial, nullptr, 0u};
+    }
+};
+
+// bcopy_uicrc / bcopy_uicsum (ref MemFunctions.cc:1263-1321, 518-875): copy copylen bytes and
+// checksum max(copylen, csumlen) bytes of the source (the residue is checksummed, not copied)
+struct CopySource {
+    static constexpr bool kCopy = true;
+    const lampi_copy_desc *d;
+    __device__ FragInfo get(size_t f) const {
+        const lampi_copy_desc x = d[f];
+        const uint32_t len = x.copylen > x.csumlen ? x.copylen : x.csumlen;
+        return {(gbyte *)(uintptr_t)x.src, len, x.partial, (uint8_t *)(uintptr_t)x.dst, x.copylen};
     }
 };
 
 struct MsgSource {
+    static constexpr bool kCopy = false;
     const uint8_t *base;
     size_t msg_len;
     size_t frag_len;
@@ -80,7 +100,24 @@ struct MsgSource {
     __device__ FragInfo get(size_t f) const {
         size_t off = f * frag_len;
         size_t rem = msg_len - off;
-        return {(gbyte *)(base + off), (uint32_t)(rem < frag_len ? rem : frag_len), partial};
+        return {(gbyte *)(base + off), (uint32_t)(rem < frag_len ? rem : frag_len), partial, nullptr, 0u};
+    }
+};
+
+// fragment k of a contiguous message copied to dst + k*dst_stride (bcopy of every fragment)
+struct MsgCopySource {
+    static constexpr bool kCopy = true;
+    const uint8_t *base;
+    size_t msg_len;
+    size_t frag_len;
+    uint32_t partial;
+    uint8_t *dst;
+    size_t dst_stride;
+    __device__ FragInfo get(size_t f) const {
+        size_t off = f * frag_len;
+        size_t rem = msg_len - off;
+        const uint32_t len = (uint32_t)(rem < frag_len ? rem : frag_len);
+        return {(gbyte *)(base + off), len, partial, dst + f * dst_stride, len};
     }
 };
 
@@ -136,6 +173,21 @@ __device__ __forceinline__ void row_words(const Row &r, uint32_t d[16]) {
         d[4 * k + 2] = r.q[k].z;
         d[4 * k + 3] = r.q[k].w;
     }
+}
+
+// 4 x dwordx4 stores of a lane's 64-byte piece.  Stores count in vmcnt in issue order with
+// the loads (MI355X_MICROARCH.md, s_waitcnt), so the ring's wait counts include them.  The
+// trailing s_nop covers the store-data read hazard before the registers are rewritten.
+__device__ __forceinline__ void store_row(gwbyte *p, const Row &r) {
+    asm volatile(
+        "global_store_dwordx4 %0, %1, off\n\t"
+        "global_store_dwordx4 %0, %2, off offset:16\n\t"
+        "global_store_dwordx4 %0, %3, off offset:32\n\t"
+        "global_store_dwordx4 %0, %4, off offset:48\n\t"
+        "s_nop 1"
+        :
+        : "v"(p), "v"(r.q[0]), "v"(r.q[1]), "v"(r.q[2]), "v"(r.q[3])
+        : "memory");
 }
 
 // ---- LDS table staging --------------------------------------------------------------
@@ -252,6 +304,52 @@ __device__ __forceinline__ void load64(gbyte *frag, long long o, long long lo, l
 #pragma unroll
         for (int w = 0; w < 16; ++w) d[w] &= byte_keep_mask(o + 4 * w, lo, hi);
     }
+}
+
+// ---- stores (fused copy) --------------------------------------------------------------
+// Aligned word at dst + c (c may be negative): whole-word store when all four bytes lie in
+// [0, hi), byte stores for a word straddling an edge, nothing outside.
+__device__ __forceinline__ void store_word(uint8_t *dst, long long c, uint32_t v, long long hi) {
+    if (c >= 0 && c + 4 <= hi) {
+        *(gwuint *)(dst + c) = v;
+    } else if (c + 4 > 0 && c < hi) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (c + j >= 0 && c + j < hi) *(gwbyte *)(dst + c + j) = (uint8_t)(v >> (8 * j));
+    }
+}
+
+// Write the 64 bytes d[16] (fragment bytes [o, o+64)) to dst + o, keeping only bytes in [0, hi).
+// m = (dst + o) & 3 and a16 = ((dst + o) & 15) == 0 are wave-uniform.  For m != 0 a lane writes
+// the aligned words covering [o - m, o - m + 64): their first m bytes are the top of the
+// previous lane's piece (`prev`), and the lane holding the frame's last piece (`tail`) also
+// writes the word at o - m + 64.
+__device__ __forceinline__ void store64(uint8_t *dst, long long o, const uint32_t d[16], long long hi, uint32_t m,
+                                        bool a16, uint32_t prev, bool tail) {
+    if (o - (long long)m >= hi || o + 64 <= 0) return;
+    if (m == 0) {
+        if (a16 && o >= 0 && o + 64 <= hi) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                *(gwu32x4 *)(dst + o + 16 * k) = u32x4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
+            return;
+        }
+#pragma unroll
+        for (int w = 0; w < 16; ++w) store_word(dst, o + 4 * w, d[w], hi);
+        return;
+    }
+    const long long a = o - (long long)m;
+    const uint32_t sh = 4u - m;
+    store_word(dst, a, __builtin_amdgcn_alignbyte(d[0], prev, sh), hi);
+#pragma unroll
+    for (int w = 1; w < 16; ++w) store_word(dst, a + 4 * w, __builtin_amdgcn_alignbyte(d[w], d[w - 1], sh), hi);
+    if (tail) store_word(dst, a + 64, __builtin_amdgcn_alignbyte(0u, d[15], sh), hi);
+}
+
+// d[15] of lane - 1 (lane 0 gets `carry`, the last lane's word of the previous row)
+__device__ __forceinline__ uint32_t prev_lane_top(uint32_t d15, uint32_t carry, int lane) {
+    const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - 1) * 4, (int)d15);
+    return lane == 0 ? carry : v;
 }
 
 // ---- CRC pieces -----------------------------------------------------------------------
@@ -408,6 +506,10 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
             fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
             fi.len = uniform(fi.len);
             fi.partial = uniform(fi.partial);
+            if constexpr (Src::kCopy) {
+                fi.dst = (uint8_t *)uniform64((uint64_t)(uintptr_t)fi.dst);
+                fi.copylen = uniform(fi.copylen);
+            }
             if (fi.len) return x;
             if (lane == 0) out[x] = fi.partial;  // uicrc(p, 0, s) == s
         }
@@ -422,6 +524,7 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
     uint32_t d[16];
     crc_load_row(cur, g, 0, lane, d);
     uint32_t C = 0;
+    uint32_t carry = 0;
 
     for (;;) {
         // prefetch the next row task
@@ -438,6 +541,16 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
         uint32_t nd[16];
         if (more) crc_load_row(nfi, ng, nr, lane, nd);
 
+        if constexpr (Src::kCopy) {  // copy before the partial register is injected
+            if (cur.copylen) {
+                const long long o = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P;
+                const uint32_t dm = (uint32_t)((uintptr_t)cur.dst - g.P) & 15u;
+                if (r == 0) carry = 0;
+                const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
+                store64(cur.dst, o, d, (long long)cur.copylen, dm & 3u, dm == 0, prev, lane == 63 && r + 1 == g.R);
+                carry = __builtin_amdgcn_readlane(d[15], 63);
+            }
+        }
         // process the current row
         if (r == 0) {
             if (g.P == 0) {
@@ -536,11 +649,15 @@ __device__ __forceinline__ void crc_pieces(const uint32_t *lds, const CrcLane &k
 
 // kAblate (tools/microbench/crc_ablation.hip only; the product launches 0):
 //   1 = loads only (words XOR-folded, no table lookups), 2 = lookups only (no global loads)
-template <int kAblate, int kChains>
+// kCopy: fused bcopy -- each row is also stored to dst + f*dst_stride (16-byte aligned) as soon
+// as it arrives; per step the ring then carries 4K stores beside 4K loads, and the waits count
+// them (first pass: 8K / 12K / 16K younger operations, then 16K).
+template <int kAblate, int kChains, bool kCopy = false>
 __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
                                                              uint32_t fpw, size_t frag_len, uint32_t partial,
                                                              const uint32_t *__restrict__ img,
-                                                             uint32_t *__restrict__ out) {
+                                                             uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
+                                                             size_t dst_stride) {
     constexpr int K = kChains;
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
@@ -573,11 +690,14 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
 
     GroupTask ta{0u, 0u};
     GroupTask tb = advance(ta);
+    GroupTask tc = advance(tb);
     RowsK<K> A, B, Cb;
     if (kAblate != 2) {
-        stage_tables<8 * K>(lds, img, [&] {
+        // all three ring slots are in flight while the workgroup builds its tables
+        stage_tables<12 * K>(lds, img, [&] {
             issue(ta, A);
             issue(tb, B);
+            issue(tc, Cb);
         });
     } else {
         stage_tables<0>(lds, img, [] {});
@@ -591,6 +711,13 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
 #pragma unroll
     for (int c = 0; c < K; ++c) C[c] = 0;
     auto process = [&](RowsK<K> &b, const GroupTask &t) {
+        if constexpr (kCopy) {
+#pragma unroll
+            for (int c = 0; c < K; ++c)
+                if (K * t.i + c < nfr)
+                    store_row((gwbyte *)(dst + (uint64_t)frag(t.i, c) * dst_stride + (uint64_t)t.r * kRowBytes + lane_off),
+                              b.x[c]);
+        }
         if (kAblate == 1) {
 #pragma unroll
             for (int c = 0; c < K; ++c) {
@@ -639,22 +766,34 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
         }
         return;
     }
+    // steady state: while one slot is checksummed the other two are in flight
+    constexpr int kL = 4 * K;  // loads (and, with kCopy, stores) per step
+    bool first = true;
     for (;;) {
-        GroupTask tc = advance(tb);
-        issue(tc, Cb);
-        wait_rows<16 * K / 2, K>(A);
+        if (!kCopy || first)
+            wait_rows<2 * kL, K>(A);
+        else
+            wait_rows<4 * kL, K>(A);
         process(A, ta);
         if (is_last(ta)) break;
         ta = advance(tc);
         issue(ta, A);
-        wait_rows<16 * K / 2, K>(B);
+        if (!kCopy)
+            wait_rows<2 * kL, K>(B);
+        else if (first)
+            wait_rows<3 * kL, K>(B);
+        else
+            wait_rows<4 * kL, K>(B);
         process(B, tb);
         if (is_last(tb)) break;
         tb = advance(ta);
         issue(tb, B);
-        wait_rows<16 * K / 2, K>(Cb);
+        first = false;
+        wait_rows<(kCopy ? 4 : 2) * kL, K>(Cb);
         process(Cb, tc);
         if (is_last(tc)) break;
+        tc = advance(tb);
+        issue(tc, Cb);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped re-loads before exit
 }
@@ -669,14 +808,26 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
         FragInfo fi = src.get(f);
         fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
         fi.len = uniform(fi.len);
+        if constexpr (Src::kCopy) {
+            fi.dst = (uint8_t *)uniform64((uint64_t)(uintptr_t)fi.dst);
+            fi.copylen = uniform(fi.copylen);
+        }
         const uint32_t R = (fi.len + (kRowBytes - 1)) / kRowBytes;
         const uint32_t s16 = (uint32_t)((uintptr_t)fi.addr & 15u);
-        uint32_t acc = 0;
+        const uint32_t dm = (uint32_t)((uintptr_t)fi.dst & 15u);
+        uint32_t acc = 0, carry = 0;
         for (uint32_t r = 0; r < R; ++r) {
             const long long o = (long long)r * kRowBytes + lane * kLaneBytes;
             const bool mask = (r + 1 == R) && (fi.len % kRowBytes != 0 || s16 != 0);
             uint32_t d[16];
             load64(fi.addr, o, 0, (long long)fi.len, mask || s16 != 0, s16, d);
+            if constexpr (Src::kCopy) {
+                if (fi.copylen) {
+                    const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
+                    store64(fi.dst, o, d, (long long)fi.copylen, dm & 3u, dm == 0, prev, lane == 63 && r + 1 == R);
+                    carry = __builtin_amdgcn_readlane(d[15], 63);
+                }
+            }
 #pragma unroll
             for (int w = 0; w < 16; ++w) acc += d[w];
         }
@@ -689,19 +840,27 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
 // hence no staging, so it uses the fastest measured read shape -- one fragment per wave,
 // short-lived 256-thread workgroups in address order, up to four rows (16 x dwordx4 per
 // lane) in flight at once.
+template <bool kCopy = false>
 __global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
-                                                             size_t frag_len, uint32_t *__restrict__ out) {
+                                                             size_t frag_len, uint32_t *__restrict__ out,
+                                                             uint8_t *__restrict__ dst = nullptr,
+                                                             size_t dst_stride = 0) {
     const int lane = threadIdx.x & 63;
     const uint32_t f = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
     if (f >= n) return;
     const uint32_t R = (uint32_t)(frag_len / kRowBytes);
     gbyte *p = (gbyte *)(base + (uint64_t)f * frag_len + (uint64_t)lane * kLaneBytes);
+    gwbyte *q = kCopy ? (gwbyte *)(dst + (uint64_t)f * dst_stride + (uint64_t)lane * kLaneBytes) : nullptr;
     uint32_t acc = 0;
     uint32_t r = 0;
     for (; r + 4 <= R; r += 4) {
         u32x4 v[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)(r + k / 4) * kRowBytes + 16 * (k & 3));
+        if constexpr (kCopy) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) *(gwu32x4 *)(q + (uint64_t)(r + k / 4) * kRowBytes + 16 * (k & 3)) = v[k];
+        }
 #pragma unroll
         for (int k = 0; k < 16; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
     }
@@ -709,6 +868,10 @@ __global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__re
         u32x4 v[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)r * kRowBytes + 16 * k);
+        if constexpr (kCopy) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *(gwu32x4 *)(q + (uint64_t)r * kRowBytes + 16 * k) = v[k];
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
     }
@@ -902,7 +1065,30 @@ hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, ui
     if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const uint32_t fpw = pick_fpw(n, (uint32_t)(frag_len / kRowBytes));
     hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains>), grid_for(n, fpw), dim3(kBlock), 0, s, base, (uint32_t)n,
-                       fpw, frag_len, partial, img, out);
+                       fpw, frag_len, partial, img, out, nullptr, (size_t)0);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint8_t *dst,
+                                   size_t dst_stride, uint32_t *out, const uint32_t *img, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t fpw = pick_fpw(n, (uint32_t)(frag_len / kRowBytes));
+    hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains, true>), grid_for(n, fpw), dim3(kBlock), 0, s, base,
+                       (uint32_t)n, fpw, frag_len, partial, img, out, dst, dst_stride);
+    return hipGetLastError();
+}
+
+hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t fpw = pick_fpw(n, 1);
+    if (mode == LAMPI_CSUM_CRC32)
+        hipLaunchKernelGGL(crc_rows_kernel<CopySource>, grid_for(n, fpw), dim3(kBlock), 0, s, CopySource{d}, n, fpw,
+                           img, out);
+    else
+        hipLaunchKernelGGL(sum_rows_kernel<CopySource>, grid_for(n, fpw), dim3(kBlock), 0, s, CopySource{d}, n, fpw,
+                           out);
     return hipGetLastError();
 }
 
@@ -920,13 +1106,37 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (n == 0) return hipSuccess;
     if (msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 && ((uintptr_t)base & 15u) == 0 &&
         n <= 0xFFFFFFFFull) {
-        hipLaunchKernelGGL(sum_regular_kernel, dim3((unsigned)((n + kWaves - 1) / kWaves)), dim3(kBlock), 0, s, base,
-                           (uint32_t)n, frag_len, out);
+        hipLaunchKernelGGL(sum_regular_kernel<false>, dim3((unsigned)((n + kWaves - 1) / kWaves)), dim3(kBlock), 0, s,
+                           base, (uint32_t)n, frag_len, out, nullptr, (size_t)0);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
     hipLaunchKernelGGL(sum_rows_kernel<MsgSource>, grid_for(n, fpw), dim3(kBlock), 0, s,
                        MsgSource{base, msg_len, frag_len, 0u}, n, fpw, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, uint8_t *dst,
+                            size_t dst_stride, size_t n, uint32_t *out, int mode, const uint32_t *img, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const bool regular = msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 &&
+                         ((uintptr_t)base & 15u) == 0 && ((uintptr_t)dst & 15u) == 0 && dst_stride % 16 == 0 &&
+                         n <= 0xFFFFFFFFull;
+    if (mode == LAMPI_CSUM_CRC32) {
+        if (regular) return launch_crc_regular_copy(base, n, frag_len, partial, dst, dst_stride, out, img, s);
+        const uint32_t fpw = pick_fpw(n, (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes));
+        hipLaunchKernelGGL(crc_rows_kernel<MsgCopySource>, grid_for(n, fpw), dim3(kBlock), 0, s,
+                           MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n, fpw, img, out);
+        return hipGetLastError();
+    }
+    if (regular) {
+        hipLaunchKernelGGL(sum_regular_kernel<true>, dim3((unsigned)((n + kWaves - 1) / kWaves)), dim3(kBlock), 0, s,
+                           base, (uint32_t)n, frag_len, out, dst, dst_stride);
+        return hipGetLastError();
+    }
+    const uint32_t fpw = pick_fpw(n, 1);
+    hipLaunchKernelGGL(sum_rows_kernel<MsgCopySource>, grid_for(n, fpw), dim3(kBlock), 0, s,
+                       MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, fpw, out);
     return hipGetLastError();
 }
 

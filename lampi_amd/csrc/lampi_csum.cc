@@ -283,6 +283,21 @@ int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_
     return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s));
 }
 
+int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (n == 0) return 0;
+    if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;
+    if (mode == LAMPI_CSUM_CRC32) {
+        e = device_tables(dev, &img);
+        if (e != hipSuccess) return to_int(e);
+    }
+    return to_int(launch_bcopy_desc(d_descs, n, d_out, mode, img, (hipStream_t)stream));
+}
+
 int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t partial, uint32_t *d_out, int mode,
                    void *stream) {
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
@@ -304,6 +319,24 @@ int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t 
                          ((uintptr_t)base & 15u) == 0;
     if (regular) return to_int(launch_crc_regular(base, n, frag_len, partial, d_out, img, grid, s));
     return to_int(launch_crc_msg(base, msg_len, frag_len, partial, n, d_out, img, grid, s));
+}
+
+int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_dst, size_t dst_stride,
+                    uint32_t partial, uint32_t *d_out, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (frag_len == 0 || frag_len > 0xFFFFFFFFull || dst_stride < frag_len || !d_out || (msg_len && (!d_msg || !d_dst)))
+        return to_int(hipErrorInvalidValue);
+    const size_t n = msg_len ? (msg_len + frag_len - 1) / frag_len : 1;
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;
+    if (mode == LAMPI_CSUM_CRC32) {
+        e = device_tables(dev, &img);
+        if (e != hipSuccess) return to_int(e);
+    }
+    return to_int(launch_msg_bcopy((const uint8_t *)d_msg, msg_len, frag_len, partial, (uint8_t *)d_dst, dst_stride, n,
+                                   d_out, mode, img, (hipStream_t)stream));
 }
 
 int lampi_fill_stream(void *d_dst, size_t nbytes, uint64_t seed, uint64_t byte_off, void *stream) {

@@ -1,7 +1,8 @@
 """Device-resident batched checksums over torch CUDA tensors (HIP on ROCm).
 
 PyTorch is only plumbing here: it owns HBM buffers and streams.  Every checksum is
-computed by the gfx950 kernels behind the C ABI (lampi_frag_csum_batch, lampi_msg_csum).
+computed by the gfx950 kernels behind the C ABI (lampi_frag_csum_batch, lampi_frag_bcopy_batch,
+lampi_msg_csum).
 """
 from __future__ import annotations
 
@@ -10,8 +11,8 @@ import torch
 
 from ._lib import CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
 
-__all__ = ["CRC32", "SUM32", "frag_csum_batch", "msg_csum", "fill_stream", "fill_stream_frags", "make_descs",
-           "as_u32"]
+__all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
+           "make_descs", "make_copy_descs", "as_u32"]
 
 
 def _stream_handle(stream: torch.cuda.Stream | None) -> int:
@@ -51,6 +52,50 @@ def make_descs(base: torch.Tensor, offsets, lengths, partials=None) -> torch.Ten
     return torch.from_numpy(host.view(np.int64)).to(base.device)
 
 
+def make_copy_descs(src: torch.Tensor, src_offsets, dst: torch.Tensor, dst_offsets, copylens, csumlens,
+                    partials=None) -> torch.Tensor:
+    """Build a device array of ``lampi_copy_desc`` (n x 32 bytes, int64 [n, 4] storage)."""
+    _require_cuda(src, "src")
+    _require_cuda(dst, "dst")
+    so = np.asarray(src_offsets, dtype=np.uint64)
+    do = np.asarray(dst_offsets, dtype=np.uint64)
+    cl = np.asarray(copylens, dtype=np.uint64)
+    sl = np.asarray(csumlens, dtype=np.uint64)
+    n = so.size
+    if not (do.size == cl.size == sl.size == n):
+        raise ValueError("descriptor fields differ in size")
+    if n:
+        if int(np.maximum(cl, sl).max()) > 0xFFFFFFFF:
+            raise ValueError("length exceeds 32 bits")
+        if int((so + np.maximum(cl, sl)).max()) > src.numel() * src.element_size():
+            raise ValueError("a source fragment extends past the end of src")
+        if int((do + cl).max()) > dst.numel() * dst.element_size():
+            raise ValueError("a copy extends past the end of dst")
+    pt = (np.full(n, CRC_INITIAL_REGISTER, dtype=np.uint64) if partials is None
+          else np.asarray(partials, dtype=np.uint64) & 0xFFFFFFFF)
+    host = np.empty((n, 4), dtype=np.uint64)
+    host[:, 0] = np.uint64(src.data_ptr()) + so
+    host[:, 1] = np.uint64(dst.data_ptr()) + do
+    host[:, 2] = cl | (sl << np.uint64(32))
+    host[:, 3] = pt
+    return torch.from_numpy(host.view(np.int64)).to(src.device)
+
+
+def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
+                     stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Fused bcopy_uicrc / bcopy_uicsum per ``lampi_copy_desc``; returns the checksums."""
+    _require_cuda(descs, "descs")
+    count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
+    if out is None:
+        out = torch.empty(count, dtype=torch.int32, device=descs.device)
+    _require_cuda(out, "out")
+    if out.numel() < count:
+        raise ValueError("out is too small")
+    check(lib().lampi_frag_bcopy_batch(descs.data_ptr(), count, out.data_ptr(), mode, _stream_handle(stream)),
+          "lampi_frag_bcopy_batch")
+    return out
+
+
 def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
                     stream: torch.cuda.Stream | None = None) -> torch.Tensor:
     """out[i] = checksum of fragment descs[i]; one wavefront per fragment."""
@@ -82,6 +127,29 @@ def msg_csum(msg: torch.Tensor, frag_len: int, partial: int = CRC_INITIAL_REGIST
         raise ValueError("out is too small")
     check(lib().lampi_msg_csum(msg.data_ptr(), nbytes, frag_len, partial & 0xFFFFFFFF, out.data_ptr(), mode,
                                _stream_handle(stream)), "lampi_msg_csum")
+    return out
+
+
+def msg_bcopy(msg: torch.Tensor, frag_len: int, dst: torch.Tensor, dst_stride: int | None = None,
+              partial: int = CRC_INITIAL_REGISTER, mode: int = CRC32, msg_len: int | None = None,
+              out: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Fragment ``msg`` and copy fragment k to ``dst`` + k*dst_stride with its checksum fused."""
+    _require_cuda(msg, "msg")
+    _require_cuda(dst, "dst")
+    nbytes = msg.numel() * msg.element_size() if msg_len is None else int(msg_len)
+    if nbytes > msg.numel() * msg.element_size():
+        raise ValueError("msg_len exceeds the tensor")
+    stride = frag_len if dst_stride is None else int(dst_stride)
+    n = (nbytes + frag_len - 1) // frag_len if nbytes else 1
+    if nbytes and (n - 1) * stride + (nbytes - (n - 1) * frag_len) > dst.numel() * dst.element_size():
+        raise ValueError("dst is too small")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=msg.device)
+    _require_cuda(out, "out")
+    if out.numel() < n:
+        raise ValueError("out is too small")
+    check(lib().lampi_msg_bcopy(msg.data_ptr(), nbytes, frag_len, dst.data_ptr(), stride, partial & 0xFFFFFFFF,
+                                out.data_ptr(), mode, _stream_handle(stream)), "lampi_msg_bcopy")
     return out
 
 

@@ -62,6 +62,10 @@ def test_desc_struct_layout():
     FD = lampi_amd.FragDesc
     assert ctypes.sizeof(FD) == 16
     assert FD.addr.offset == 0 and FD.length.offset == 8 and FD.partial.offset == 12
+    CD = lampi_amd._lib.CopyDesc
+    assert ctypes.sizeof(CD) == 32
+    assert [getattr(CD, f).offset for f in ("src", "dst", "copylen", "csumlen", "partial", "reserved")] == \
+        [0, 8, 16, 20, 24, 28]
 
 
 def test_no_oracle_in_product():
@@ -115,7 +119,9 @@ int main(int argc, char **) { return argc > 5 ? (int)send_contig(0, 0, 0) : 0; }
 int main(void) {
     lampi_frag_desc d = {0, 0, LAMPI_CRC_INITIAL_REGISTER};
     (void)d;
-    return (int)(sizeof(lampi_frag_desc) != 16);
+    lampi_copy_desc c = {0, 0, 0, 0, LAMPI_CRC_INITIAL_REGISTER, 0};
+    (void)c;
+    return (int)(sizeof(lampi_frag_desc) != 16 || sizeof(lampi_copy_desc) != 32);
 }
 ''')
     libdir = os.path.dirname(lampi_amd._lib.LIB_PATH)

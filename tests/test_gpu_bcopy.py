@@ -1,0 +1,171 @@
+"""GPU parity of the fused copy + checksum batch (lampi_frag_bcopy_batch).
+
+bcopy_uicrc / bcopy_uicsum (ref src/util/MemFunctions.cc:1263-1321, 518-875) copy `copylen`
+bytes and checksum max(copylen, csumlen) bytes; the residue is checksummed, never copied.
+Checked bit-exact: checksums against the reference-generated fixtures (tests/golden, `bcopy`)
+and the oracle; destination bytes against the source, with every byte outside the copies
+left untouched (sentinel stream).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EDGE_LENS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 63, 64, 65, 127, 1023, 1024, 1025, 1976, 4092, 4095, 4096, 4097,
+             8191, 8192, 16384, 16385, 65455, 65456]
+
+
+def _dv():
+    from lampi_amd import device as dv
+
+    return dv
+
+
+def _layout(totals, copylens, src_align, dst_align):
+    """Disjoint 64-byte-aligned slots (plus 64 bytes of gap) for every source and destination."""
+    slot_s = (np.asarray(totals, np.int64) + 16 + 64 + 63) // 64 * 64
+    slot_d = (np.asarray(copylens, np.int64) + 16 + 64 + 63) // 64 * 64
+    so = np.concatenate([[0], np.cumsum(slot_s)[:-1]]) + np.asarray(src_align, np.int64)
+    do = np.concatenate([[0], np.cumsum(slot_d)[:-1]]) + np.asarray(dst_align, np.int64)
+    return so.astype(np.uint64), do.astype(np.uint64), int(slot_s.sum()), int(slot_d.sum())
+
+
+def _run(cuda, oracle, copylens, csumlens, src_align, dst_align, partials, mode, src_fill=None):
+    """Run one batch; return (checksums, expected checksums, dst bytes, expected dst bytes)."""
+    import torch
+
+    dv = _dv()
+    cl = np.asarray(copylens, np.uint64)
+    sl = np.asarray(csumlens, np.uint64)
+    tot = np.maximum(cl, sl)
+    so, do, ns, nd = _layout(tot, cl, src_align, dst_align)
+    src = torch.empty(max(ns, 64), dtype=torch.uint8, device=cuda)
+    dv.fill_stream(src, seed=41)
+    host_src = src.cpu().numpy()
+    if src_fill is not None:  # caller-provided payloads (fixture slices)
+        for i, b in enumerate(src_fill):
+            host_src[int(so[i]):int(so[i]) + b.size] = b
+        src.copy_(torch.from_numpy(host_src).to(cuda))
+    dst = torch.empty(max(nd, 64), dtype=torch.uint8, device=cuda)
+    dv.fill_stream(dst, seed=42)
+    want_dst = dst.cpu().numpy().copy()
+    for i in range(cl.size):
+        a, b, n = int(so[i]), int(do[i]), int(cl[i])
+        want_dst[b:b + n] = host_src[a:a + n]
+    descs = dv.make_copy_descs(src, so, dst, do, cl, sl, partials)
+    got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=mode))
+    want = oracle.desc_batch(host_src, so, tot.astype(np.uint32),
+                             None if mode == 1 else np.asarray(partials, np.uint64).astype(np.uint32), mode)
+    return got, want, dst.cpu().numpy(), want_dst
+
+
+def _assert_same(got, want, dgot, dwant, info):
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [info(i) for i in bad[:8]]
+    diff = np.nonzero(dgot != dwant)[0]
+    assert diff.size == 0, f"{diff.size} destination bytes differ, first at {int(diff[0])}"
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_bcopy_batch_reference_fixtures(cuda, oracle, mode):
+    """The reference's own bcopy_uicrc / bcopy_uicsum results (tests/golden/fixtures.json)."""
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fixtures.json")) as f:
+        cases = json.load(f)["bcopy"]
+    if mode == 1:  # the batch starts every fragment from a fresh partial-word state
+        cases = [c for c in cases if c["plen"] == 0]
+    cl = [c["copylen"] for c in cases]
+    sl = [c["clen"] for c in cases]
+    payload = [oracle.stream(c["seed"], c["off"], max(c["copylen"], c["clen"])) for c in cases]
+    got, want, dgot, dwant = _run(cuda, oracle, cl, sl, [c["src_align"] for c in cases],
+                                  [c["dst_align"] for c in cases], [c["partial"] for c in cases], mode, payload)
+    fx = np.array([c["crc"] if mode == 0 else c["sum"] for c in cases], np.uint32)
+    assert np.array_equal(want, fx)  # oracle == reference on these inputs
+    _assert_same(got, fx, dgot, dwant, lambda i: (cl[i], sl[i], cases[i]["src_align"], cases[i]["dst_align"]))
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_bcopy_batch_edges_and_alignment(cuda, oracle, mode):
+    """Every edge length x source/destination misalignment x (copy =, <, > checksum length)."""
+    rng = np.random.default_rng(515)
+    cl, sl, sa, da = [], [], [], []
+    for L in EDGE_LENS:
+        for a in range(16):
+            for kind in range(3):
+                b = int(rng.integers(0, 16))
+                short = int(rng.integers(0, L + 1))
+                cl.append(L if kind != 1 else short)  # kind 1: copylen < csumlen (receive side)
+                sl.append(L if kind != 2 else short)  # kind 2: csumlen < copylen
+                sa.append(a)
+                da.append(b)
+    parts = rng.integers(0, 2**32, size=len(cl), dtype=np.uint64)
+    parts[::4] = 0xFFFFFFFF
+    got, want, dgot, dwant = _run(cuda, oracle, cl, sl, sa, da, parts, mode)
+    _assert_same(got, want, dgot, dwant, lambda i: (cl[i], sl[i], sa[i], da[i]))
+
+
+def test_bcopy_batch_random(cuda, oracle):
+    rng = np.random.default_rng(77)
+    n = 6000
+    cl = rng.integers(0, 70000, size=n)
+    sl = np.where(rng.random(n) < 0.3, rng.integers(0, 70000, size=n), cl)
+    sa = rng.integers(0, 16, size=n)
+    da = np.where(rng.random(n) < 0.5, sa, rng.integers(0, 16, size=n))
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    for mode in (0, 1):
+        got, want, dgot, dwant = _run(cuda, oracle, cl, sl, sa, da, parts, mode)
+        _assert_same(got, want, dgot, dwant, lambda i: (int(cl[i]), int(sl[i]), int(sa[i]), int(da[i])))
+
+
+def test_bcopy_batch_uniform_4k(cuda, oracle):
+    """256K x 4 KiB gather into a staging array (the send-side shape): checksums vs the oracle,
+    the copy compared on the device."""
+    import torch
+
+    dv = _dv()
+    n, L = 262144, 4096
+    src = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(src, seed=2)
+    dst = torch.zeros(n * L, dtype=torch.uint8, device=cuda)
+    # scatter: fragment i goes to slot perm[i]
+    perm = np.random.default_rng(5).permutation(n).astype(np.uint64)
+    offs = np.arange(n, dtype=np.uint64) * L
+    descs = dv.make_copy_descs(src, offs, dst, perm * L, np.full(n, L), np.full(n, L))
+    for mode in (0, 1):
+        got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=mode))
+        assert np.array_equal(got, oracle.uniform_batch(2, 0, n, L, mode))
+    assert torch.equal(dst.view(n, L)[torch.from_numpy(perm.astype(np.int64)).to(cuda)], src.view(n, L))
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("msg_len,frag_len,stride,dst_off", [
+    (4096 * 50000, 4096, 4096, 0),          # regular fast path, plain copy
+    (4096 * 20000, 4096, 8192, 0),          # regular, staging slots with gaps
+    (16384 * 3000, 16384, 16384 + 64, 16),  # regular, 4-row fragments
+    (65456 * 300 + 17, 65456, 65528, 0),    # GM payload into 72 + 65456-byte slots (general path)
+    (1000003, 4096, 4100, 3),               # ragged everything
+    (5, 4096, 4096, 1),                     # one short fragment
+])
+def test_msg_bcopy(cuda, oracle, mode, msg_len, frag_len, stride, dst_off):
+    """lampi_msg_bcopy: fragment k -> dst + k*stride with its checksum fused; gap bytes untouched."""
+    import torch
+
+    dv = _dv()
+    msg = torch.empty(msg_len, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(msg, seed=13)
+    n = (msg_len + frag_len - 1) // frag_len
+    dst_bytes = dst_off + (n - 1) * stride + frag_len + 64
+    dst = torch.empty(dst_bytes, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(dst, seed=14)
+    want_dst = dst.cpu().numpy().copy()
+    host = msg.cpu().numpy()
+    offs = np.arange(n, dtype=np.uint64) * frag_len
+    lens = np.minimum(frag_len, msg_len - offs.astype(np.int64)).astype(np.uint32)
+    for k in range(n):
+        a, ln = int(offs[k]), int(lens[k])
+        want_dst[dst_off + k * stride:dst_off + k * stride + ln] = host[a:a + ln]
+    got = dv.as_u32(dv.msg_bcopy(msg, frag_len, dst[dst_off:], stride, partial=0x0BADF00D, mode=mode))
+    want = oracle.desc_batch(host, offs, lens, np.full(n, 0x0BADF00D, np.uint32) if mode == 0 else None, mode)
+    _assert_same(got, want, dst.cpu().numpy(), want_dst, lambda i: (i, int(lens[i])))

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
-#   smoke | tests | bench | bench16k | benchsum | benchC | prof | pmc | e2e | microbench
+#   smoke | tests | tests_bcopy | bench | bench16k | benchsum | benchC | bcopy | prof | pmc | e2e | microbench
 # A test failure (exit 1) lets later steps run; a fault, abort, segfault, timeout or
 # kill (exit >= 124, 134, 139, ...) ends the session immediately.
 set -u
@@ -38,6 +38,9 @@ for step in "$@"; do
          run pmc_ea 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv \
             -d gpurun_out/pmc_ea -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     e2e) run e2e 600 python bench.py --e2e ;;
+    bcopy) run bcopy 600 python bench.py --bcopy --steps 10 &&
+           run bcopysum 600 python bench.py --bcopy --mode sum --steps 10 ;;
+    tests_bcopy) run pytest_bcopy 600 python -m pytest tests/test_gpu_bcopy.py -m gpu -x -q ;;
     microbench) run microbench 300 tools/microbench/readbw ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -82,12 +82,13 @@ int main(int argc, char **argv) {
     if (argc > 2) return 0;  // probes only
     for (size_t L : {4096ul, 16384ul}) {
         const uint32_t n = (uint32_t)(bytes / L);
-        for (int chains : {2, 4})
-        for (uint32_t fpw : {8u, 16u, 32u}) {
+        for (int chains : {2})
+        for (uint32_t fpw : (L == 4096 ? std::vector<uint32_t>{16u, 24u, 32u, 40u, 48u, 64u}
+                                       : std::vector<uint32_t>{4u, 8u, 12u, 16u})) {
             const dim3 grid((n + kWaves * fpw - 1) / (kWaves * fpw));
             for (int v = 0; v < 3; ++v) {
                 auto launch = [&] {
-#define LK(V, K) hipLaunchKernelGGL((crc_regular_kernel<V, K>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu, dimg, out)
+#define LK(V, K) hipLaunchKernelGGL((crc_regular_kernel<V, K>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu, dimg, out, nullptr, (size_t)0)
                     if (chains == 2) {
                         if (v == 0) LK(0, 2); else if (v == 1) LK(1, 2); else LK(2, 2);
                     } else {
