@@ -100,6 +100,18 @@ std::vector<uint32_t> build_table_image() {
     // Horner step between rows: the next 64-byte piece of a lane starts 4032 bytes later
     const Gf2Mat h = swapped(shift_matrix(kRowBytes - kLaneBytes));
     for (int b = 0; b < 32; ++b) img[kImgHornerCols + b] = h.col[b];
+
+    // coalesced layout: lane l's last chunk ends 16*(63-l) bytes before the row end, and
+    // consecutive chunks of a lane (also across rows) are 1008 bytes apart
+    const Gf2Mat step16 = shift_matrix(kChunkBytes);
+    m = mat_identity();
+    for (int l = kWave - 1; l >= 0; --l) {
+        const Gf2Mat ms = swapped(m);
+        for (int b = 0; b < 32; ++b) img[kImgCombine16Cols + l * 32 + b] = ms.col[b];
+        m = mat_mul(step16, m);
+    }
+    const Gf2Mat h16 = swapped(shift_matrix(kChunkStep));
+    for (int b = 0; b < 32; ++b) img[kImgHorner16Cols + b] = h16.col[b];
     return img;
 }
 

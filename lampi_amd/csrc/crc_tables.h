@@ -31,11 +31,18 @@ constexpr int kRowBytes = kWave * kLaneBytes;  // 4096
 //   [kImgCombineCols, +2048) per-lane final shift by 64*(63-l) bytes (swapped domain), as
 //                            matrix columns: word l*32 + b = M_l(1 << b)
 //   [kImgHornerCols, +32)    shift by kRowBytes - kLaneBytes = 4032 bytes, columns b
+//   [kImgCombine16Cols, +2048), [kImgHorner16Cols, +32): the same for the coalesced layout
+//                            of the fused-copy kernel (lane l owns the 16-byte chunks at
+//                            16l + 1024k of each row): final shift 16*(63-l), step 1008 bytes
 // Nibble tables are XORs of four columns: M(v << 4p) = XOR_{bit b of v} col[4p + b].
 constexpr size_t kImgSliceT = 0;
 constexpr size_t kImgCombineCols = 1024;
 constexpr size_t kImgHornerCols = 1024 + 2048;
-constexpr size_t kImgWords = 1024 + 2048 + 32;
+constexpr size_t kImgCombine16Cols = kImgHornerCols + 32;
+constexpr size_t kImgHorner16Cols = kImgCombine16Cols + 2048;
+constexpr size_t kImgWords = kImgHorner16Cols + 32;
+constexpr int kChunkBytes = 16;                          // coalesced layout: 16-byte chunks
+constexpr int kChunkStep = kRowBytes / 4 - kChunkBytes;  // 1008 zero bytes between a lane's chunks
 
 inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 

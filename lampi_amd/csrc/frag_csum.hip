@@ -143,14 +143,17 @@ struct Row {
     u32x4 q[4];
 };
 
+// the lane's four 16-byte chunks at p, p + kS, p + 2kS, p + 3kS (kS = 16: one contiguous
+// 64-byte piece; kS = 1024: the coalesced layout, every instruction covers 1 KiB of the row)
+template <int kS = 16>
 __device__ __forceinline__ void issue_row(gbyte *p, Row &r) {
     asm volatile(
         "global_load_dwordx4 %0, %4, off\n\t"
-        "global_load_dwordx4 %1, %4, off offset:16\n\t"
-        "global_load_dwordx4 %2, %4, off offset:32\n\t"
-        "global_load_dwordx4 %3, %4, off offset:48"
+        "global_load_dwordx4 %1, %4, off offset:%5\n\t"
+        "global_load_dwordx4 %2, %4, off offset:%6\n\t"
+        "global_load_dwordx4 %3, %4, off offset:%7"
         : "=&v"(r.q[0]), "=&v"(r.q[1]), "=&v"(r.q[2]), "=&v"(r.q[3])
-        : "v"(p)
+        : "v"(p), "n"(kS), "n"(2 * kS), "n"(3 * kS)
         : "memory");
 }
 
@@ -178,15 +181,16 @@ __device__ __forceinline__ void row_words(const Row &r, uint32_t d[16]) {
 // 4 x dwordx4 stores of a lane's 64-byte piece.  Stores count in vmcnt in issue order with
 // the loads (MI355X_MICROARCH.md, s_waitcnt), so the ring's wait counts include them.  The
 // trailing s_nop covers the store-data read hazard before the registers are rewritten.
+template <int kS = 16>
 __device__ __forceinline__ void store_row(gwbyte *p, const Row &r) {
     asm volatile(
         "global_store_dwordx4 %0, %1, off\n\t"
-        "global_store_dwordx4 %0, %2, off offset:16\n\t"
-        "global_store_dwordx4 %0, %3, off offset:32\n\t"
-        "global_store_dwordx4 %0, %4, off offset:48\n\t"
+        "global_store_dwordx4 %0, %2, off offset:%5\n\t"
+        "global_store_dwordx4 %0, %3, off offset:%6\n\t"
+        "global_store_dwordx4 %0, %4, off offset:%7\n\t"
         "s_nop 1"
         :
-        : "v"(p), "v"(r.q[0]), "v"(r.q[1]), "v"(r.q[2]), "v"(r.q[3])
+        : "v"(p), "v"(r.q[0]), "v"(r.q[1]), "v"(r.q[2]), "v"(r.q[3]), "n"(kS), "n"(2 * kS), "n"(3 * kS)
         : "memory");
 }
 
@@ -197,7 +201,7 @@ __device__ __forceinline__ void store_row(gwbyte *p, const Row &r) {
 // __syncthreads() would also wait for the row loads.
 // kParts (diagnostics only, tools/microbench/crc_ablation.hip): bit 0 slicing, bit 1 combine,
 // bit 2 Horner tables; the product always builds all three.
-template <int kPre, class Pre, int kParts = 7>
+template <int kPre, class Pre, int kParts = 7, size_t kComb = kImgCombineCols, size_t kHorn = kImgHornerCols>
 __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__restrict__ img, Pre pre) {
     const uint32_t t = threadIdx.x;  // 256 threads
     gbyte *g = (gbyte *)img;
@@ -211,10 +215,10 @@ __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__re
         asm volatile("global_load_dword %0, %1, off" : "=&v"(sv[kk]) : "v"(g + 4 * (kImgSliceT + 4 * (r0 + 32 * kk) + sj)) : "memory");
     // combine: lane l = t & 63, nibble positions p0 = t >> 6 and p0 + 4 (4 columns each)
     const uint32_t l = t & 63u, p0 = t >> 6;
-    u32x4 ca = issue_b128(g + 4 * (kImgCombineCols + l * 32 + 4 * p0));
-    u32x4 cb = issue_b128(g + 4 * (kImgCombineCols + l * 32 + 4 * (p0 + 4)));
+    u32x4 ca = issue_b128(g + 4 * (kComb + l * 32 + 4 * p0));
+    u32x4 cb = issue_b128(g + 4 * (kComb + l * 32 + 4 * (p0 + 4)));
     // Horner: threads 0..127, p = t >> 4 (loads beyond 127 re-read a valid column)
-    u32x4 hc = issue_b128(g + 4 * (kImgHornerCols + 4 * ((t >> 4) & 7u)));
+    u32x4 hc = issue_b128(g + 4 * (kHorn + 4 * ((t >> 4) & 7u)));
     pre();
     asm volatile("s_waitcnt vmcnt(%4)" : "+v"(ca), "+v"(cb), "+v"(hc), "+v"(sv[0]) : "n"(kPre) : "memory");
     asm volatile("" : "+v"(sv[1]), "+v"(sv[2]), "+v"(sv[3]), "+v"(sv[4]), "+v"(sv[5]), "+v"(sv[6]), "+v"(sv[7]));
@@ -647,11 +651,50 @@ __device__ __forceinline__ void crc_pieces(const uint32_t *lds, const CrcLane &k
     for (int c = 0; c < K; ++c) C[c] = xor3(t[c].t0, t[c].t1, t[c].t2) ^ t[c].t3;
 }
 
+// Coalesced layout (fused copy): lane l holds the 16-byte chunks at 16l + 1024q of a row.
+// Every chunk but the fragment's first is preceded by a 1008-byte Horner shift (the same step
+// inside a row and across rows); the final per-lane shift is 16*(63-l).
+template <int K>
+__device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k, uint32_t (&C)[K],
+                                           const RowsK<K> &b, bool start, uint32_t init) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (start && q == 0) {
+#pragma unroll
+            for (int c = 0; c < K; ++c) C[c] = init;
+        } else {
+#pragma unroll
+            for (int c = 0; c < K; ++c) C[c] = horner_shift(lds, C[c]);
+        }
+        uint32_t X[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) X[c] = C[c] ^ b.x[c].q[q].x;
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+            Look4 t[K];
+#pragma unroll
+            for (int c = 0; c < K; ++c) t[c] = look4(lds, k, X[c]);
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                const uint32_t d = w == 1 ? b.x[c].q[q].y : w == 2 ? b.x[c].q[q].z : b.x[c].q[q].w;
+                X[c] = xor3(xor3(t[c].t0, t[c].t1, t[c].t2), t[c].t3, d);
+            }
+        }
+        Look4 t[K];
+#pragma unroll
+        for (int c = 0; c < K; ++c) t[c] = look4(lds, k, X[c]);
+#pragma unroll
+        for (int c = 0; c < K; ++c) C[c] = xor3(t[c].t0, t[c].t1, t[c].t2) ^ t[c].t3;
+    }
+}
+
 // kAblate (tools/microbench/crc_ablation.hip only; the product launches 0):
 //   1 = loads only (words XOR-folded, no table lookups), 2 = lookups only (no global loads)
 // kCopy: fused bcopy -- each row is also stored to dst + f*dst_stride (16-byte aligned) as soon
 // as it arrives; per step the ring then carries 4K stores beside 4K loads, and the waits count
-// them (first pass: 8K / 12K / 16K younger operations, then 16K).
+// them (first pass: 8K / 12K / 16K younger operations, then 16K).  Rows move in the coalesced
+// layout (crc_chunks): lane-contiguous 64-byte stores run at 51% of the HBM roofline on
+// MI355X against 71% for 1 KiB-per-instruction stores (profiles/r01_copy_patterns.txt).
 template <int kAblate, int kChains, bool kCopy = false>
 __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
                                                              uint32_t fpw, size_t frag_len, uint32_t partial,
@@ -659,6 +702,8 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
                                                              uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
                                                              size_t dst_stride) {
     constexpr int K = kChains;
+    constexpr bool kCoal = kCopy;                   // coalesced row layout
+    constexpr int kS = kCoal ? kRowBytes / 4 : 16;  // chunk stride of a lane
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
     const uint32_t R = (uint32_t)(frag_len / kRowBytes);
@@ -666,7 +711,7 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
     // fragments of this wave: f0 + kWaves*j, j < nfr; processed in groups of K
     const uint32_t nfr = f0 < n ? min(fpw, (n - f0 + kWaves - 1) / kWaves) : 0u;
     const uint32_t ngrp = (nfr + K - 1) / K;
-    const uint32_t lane_off = (uint32_t)lane * kLaneBytes;
+    const uint32_t lane_off = (uint32_t)lane * (kCoal ? kChunkBytes : kLaneBytes);
     const uint32_t vinit = __builtin_bswap32(partial);
 
     auto advance = [&](GroupTask t) -> GroupTask {
@@ -685,20 +730,23 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
     };
     auto issue = [&](const GroupTask &t, RowsK<K> &b) {
 #pragma unroll
-        for (int c = 0; c < K; ++c) issue_row(row_ptr(frag(t.i, c), t.r), b.x[c]);
+        for (int c = 0; c < K; ++c) issue_row<kS>(row_ptr(frag(t.i, c), t.r), b.x[c]);
     };
 
     GroupTask ta{0u, 0u};
     GroupTask tb = advance(ta);
     GroupTask tc = advance(tb);
     RowsK<K> A, B, Cb;
+    auto issue_all = [&] {
+        issue(ta, A);
+        issue(tb, B);
+        issue(tc, Cb);
+    };
+    constexpr size_t kComb = kCoal ? kImgCombine16Cols : kImgCombineCols;
+    constexpr size_t kHorn = kCoal ? kImgHorner16Cols : kImgHornerCols;
     if (kAblate != 2) {
         // all three ring slots are in flight while the workgroup builds its tables
-        stage_tables<12 * K>(lds, img, [&] {
-            issue(ta, A);
-            issue(tb, B);
-            issue(tc, Cb);
-        });
+        stage_tables<12 * K, decltype(issue_all), 7, kComb, kHorn>(lds, img, issue_all);
     } else {
         stage_tables<0>(lds, img, [] {});
     }
@@ -715,8 +763,9 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
 #pragma unroll
             for (int c = 0; c < K; ++c)
                 if (K * t.i + c < nfr)
-                    store_row((gwbyte *)(dst + (uint64_t)frag(t.i, c) * dst_stride + (uint64_t)t.r * kRowBytes + lane_off),
-                              b.x[c]);
+                    store_row<kS>(
+                        (gwbyte *)(dst + (uint64_t)frag(t.i, c) * dst_stride + (uint64_t)t.r * kRowBytes + lane_off),
+                        b.x[c]);
         }
         if (kAblate == 1) {
 #pragma unroll
@@ -733,14 +782,18 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
             }
             return;
         }
-        if (t.r == 0) {
-#pragma unroll
-            for (int c = 0; c < K; ++c) C[c] = (lane == 0) ? vinit : 0u;
+        if constexpr (kCoal) {
+            crc_chunks<K>(lds, k, C, b, t.r == 0, (lane == 0) ? vinit : 0u);
         } else {
+            if (t.r == 0) {
 #pragma unroll
-            for (int c = 0; c < K; ++c) C[c] = horner_shift(lds, C[c]);
+                for (int c = 0; c < K; ++c) C[c] = (lane == 0) ? vinit : 0u;
+            } else {
+#pragma unroll
+                for (int c = 0; c < K; ++c) C[c] = horner_shift(lds, C[c]);
+            }
+            crc_pieces<K>(lds, k, C, b);
         }
-        crc_pieces<K>(lds, k, C, b);
         if (t.r + 1 == R) {
             uint32_t x[K];
 #pragma unroll
@@ -849,17 +902,21 @@ __global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__re
     const uint32_t f = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
     if (f >= n) return;
     const uint32_t R = (uint32_t)(frag_len / kRowBytes);
-    gbyte *p = (gbyte *)(base + (uint64_t)f * frag_len + (uint64_t)lane * kLaneBytes);
-    gwbyte *q = kCopy ? (gwbyte *)(dst + (uint64_t)f * dst_stride + (uint64_t)lane * kLaneBytes) : nullptr;
+    // the sum is order-free: the copy moves rows in the coalesced layout (1 KiB per store
+    // instruction), the read-only sum keeps lane-contiguous 64-byte pieces
+    constexpr int kS = kCopy ? kRowBytes / 4 : 16;
+    const uint64_t lo = (uint64_t)lane * (kCopy ? kChunkBytes : kLaneBytes);
+    gbyte *p = (gbyte *)(base + (uint64_t)f * frag_len + lo);
+    gwbyte *q = kCopy ? (gwbyte *)(dst + (uint64_t)f * dst_stride + lo) : nullptr;
     uint32_t acc = 0;
     uint32_t r = 0;
     for (; r + 4 <= R; r += 4) {
         u32x4 v[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)(r + k / 4) * kRowBytes + 16 * (k & 3));
+        for (int k = 0; k < 16; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)(r + k / 4) * kRowBytes + kS * (k & 3));
         if constexpr (kCopy) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) *(gwu32x4 *)(q + (uint64_t)(r + k / 4) * kRowBytes + 16 * (k & 3)) = v[k];
+            for (int k = 0; k < 16; ++k) *(gwu32x4 *)(q + (uint64_t)(r + k / 4) * kRowBytes + kS * (k & 3)) = v[k];
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
@@ -867,10 +924,10 @@ __global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__re
     for (; r < R; ++r) {
         u32x4 v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)r * kRowBytes + 16 * k);
+        for (int k = 0; k < 4; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)r * kRowBytes + kS * k);
         if constexpr (kCopy) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) *(gwu32x4 *)(q + (uint64_t)r * kRowBytes + 16 * k) = v[k];
+            for (int k = 0; k < 4; ++k) *(gwu32x4 *)(q + (uint64_t)r * kRowBytes + kS * k) = v[k];
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;

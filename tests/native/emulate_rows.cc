@@ -64,6 +64,44 @@ static uint32_t emulate(const std::vector<uint32_t> &img, const uint8_t *msg, ui
     return res;
 }
 
+// Coalesced layout of the fused-copy kernel: lane l holds the 16-byte chunks at 16l + 1024q of
+// every row; each chunk except the first is preceded by a 1008-byte Horner step and the
+// lane's register is finally shifted by 16*(63-l) (kImgHorner16Cols / kImgCombine16Cols).
+static uint32_t emulate_coalesced(const std::vector<uint32_t> &img, const uint8_t *msg, uint32_t L,
+                                  uint32_t partial) {
+    if (L == 0) return partial;
+    const uint32_t R = (L + kRowBytes - 1) / kRowBytes;
+    const uint32_t P = R * kRowBytes - L;
+    const uint32_t v = bswap32(partial);
+    uint32_t total = 0;
+    for (int lane = 0; lane < kWave; ++lane) {
+        uint32_t C = 0;
+        for (uint32_t r = 0; r < R; ++r) {
+            for (int q = 0; q < 4; ++q) {
+                if (r || q) C = nib(&img[kImgHorner16Cols], C);
+                for (int w = 0; w < 4; ++w) {
+                    const long long fp = (long long)r * kRowBytes + q * (kRowBytes / 4) + lane * kChunkBytes + 4 * w;
+                    const long long o = fp - P;
+                    uint32_t word = 0;
+                    for (int j = 0; j < 4; ++j) {
+                        long long b = o + j;
+                        uint32_t byte = (b >= 0 && b < (long long)L) ? msg[b] : 0u;
+                        if (b >= 0 && b < 4 && b < (long long)L) byte ^= (v >> (8 * b)) & 0xFFu;
+                        word |= byte << (8 * j);
+                    }
+                    const uint32_t X = C ^ word;
+                    C = img[kImgSliceT + 4 * (X & 255u) + 0] ^ img[kImgSliceT + 4 * ((X >> 8) & 255u) + 1] ^
+                        img[kImgSliceT + 4 * ((X >> 16) & 255u) + 2] ^ img[kImgSliceT + 4 * (X >> 24) + 3];
+                }
+            }
+        }
+        total ^= nib(&img[kImgCombine16Cols + lane * 32], C);
+    }
+    uint32_t res = bswap32(total);
+    if (L < 4) res ^= partial << (8 * L);
+    return res;
+}
+
 int main(int argc, char **argv) {
     const int cases = argc > 1 ? atoi(argv[1]) : 400;
     const std::vector<uint32_t> img = build_table_image();
@@ -82,6 +120,13 @@ int main(int argc, char **argv) {
         const uint32_t got = emulate(img, buf.data(), L, partial);
         if (want != got) {
             if (++bad < 10) std::printf("MISMATCH L=%u partial=%08x want=%08x got=%08x\n", L, partial, want, got);
+        }
+        if (i % 4 == 0) {  // the coalesced decomposition (fused-copy kernel)
+            const uint32_t gc = emulate_coalesced(img, buf.data(), L, partial);
+            if (want != gc) {
+                if (++bad < 10)
+                    std::printf("MISMATCH (coalesced) L=%u partial=%08x want=%08x got=%08x\n", L, partial, want, gc);
+            }
         }
     }
     // known answer: CRC-32/MPEG-2 check value
