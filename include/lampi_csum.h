@@ -132,6 +132,36 @@ int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t 
                    uint32_t *d_out, int mode, void *stream);
 
 /* ------------------------------------------------------------------------------------
+ * Headers and receive-side verification (device-resident, batched).
+ * Headers are n records of `stride` bytes starting at d_hdrs (d_hdrs, stride and
+ * csum_offset 4-byte aligned).  Masks hold one bit per fragment, bit (i % 32) of word
+ * i / 32, SET when fragment i FAILS; *d_nbad receives the number of failures.
+ * ---------------------------------------------------------------------------------- */
+
+/* out[i] = BasePath_t::headerChecksum(hdr_i, crclen, word_count)
+ * (ref src/path/common/path.h:280-314): CRC mode the byte-swapped uicrc of the first crclen
+ * bytes (so CRC(header || stored) == 0), SUM mode the sum of word_count 32-bit words.
+ * Senders: src/path/gm/sendFrag.cc:218-225, gm/recvFrag.cc:125-130, quadrics/sendFrag.h:876-879. */
+int lampi_header_csum_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen,
+                            uint32_t word_count, uint32_t *d_out, int mode, void *stream);
+
+/* Receiver header check (ref src/path/gm/path.cc:364-393): header i fails unless
+ * CRC mode: uicrc(hdr_i, hdr_bytes) == 0 (the whole header including the stored checksum);
+ * SUM mode: the sum of word_count words == 2 x the stored checksum at csum_offset. */
+int lampi_header_check_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t hdr_bytes,
+                             uint32_t word_count, uint32_t csum_offset, uint32_t *d_mask,
+                             uint32_t *d_nbad, int mode, void *stream);
+
+/* CheckData (ref src/path/gm/recvFrag.h:213-257): fragment i fails iff its length is nonzero
+ * and d_calc[i] != its expected checksum.  Expected checksums and lengths are 32-bit values
+ * read at d_expected + i*expected_stride and d_lengths + i*lengths_stride -- e.g. straight
+ * from an array of gmHeaderData (dataChecksum @64, dataLength @20, stride = the record size).
+ * d_lengths may be NULL (every length nonzero). */
+int lampi_check_data_batch(const uint32_t *d_calc, const void *d_expected, size_t expected_stride,
+                           const void *d_lengths, size_t lengths_stride, size_t n, uint32_t *d_mask,
+                           uint32_t *d_nbad, void *stream);
+
+/* ------------------------------------------------------------------------------------
  * Utilities (bench/test support, device-side).
  * ---------------------------------------------------------------------------------- */
 

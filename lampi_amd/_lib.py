@@ -57,6 +57,12 @@ PROTOTYPES = {
     "lampi_frag_bcopy_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_msg_bcopy": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, ctypes.c_uint32, c_void_p,
                                        ctypes.c_int, c_void_p]),
+    "lampi_header_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, ctypes.c_uint32, c_void_p,
+                                               ctypes.c_int, c_void_p]),
+    "lampi_header_check_batch": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_int, c_void_p]),
+    "lampi_check_data_batch": (ctypes.c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_void_p,
+                                              c_void_p, c_void_p]),
     "lampi_msg_csum": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, c_void_p, ctypes.c_int,
                                       c_void_p]),
     "lampi_fill_stream": (ctypes.c_int, [c_void_p, c_size_t, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),

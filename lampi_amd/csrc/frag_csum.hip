@@ -695,14 +695,13 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // them (first pass: 8K / 12K / 16K younger operations, then 16K).  Rows move in the coalesced
 // layout (crc_chunks): lane-contiguous 64-byte stores run at 51% of the HBM roofline on
 // MI355X against 71% for 1 KiB-per-instruction stores (profiles/r01_copy_patterns.txt).
-template <int kAblate, int kChains, bool kCopy = false>
+template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy>
 __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
                                                              uint32_t fpw, size_t frag_len, uint32_t partial,
                                                              const uint32_t *__restrict__ img,
                                                              uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
                                                              size_t dst_stride) {
     constexpr int K = kChains;
-    constexpr bool kCoal = kCopy;                   // coalesced row layout
     constexpr int kS = kCoal ? kRowBytes / 4 : 16;  // chunk stride of a lane
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
@@ -934,6 +933,96 @@ __global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__re
     }
     acc = wave_add(acc);
     if (lane == 0) out[f] = acc;
+}
+
+// ---- headers and receive-side verification -----------------------------------------------
+// Headers are small (68-128 B): one thread per header, slicing-by-4 in the swapped domain
+// from a 4 KiB LDS copy of the tables (S_j[i] at j*256 + i), byte steps C = (C >> 8) ^
+// S_3[(C ^ b) & 255] for a ragged tail.  Header addresses are 4-byte aligned (host-checked).
+__device__ __forceinline__ uint32_t thread_crc(const uint32_t *S, gbyte *p, uint32_t len, uint32_t partial) {
+    uint32_t C = __builtin_bswap32(partial);
+    uint32_t i = 0;
+    for (; i + 4 <= len; i += 4) {
+        const uint32_t X = C ^ *(guint *)(p + i);
+        C = S[X & 255u] ^ S[256 + ((X >> 8) & 255u)] ^ S[512 + ((X >> 16) & 255u)] ^ S[768 + (X >> 24)];
+    }
+    for (; i < len; ++i) C = (C >> 8) ^ S[768 + ((C ^ p[i]) & 255u)];
+    return __builtin_bswap32(C);
+}
+
+__device__ __forceinline__ void stage_slices(uint32_t *S, const uint32_t *__restrict__ img) {
+    for (uint32_t t = threadIdx.x; t < 1024; t += blockDim.x) S[(t & 3u) * 256 + (t >> 2)] = img[kImgSliceT + t];
+    __syncthreads();
+}
+
+// BasePath_t::headerChecksum (ref src/path/common/path.h:280-314): CRC mode bswap(uicrc(h, crclen))
+// (so that CRC(header || stored) == 0), SUM mode the sum of word_count 32-bit words.
+__global__ void __launch_bounds__(256) header_csum_kernel(const uint8_t *__restrict__ hdrs, uint32_t n, size_t stride,
+                                                          uint32_t crclen, uint32_t word_count, int mode,
+                                                          const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
+    __shared__ uint32_t S[1024];
+    if (mode == LAMPI_CSUM_CRC32) stage_slices(S, img);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    gbyte *h = (gbyte *)(hdrs + (size_t)i * stride);
+    uint32_t v = 0;
+    if (mode == LAMPI_CSUM_CRC32) {
+        v = __builtin_bswap32(thread_crc(S, h, crclen, kCrcInit));
+    } else {
+        for (uint32_t w = 0; w < word_count; ++w) v += *(guint *)(h + 4 * w);
+    }
+    out[i] = v;
+}
+
+// One bit per fragment, set when it FAILS (wave ballot -> two mask words), plus a count.
+__device__ __forceinline__ void emit_mask(uint32_t i, uint32_t n, bool bad, uint32_t *mask, uint32_t *nbad) {
+    const uint64_t b = __ballot(bad && i < n);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w0 = (i - lane) / 32;  // first mask word of this wave (i - lane is a multiple of 64)
+    if (lane == 0 && i < n) mask[w0] = (uint32_t)b;
+    if (lane == 32 && i < n) mask[w0 + 1] = (uint32_t)(b >> 32);
+    if (lane == 0 && b) atomicAdd(nbad, (uint32_t)__popcll(b));
+}
+
+// Receiver header check (ref src/path/gm/path.cc:364-393): CRC mode accepts iff
+// uicrc(header, hdr_bytes) == 0 over the whole header including the stored checksum; SUM mode
+// iff the sum of word_count words == 2 x the stored checksum (at csum_offset).
+__global__ void __launch_bounds__(256) header_check_kernel(const uint8_t *__restrict__ hdrs, uint32_t n, size_t stride,
+                                                           uint32_t hdr_bytes, uint32_t word_count,
+                                                           uint32_t csum_offset, int mode,
+                                                           const uint32_t *__restrict__ img, uint32_t *mask,
+                                                           uint32_t *nbad) {
+    __shared__ uint32_t S[1024];
+    if (mode == LAMPI_CSUM_CRC32) stage_slices(S, img);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    if (i < n) {
+        gbyte *h = (gbyte *)(hdrs + (size_t)i * stride);
+        if (mode == LAMPI_CSUM_CRC32) {
+            bad = thread_crc(S, h, hdr_bytes, kCrcInit) != 0u;
+        } else {
+            uint32_t v = 0;
+            for (uint32_t w = 0; w < word_count; ++w) v += *(guint *)(h + 4 * w);
+            const uint32_t stored = *(guint *)(h + csum_offset);
+            bad = v != stored + stored;
+        }
+    }
+    emit_mask(i, n, bad, mask, nbad);
+}
+
+// CheckData (ref src/path/gm/recvFrag.h:213-257): fragment i is corrupt iff its length is
+// nonzero and calc[i] != expected; expected values and lengths are read through byte strides
+// (e.g. straight out of an array of headers: dataChecksum @64, dataLength @20).
+__global__ void __launch_bounds__(256) check_data_kernel(const uint32_t *__restrict__ calc, const uint8_t *expected,
+                                                         size_t exp_stride, const uint8_t *lengths, size_t len_stride,
+                                                         uint32_t n, uint32_t *mask, uint32_t *nbad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    if (i < n) {
+        const uint32_t len = lengths ? *(guint *)(lengths + (size_t)i * len_stride) : 1u;
+        bad = len != 0 && calc[i] != *(guint *)(expected + (size_t)i * exp_stride);
+    }
+    emit_mask(i, n, bad, mask, nbad);
 }
 
 // ---- synthetic stream fill ----------------------------------------------------------------
@@ -1194,6 +1283,33 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
     const uint32_t fpw = pick_fpw(n, 1);
     hipLaunchKernelGGL(sum_rows_kernel<MsgCopySource>, grid_for(n, fpw), dim3(kBlock), 0, s,
                        MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, fpw, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_header_csum(const uint8_t *hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
+                              int mode, const uint32_t *img, uint32_t *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(header_csum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hdrs, (uint32_t)n, stride,
+                       crclen, word_count, mode, img, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_header_check(const uint8_t *hdrs, size_t n, size_t stride, uint32_t hdr_bytes, uint32_t word_count,
+                               uint32_t csum_offset, int mode, const uint32_t *img, uint32_t *mask, uint32_t *nbad,
+                               hipStream_t s) {
+    hipError_t e = hipMemsetAsync(nbad, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n == 0) return e;
+    hipLaunchKernelGGL(header_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hdrs, (uint32_t)n,
+                       stride, hdr_bytes, word_count, csum_offset, mode, img, mask, nbad);
+    return hipGetLastError();
+}
+
+hipError_t launch_check_data(const uint32_t *calc, const uint8_t *expected, size_t exp_stride, const uint8_t *lengths,
+                             size_t len_stride, size_t n, uint32_t *mask, uint32_t *nbad, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(nbad, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n == 0) return e;
+    hipLaunchKernelGGL(check_data_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, calc, expected,
+                       exp_stride, lengths, len_stride, (uint32_t)n, mask, nbad);
     return hipGetLastError();
 }
 

@@ -339,6 +339,51 @@ int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_
                                    d_out, mode, img, (hipStream_t)stream));
 }
 
+int lampi_header_csum_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
+                            uint32_t *d_out, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (n == 0) return 0;
+    if (!d_hdrs || !d_out || ((uintptr_t)d_hdrs & 3u) || (stride & 3u) || n > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_header_csum((const uint8_t *)d_hdrs, n, stride, crclen, word_count, mode, img, d_out,
+                                     (hipStream_t)stream));
+}
+
+int lampi_header_check_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t hdr_bytes, uint32_t word_count,
+                             uint32_t csum_offset, uint32_t *d_mask, uint32_t *d_nbad, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (!d_nbad || (n && (!d_hdrs || !d_mask)) || ((uintptr_t)d_hdrs & 3u) || (stride & 3u) || (csum_offset & 3u) ||
+        n > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_header_check((const uint8_t *)d_hdrs, n, stride, hdr_bytes, word_count, csum_offset, mode,
+                                      img, d_mask, d_nbad, (hipStream_t)stream));
+}
+
+int lampi_check_data_batch(const uint32_t *d_calc, const void *d_expected, size_t expected_stride,
+                           const void *d_lengths, size_t lengths_stride, size_t n, uint32_t *d_mask, uint32_t *d_nbad,
+                           void *stream) {
+    if (!d_nbad || (n && (!d_calc || !d_expected || !d_mask)) || ((uintptr_t)d_expected & 3u) ||
+        (expected_stride & 3u) || ((uintptr_t)d_lengths & 3u) || (lengths_stride & 3u) || n > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_check_data(d_calc, (const uint8_t *)d_expected, expected_stride, (const uint8_t *)d_lengths,
+                                    lengths_stride, n, d_mask, d_nbad, (hipStream_t)stream));
+}
+
 int lampi_fill_stream(void *d_dst, size_t nbytes, uint64_t seed, uint64_t byte_off, void *stream) {
     if (nbytes == 0) return 0;
     if (!d_dst) return to_int(hipErrorInvalidValue);

@@ -12,7 +12,8 @@ import torch
 from ._lib import CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
 
 __all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
-           "make_descs", "make_copy_descs", "as_u32"]
+           "make_descs", "make_copy_descs", "as_u32", "header_csum_batch", "header_check_batch", "check_data_batch",
+           "mask_bits"]
 
 
 def _stream_handle(stream: torch.cuda.Stream | None) -> int:
@@ -151,6 +152,63 @@ def msg_bcopy(msg: torch.Tensor, frag_len: int, dst: torch.Tensor, dst_stride: i
     check(lib().lampi_msg_bcopy(msg.data_ptr(), nbytes, frag_len, dst.data_ptr(), stride, partial & 0xFFFFFFFF,
                                 out.data_ptr(), mode, _stream_handle(stream)), "lampi_msg_bcopy")
     return out
+
+
+def _records(t: torch.Tensor, n: int, stride: int, what: str) -> None:
+    _require_cuda(t, what)
+    if n and (n - 1) * stride + 4 > t.numel() * t.element_size():
+        raise ValueError(f"{what} is too small for {n} records of stride {stride}")
+
+
+def header_csum_batch(hdrs: torch.Tensor, n: int, stride: int, crclen: int, word_count: int, mode: int = CRC32,
+                      out: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """BasePath_t::headerChecksum of n headers ``stride`` bytes apart (src/path/common/path.h:280-314)."""
+    _records(hdrs, n, stride, "hdrs")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=hdrs.device)
+    check(lib().lampi_header_csum_batch(hdrs.data_ptr(), n, stride, crclen, word_count, out.data_ptr(), mode,
+                                        _stream_handle(stream)), "lampi_header_csum_batch")
+    return out
+
+
+def _mask_out(n: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    return (torch.zeros(max(1, (n + 31) // 32), dtype=torch.int32, device=device),
+            torch.zeros(1, dtype=torch.int32, device=device))
+
+
+def header_check_batch(hdrs: torch.Tensor, n: int, stride: int, hdr_bytes: int, word_count: int, csum_offset: int,
+                       mode: int = CRC32, stream: torch.cuda.Stream | None = None):
+    """Receiver header check (src/path/gm/path.cc:364-393); returns (mask, nbad), mask bit set = bad."""
+    _records(hdrs, n, stride, "hdrs")
+    mask, nbad = _mask_out(n, hdrs.device)
+    check(lib().lampi_header_check_batch(hdrs.data_ptr(), n, stride, hdr_bytes, word_count, csum_offset,
+                                         mask.data_ptr(), nbad.data_ptr(), mode, _stream_handle(stream)),
+          "lampi_header_check_batch")
+    return mask, nbad
+
+
+def check_data_batch(calc: torch.Tensor, expected: torch.Tensor, expected_stride: int = 4,
+                     lengths: torch.Tensor | None = None, lengths_stride: int = 4, n: int | None = None,
+                     expected_offset: int = 0, lengths_offset: int = 0, stream: torch.cuda.Stream | None = None):
+    """CheckData over a batch (src/path/gm/recvFrag.h:213-257); returns (mask, nbad), bit set = corrupt."""
+    _require_cuda(calc, "calc")
+    count = calc.numel() if n is None else int(n)
+    _records(expected, count, expected_stride, "expected")
+    lp = 0
+    if lengths is not None:
+        _records(lengths, count, lengths_stride, "lengths")
+        lp = lengths.data_ptr() + lengths_offset
+    mask, nbad = _mask_out(count, calc.device)
+    check(lib().lampi_check_data_batch(calc.data_ptr(), expected.data_ptr() + expected_offset, expected_stride,
+                                       lp or None, lengths_stride, count, mask.data_ptr(), nbad.data_ptr(),
+                                       _stream_handle(stream)), "lampi_check_data_batch")
+    return mask, nbad
+
+
+def mask_bits(mask: torch.Tensor, n: int) -> np.ndarray:
+    """Device mask words -> bool array of length n (True = failed)."""
+    w = mask.cpu().numpy().view(np.uint32)
+    return ((w[np.arange(n) // 32] >> (np.arange(n) % 32).astype(np.uint32)) & 1).astype(bool)
 
 
 def fill_stream(dst: torch.Tensor, seed: int, byte_off: int = 0, nbytes: int | None = None,

@@ -82,17 +82,17 @@ int main(int argc, char **argv) {
     if (argc > 2) return 0;  // probes only
     for (size_t L : {4096ul, 16384ul}) {
         const uint32_t n = (uint32_t)(bytes / L);
-        for (int chains : {2})
-        for (uint32_t fpw : (L == 4096 ? std::vector<uint32_t>{16u, 24u, 32u, 40u, 48u, 64u}
-                                       : std::vector<uint32_t>{4u, 8u, 12u, 16u})) {
+        const int chains = 2;
+        for (int coal : {0, 1})  // 1: coalesced row layout (the fused-copy kernel's), read only
+        for (uint32_t fpw : (L == 4096 ? std::vector<uint32_t>{16u, 32u, 48u} : std::vector<uint32_t>{8u, 12u})) {
             const dim3 grid((n + kWaves * fpw - 1) / (kWaves * fpw));
             for (int v = 0; v < 3; ++v) {
                 auto launch = [&] {
-#define LK(V, K) hipLaunchKernelGGL((crc_regular_kernel<V, K>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu, dimg, out, nullptr, (size_t)0)
-                    if (chains == 2) {
-                        if (v == 0) LK(0, 2); else if (v == 1) LK(1, 2); else LK(2, 2);
+#define LK(V, C) hipLaunchKernelGGL((crc_regular_kernel<V, 2, false, C>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu, dimg, out, nullptr, (size_t)0)
+                    if (coal == 0) {
+                        if (v == 0) LK(0, false); else if (v == 1) LK(1, false); else LK(2, false);
                     } else {
-                        if (v == 0) LK(0, 4); else if (v == 1) LK(1, 4); else LK(2, 4);
+                        if (v == 0) LK(0, true); else if (v == 1) LK(1, true); else LK(2, true);
                     }
 #undef LK
                 };
@@ -106,7 +106,8 @@ int main(int argc, char **argv) {
                 float ms;
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 const double s = ms / 1e3 / reps;
-                printf("K=%d L=%5zu fpw=%2u %-13s grid=%6u  %8.3f ms  %8.1f GB/s  %5.1f%% of 8 TB/s\n", chains, L, fpw, names[v],
+                printf("K=%d %s L=%5zu fpw=%2u %-13s grid=%6u  %8.3f ms  %8.1f GB/s  %5.1f%% of 8 TB/s\n", chains,
+                       coal ? "coal" : "lane", L, fpw, names[v],
                        grid.x, s * 1e3, bytes / s / 1e9, bytes / s / 8e12 * 100);
                 fflush(stdout);
                 (void)0;
