@@ -116,6 +116,21 @@ typedef struct lampi_copy_desc {
 int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d_out, int mode,
                            void *stream);
 
+/* Chained checksums over typemap pieces (non-contiguous datatypes).  Fragment f is the
+ * concatenation of the checksummed ranges (max(copylen, csumlen) bytes at src) of pieces
+ * d_pieces[d_first[f]] .. d_pieces[d_first[f+1] - 1], in that order (d_first: nfrags + 1
+ * nondecreasing entries); each piece is also copied to its dst (copylen bytes, 0 = no copy).
+ * out[f] = what the reference's piece-by-piece calls return: CRC mode the register threaded
+ * through every piece from d_pieces[d_first[f]].partial (0xFFFFFFFF for a fragment with no
+ * pieces; other pieces' partial is ignored), SUM mode the total of the increments with the
+ * partial-word state threaded from a fresh state -- i.e. the checksum of the packed bytes.
+ * Send side: gather into the payload, src/path/gm/sendFrag.cc:157-217 (also ib/sendFrag.cc:140-203,
+ * quadrics/sendFrag.h:988-1051); receive side: scatter to the application buffer,
+ * src/path/common/BaseDesc.cc:72-163.  Fragments up to 4 GiB - 1 bytes.  Uses
+ * 8 * npieces bytes of stream-ordered scratch. */
+int lampi_chain_csum_batch(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first,
+                           size_t nfrags, uint32_t *d_out, int mode, void *stream);
+
 /* Fragments a contiguous device-resident message like lampi_msg_csum and copies fragment k
  * to d_dst + k*dst_stride (dst_stride >= frag_len; e.g. frag_len for a plain copy, or the
  * slot size of a staging ring) with its checksum fused: bcopy_uicrc / bcopy_uicsum of every

@@ -57,6 +57,8 @@ PROTOTYPES = {
     "lampi_frag_bcopy_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_msg_bcopy": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, ctypes.c_uint32, c_void_p,
                                        ctypes.c_int, c_void_p]),
+    "lampi_chain_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, ctypes.c_int,
+                                              c_void_p]),
     "lampi_header_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, ctypes.c_uint32, c_void_p,
                                                ctypes.c_int, c_void_p]),
     "lampi_header_check_batch": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, ctypes.c_uint32,

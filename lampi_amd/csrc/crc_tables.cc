@@ -112,6 +112,13 @@ std::vector<uint32_t> build_table_image() {
     }
     const Gf2Mat h16 = swapped(shift_matrix(kChunkStep));
     for (int b = 0; b < 32; ++b) img[kImgHorner16Cols + b] = h16.col[b];
+
+    // powers of two for arbitrary shifts, normal domain (squaring from one byte)
+    Gf2Mat pw = shift_matrix(1);
+    for (int e = 0; e < 32; ++e) {
+        for (int c = 0; c < 32; ++c) img[kImgPow2Cols + e * 32 + c] = pw.col[c];
+        pw = mat_mul(pw, pw);
+    }
     return img;
 }
 

@@ -72,6 +72,7 @@ struct FragInfo {
 // ---- fragment sources (wave-uniform) ----------------------------------------------
 struct DescSource {
     static constexpr bool kCopy = false;
+    static constexpr bool kPhase = false;  // SUM: partial & 3 is the byte phase (PieceSource only)
     const lampi_frag_desc *d;
     __device__ FragInfo get(size_t f) const {
         const lampi_frag_desc x = d[f];
@@ -83,6 +84,7 @@ struct DescSource {
 // checksum max(copylen, csumlen) bytes of the source (the residue is checksummed, not copied)
 struct CopySource {
     static constexpr bool kCopy = true;
+    static constexpr bool kPhase = false;
     const lampi_copy_desc *d;
     __device__ FragInfo get(size_t f) const {
         const lampi_copy_desc x = d[f];
@@ -93,6 +95,7 @@ struct CopySource {
 
 struct MsgSource {
     static constexpr bool kCopy = false;
+    static constexpr bool kPhase = false;
     const uint8_t *base;
     size_t msg_len;
     size_t frag_len;
@@ -107,6 +110,7 @@ struct MsgSource {
 // fragment k of a contiguous message copied to dst + k*dst_stride (bcopy of every fragment)
 struct MsgCopySource {
     static constexpr bool kCopy = true;
+    static constexpr bool kPhase = false;
     const uint8_t *base;
     size_t msg_len;
     size_t frag_len;
@@ -118,6 +122,24 @@ struct MsgCopySource {
         size_t rem = msg_len - off;
         const uint32_t len = (uint32_t)(rem < frag_len ? rem : frag_len);
         return {(gbyte *)(base + off), len, partial, dst + f * dst_stride, len};
+    }
+};
+
+// Typemap pieces of chained checksums (lampi_chain_csum_batch): pieces longer than `small`
+// bytes; the others read as empty here and are done one thread per piece.  CRC values start
+// from a zero register (the chain fold threads the caller's register); SUM values are taken at
+// the piece's byte phase in its fragment's word grid (phase[k], partial-word chaining).
+struct PieceSource {
+    static constexpr bool kCopy = true;
+    static constexpr bool kPhase = true;
+    const lampi_copy_desc *d;
+    const uint32_t *phase;  // SUM only (nullptr for CRC)
+    uint32_t small;
+    __device__ FragInfo get(size_t f) const {
+        const lampi_copy_desc x = d[f];
+        const uint32_t len = x.copylen > x.csumlen ? x.copylen : x.csumlen;
+        if (len <= small) return {(gbyte *)(uintptr_t)x.src, 0u, 0u, nullptr, 0u};
+        return {(gbyte *)(uintptr_t)x.src, len, phase ? phase[f] : 0u, (uint8_t *)(uintptr_t)x.dst, x.copylen};
     }
 };
 
@@ -311,43 +333,43 @@ __device__ __forceinline__ void load64(gbyte *frag, long long o, long long lo, l
 }
 
 // ---- stores (fused copy) --------------------------------------------------------------
-// Aligned word at dst + c (c may be negative): whole-word store when all four bytes lie in
-// [0, hi), byte stores for a word straddling an edge, nothing outside.
-__device__ __forceinline__ void store_word(uint8_t *dst, long long c, uint32_t v, long long hi) {
-    if (c >= 0 && c + 4 <= hi) {
+// Aligned word at dst + c: whole-word store when all four bytes lie in [lo, hi), byte stores
+// for a word straddling an edge, nothing outside.
+__device__ __forceinline__ void store_word(uint8_t *dst, long long c, uint32_t v, long long lo, long long hi) {
+    if (c >= lo && c + 4 <= hi) {
         *(gwuint *)(dst + c) = v;
-    } else if (c + 4 > 0 && c < hi) {
+    } else if (c + 4 > lo && c < hi) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            if (c + j >= 0 && c + j < hi) *(gwbyte *)(dst + c + j) = (uint8_t)(v >> (8 * j));
+            if (c + j >= lo && c + j < hi) *(gwbyte *)(dst + c + j) = (uint8_t)(v >> (8 * j));
     }
 }
 
-// Write the 64 bytes d[16] (fragment bytes [o, o+64)) to dst + o, keeping only bytes in [0, hi).
-// m = (dst + o) & 3 and a16 = ((dst + o) & 15) == 0 are wave-uniform.  For m != 0 a lane writes
-// the aligned words covering [o - m, o - m + 64): their first m bytes are the top of the
-// previous lane's piece (`prev`), and the lane holding the frame's last piece (`tail`) also
-// writes the word at o - m + 64.
-__device__ __forceinline__ void store64(uint8_t *dst, long long o, const uint32_t d[16], long long hi, uint32_t m,
-                                        bool a16, uint32_t prev, bool tail) {
-    if (o - (long long)m >= hi || o + 64 <= 0) return;
+// Write the 64 bytes d[16] (bytes [o, o+64) of the frame) to dst + o, keeping only bytes in
+// [lo, hi).  m = (dst + o) & 3 and a16 = ((dst + o) & 15) == 0 are wave-uniform.  For m != 0 a
+// lane writes the aligned words covering [o - m, o - m + 64): their first m bytes are the top
+// of the previous lane's piece (`prev`), and the lane holding the frame's last piece (`tail`)
+// also writes the word at o - m + 64.
+__device__ __forceinline__ void store64(uint8_t *dst, long long o, const uint32_t d[16], long long lo, long long hi,
+                                        uint32_t m, bool a16, uint32_t prev, bool tail) {
+    if (o - (long long)m >= hi || o + 64 <= lo) return;
     if (m == 0) {
-        if (a16 && o >= 0 && o + 64 <= hi) {
+        if (a16 && o >= lo && o + 64 <= hi) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 *(gwu32x4 *)(dst + o + 16 * k) = u32x4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
             return;
         }
 #pragma unroll
-        for (int w = 0; w < 16; ++w) store_word(dst, o + 4 * w, d[w], hi);
+        for (int w = 0; w < 16; ++w) store_word(dst, o + 4 * w, d[w], lo, hi);
         return;
     }
     const long long a = o - (long long)m;
     const uint32_t sh = 4u - m;
-    store_word(dst, a, __builtin_amdgcn_alignbyte(d[0], prev, sh), hi);
+    store_word(dst, a, __builtin_amdgcn_alignbyte(d[0], prev, sh), lo, hi);
 #pragma unroll
-    for (int w = 1; w < 16; ++w) store_word(dst, a + 4 * w, __builtin_amdgcn_alignbyte(d[w], d[w - 1], sh), hi);
-    if (tail) store_word(dst, a + 64, __builtin_amdgcn_alignbyte(0u, d[15], sh), hi);
+    for (int w = 1; w < 16; ++w) store_word(dst, a + 4 * w, __builtin_amdgcn_alignbyte(d[w], d[w - 1], sh), lo, hi);
+    if (tail) store_word(dst, a + 64, __builtin_amdgcn_alignbyte(0u, d[15], sh), lo, hi);
 }
 
 // d[15] of lane - 1 (lane 0 gets `carry`, the last lane's word of the previous row)
@@ -551,7 +573,7 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
                 const uint32_t dm = (uint32_t)((uintptr_t)cur.dst - g.P) & 15u;
                 if (r == 0) carry = 0;
                 const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
-                store64(cur.dst, o, d, (long long)cur.copylen, dm & 3u, dm == 0, prev, lane == 63 && r + 1 == g.R);
+                store64(cur.dst, o, d, 0, (long long)cur.copylen, dm & 3u, dm == 0, prev, lane == 63 && r + 1 == g.R);
                 carry = __builtin_amdgcn_readlane(d[15], 63);
             }
         }
@@ -864,19 +886,25 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
             fi.dst = (uint8_t *)uniform64((uint64_t)(uintptr_t)fi.dst);
             fi.copylen = uniform(fi.copylen);
         }
-        const uint32_t R = (fi.len + (kRowBytes - 1)) / kRowBytes;
-        const uint32_t s16 = (uint32_t)((uintptr_t)fi.addr & 15u);
-        const uint32_t dm = (uint32_t)((uintptr_t)fi.dst & 15u);
+        // byte phase of the first byte in the word grid (chained pieces); the frame starts
+        // `ph` bytes early and those bytes read as zero
+        const uint32_t ph = Src::kPhase ? (uniform(fi.partial) & 3u) : 0u;
+        gbyte *fb = fi.addr - ph;
+        const uint32_t span = fi.len + ph;
+        const uint32_t R = (span + (kRowBytes - 1)) / kRowBytes;
+        const uint32_t s16 = (uint32_t)((uintptr_t)fb & 15u);
+        uint8_t *db = fi.dst - ph;
+        const uint32_t dm = (uint32_t)((uintptr_t)db & 15u);
         uint32_t acc = 0, carry = 0;
         for (uint32_t r = 0; r < R; ++r) {
             const long long o = (long long)r * kRowBytes + lane * kLaneBytes;
-            const bool mask = (r + 1 == R) && (fi.len % kRowBytes != 0 || s16 != 0);
+            const bool mask = (r == 0 && ph != 0) || (r + 1 == R && span % kRowBytes != 0) || s16 != 0;
             uint32_t d[16];
-            load64(fi.addr, o, 0, (long long)fi.len, mask || s16 != 0, s16, d);
+            load64(fb, o, ph, (long long)span, mask, s16, d);
             if constexpr (Src::kCopy) {
                 if (fi.copylen) {
                     const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
-                    store64(fi.dst, o, d, (long long)fi.copylen, dm & 3u, dm == 0, prev, lane == 63 && r + 1 == R);
+                    store64(db, o, d, ph, (long long)fi.copylen + ph, dm & 3u, dm == 0, prev, lane == 63 && r + 1 == R);
                     carry = __builtin_amdgcn_readlane(d[15], 63);
                 }
             }
@@ -1023,6 +1051,133 @@ __global__ void __launch_bounds__(256) check_data_kernel(const uint32_t *__restr
         bad = len != 0 && calc[i] != *(guint *)(expected + (size_t)i * exp_stride);
     }
     emit_mask(i, n, bad, mask, nbad);
+}
+
+// ---- chained checksums over typemap pieces ------------------------------------------------
+// Fragment f = pieces first[f] .. first[f+1]-1 concatenated (ref src/path/gm/sendFrag.cc:157-217,
+// src/path/common/BaseDesc.cc:72-163).  Pass 1 (SUM only): byte phase of every piece.  Pass 2:
+// per-piece values, large pieces one wavefront each (crc_rows_kernel / sum_rows_kernel over
+// PieceSource), small ones one thread each (below).  Pass 3: one wavefront per fragment folds
+// them: CRC (C, len) pairs combine as (a, la) . (b, lb) = (shift_lb(a) ^ b, la + lb) --
+// associative, so lanes fold contiguous runs of pieces and a DPP-free shuffle tree joins the
+// lanes -- and the caller's register enters as shift_total(partial); SUM values just add.
+__global__ void __launch_bounds__(256) chain_phase_kernel(const lampi_copy_desc *__restrict__ d,
+                                                          const uint32_t *__restrict__ first, uint32_t nfrags,
+                                                          uint32_t *__restrict__ phase) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nfrags) return;
+    uint32_t off = 0;
+    for (uint32_t k = first[f]; k < first[f + 1]; ++k) {
+        phase[k] = off & 3u;
+        const uint32_t len = d[k].copylen > d[k].csumlen ? d[k].copylen : d[k].csumlen;
+        off += len;
+    }
+}
+
+// pieces of at most `small` bytes: byte / aligned-word loops in one thread
+__global__ void __launch_bounds__(256) chain_small_kernel(const lampi_copy_desc *__restrict__ d, uint32_t npieces,
+                                                          const uint32_t *__restrict__ phase, uint32_t small, int mode,
+                                                          const uint32_t *__restrict__ img, uint32_t *__restrict__ vals) {
+    __shared__ uint32_t S[1024];
+    if (mode == LAMPI_CSUM_CRC32) stage_slices(S, img);
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= npieces) return;
+    const lampi_copy_desc x = d[k];
+    const uint32_t len = x.copylen > x.csumlen ? x.copylen : x.csumlen;
+    if (len > small) return;
+    gbyte *p = (gbyte *)(uintptr_t)x.src;
+    gwbyte *q = (gwbyte *)(uintptr_t)x.dst;
+    for (uint32_t i = 0; i < x.copylen; ++i) q[i] = p[i];
+    if (mode == LAMPI_CSUM_CRC32) {
+        uint32_t C = 0;  // swapped domain, zero register
+        uint32_t i = 0;
+        for (; i < len && (((uintptr_t)(p + i)) & 3u); ++i) C = (C >> 8) ^ S[768 + ((C ^ p[i]) & 255u)];
+        for (; i + 4 <= len; i += 4) {
+            const uint32_t X = C ^ *(guint *)(p + i);
+            C = S[X & 255u] ^ S[256 + ((X >> 8) & 255u)] ^ S[512 + ((X >> 16) & 255u)] ^ S[768 + (X >> 24)];
+        }
+        for (; i < len; ++i) C = (C >> 8) ^ S[768 + ((C ^ p[i]) & 255u)];
+        vals[k] = __builtin_bswap32(C);
+    } else {
+        const uint32_t ph = phase[k];
+        uint32_t acc = 0, i = 0;
+        for (; i < len && (((uintptr_t)(p + i)) & 3u); ++i) acc += (uint32_t)p[i] << (8 * ((ph + i) & 3u));
+        for (; i + 4 <= len; i += 4) {  // a whole word lands rotated by its phase
+            const uint32_t w = *(guint *)(p + i);
+            const uint32_t r = 8 * ((ph + i) & 3u);
+            acc += r ? (w << r) | (w >> (32 - r)) : w;
+        }
+        for (; i < len; ++i) acc += (uint32_t)p[i] << (8 * ((ph + i) & 3u));
+        vals[k] = acc;
+    }
+}
+
+// C after `len` zero bytes (normal domain), T[e*128 + p*16 + v] = shift_{2^e}(v << 4p)
+__device__ __forceinline__ uint32_t shift_by(const uint32_t *T, uint32_t C, uint32_t len) {
+    while (len) {
+        const uint32_t e = __builtin_ctz(len);
+        len &= len - 1;
+        const uint32_t *t = T + e * 128;
+        uint32_t r = 0;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) r ^= t[p * 16 + ((C >> (4 * p)) & 15u)];
+        C = r;
+    }
+    return C;
+}
+
+__global__ void __launch_bounds__(256) chain_fold_kernel(const lampi_copy_desc *__restrict__ d,
+                                                         const uint32_t *__restrict__ first, uint32_t nfrags,
+                                                         const uint32_t *__restrict__ vals, int mode,
+                                                         const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
+    __shared__ uint32_t T[32 * 128];  // 16 KiB: nibble tables of shift by 2^e bytes
+    if (mode == LAMPI_CSUM_CRC32) {
+        for (uint32_t t = threadIdx.x; t < 32 * 128; t += blockDim.x) {
+            const uint32_t e = t >> 7, p = (t >> 4) & 7u, v = t & 15u;
+            const uint32_t *col = img + kImgPow2Cols + e * 32 + 4 * p;
+            uint32_t x = 0;
+            if (v & 1) x ^= col[0];
+            if (v & 2) x ^= col[1];
+            if (v & 4) x ^= col[2];
+            if (v & 8) x ^= col[3];
+            T[t] = x;
+        }
+        __syncthreads();
+    }
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t f = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
+    if (f >= nfrags) return;
+    const uint32_t k0 = first[f], k1 = first[f + 1];
+    const uint32_t np = k1 > k0 ? k1 - k0 : 0u;
+    const uint32_t per = (np + 63) / 64;  // contiguous run of pieces per lane
+    const uint32_t a = k0 + min(np, lane * per), b = k0 + min(np, (lane + 1) * per);
+    if (mode != LAMPI_CSUM_CRC32) {
+        uint32_t acc = 0;
+        for (uint32_t k = a; k < b; ++k) acc += vals[k];
+        acc = wave_add(acc);
+        if (lane == 0) out[f] = acc;
+        return;
+    }
+    uint32_t C = 0, L = 0;
+    for (uint32_t k = a; k < b; ++k) {
+        const uint32_t len = d[k].copylen > d[k].csumlen ? d[k].copylen : d[k].csumlen;
+        C = shift_by(T, C, len) ^ vals[k];
+        L += len;
+    }
+    // ordered tree: at distance s, lane l (l % 2s == 0) absorbs lane l + s
+#pragma unroll
+    for (uint32_t s = 1; s < 64; s <<= 1) {
+        const uint32_t oc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + s) & 63u) * 4), (int)C);
+        const uint32_t ol = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + s) & 63u) * 4), (int)L);
+        if ((lane & (2 * s - 1)) == 0) {
+            C = shift_by(T, C, ol) ^ oc;
+            L += ol;
+        }
+    }
+    if (lane == 0) {
+        const uint32_t partial = np ? d[k0].partial : kCrcInit;
+        out[f] = shift_by(T, partial, L) ^ C;
+    }
 }
 
 // ---- synthetic stream fill ----------------------------------------------------------------
@@ -1310,6 +1465,31 @@ hipError_t launch_check_data(const uint32_t *calc, const uint8_t *expected, size
     if (e != hipSuccess || n == 0) return e;
     hipLaunchKernelGGL(check_data_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, calc, expected,
                        exp_stride, lengths, len_stride, (uint32_t)n, mask, nbad);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t *first, size_t nfrags, uint32_t *out,
+                        int mode, const uint32_t *img, uint32_t *vals, uint32_t *phase, hipStream_t s) {
+    if (nfrags == 0) return hipSuccess;
+    constexpr uint32_t kSmall = 256;  // pieces up to this many bytes: one thread each
+    const bool sum = mode != LAMPI_CSUM_CRC32;
+    if (npieces) {
+        if (sum)
+            hipLaunchKernelGGL(chain_phase_kernel, dim3((unsigned)((nfrags + 255) / 256)), dim3(256), 0, s, d, first,
+                               (uint32_t)nfrags, phase);
+        const uint32_t fpw = pick_fpw(npieces, 1);
+        const PieceSource src{d, sum ? phase : nullptr, kSmall};
+        if (sum)
+            hipLaunchKernelGGL(sum_rows_kernel<PieceSource>, grid_for(npieces, fpw), dim3(kBlock), 0, s, src, npieces,
+                               fpw, vals);
+        else
+            hipLaunchKernelGGL(crc_rows_kernel<PieceSource>, grid_for(npieces, fpw), dim3(kBlock), 0, s, src, npieces,
+                               fpw, img, vals);
+        hipLaunchKernelGGL(chain_small_kernel, dim3((unsigned)((npieces + 255) / 256)), dim3(256), 0, s, d,
+                           (uint32_t)npieces, phase, kSmall, mode, img, vals);
+    }
+    hipLaunchKernelGGL(chain_fold_kernel, dim3((unsigned)((nfrags + kWaves - 1) / kWaves)), dim3(kBlock), 0, s, d, first,
+                       (uint32_t)nfrags, vals, mode, img, out);
     return hipGetLastError();
 }
 

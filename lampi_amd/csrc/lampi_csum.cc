@@ -339,6 +339,33 @@ int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_
                                    d_out, mode, img, (hipStream_t)stream));
 }
 
+int lampi_chain_csum_batch(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first, size_t nfrags,
+                           uint32_t *d_out, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (nfrags == 0) return 0;
+    if (!d_first || !d_out || (npieces && !d_pieces) || npieces > 0xFFFFFFFFull || nfrags > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t *scratch = nullptr;
+    if (npieces) {
+        e = hipMallocAsync((void **)&scratch, 2 * npieces * sizeof(uint32_t), s);
+        if (e != hipSuccess) return to_int(e);
+    }
+    e = launch_chain(d_pieces, npieces, d_first, nfrags, d_out, mode, img, scratch, scratch ? scratch + npieces : nullptr,
+                     s);
+    if (scratch) {
+        const hipError_t f = hipFreeAsync(scratch, s);
+        if (e == hipSuccess) e = f;
+    }
+    return to_int(e);
+}
+
 int lampi_header_csum_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
                             uint32_t *d_out, int mode, void *stream) {
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);

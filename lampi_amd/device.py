@@ -12,7 +12,7 @@ import torch
 from ._lib import CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
 
 __all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
-           "make_descs", "make_copy_descs", "as_u32", "header_csum_batch", "header_check_batch", "check_data_batch",
+           "make_descs", "make_copy_descs", "as_u32", "chain_csum_batch", "header_csum_batch", "header_check_batch", "check_data_batch",
            "mask_bits"]
 
 
@@ -151,6 +151,28 @@ def msg_bcopy(msg: torch.Tensor, frag_len: int, dst: torch.Tensor, dst_stride: i
         raise ValueError("out is too small")
     check(lib().lampi_msg_bcopy(msg.data_ptr(), nbytes, frag_len, dst.data_ptr(), stride, partial & 0xFFFFFFFF,
                                 out.data_ptr(), mode, _stream_handle(stream)), "lampi_msg_bcopy")
+    return out
+
+
+def chain_csum_batch(pieces: torch.Tensor, first, mode: int = CRC32, out: torch.Tensor | None = None,
+                     stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Chained checksum per fragment over its typemap pieces (``lampi_copy_desc`` rows of
+    ``pieces``; fragment f = pieces first[f] .. first[f+1]-1)."""
+    _require_cuda(pieces, "pieces")
+    npieces = pieces.numel() * pieces.element_size() // 32
+    fa = np.asarray(first, dtype=np.uint32) if not isinstance(first, torch.Tensor) else None
+    if fa is not None:
+        if fa.size < 1 or (fa.size > 1 and (np.any(np.diff(fa.astype(np.int64)) < 0) or int(fa[-1]) > npieces)):
+            raise ValueError("first must be nondecreasing and end at most at the piece count")
+        first_t = torch.from_numpy(fa.view(np.int32)).to(pieces.device)
+    else:
+        _require_cuda(first, "first")
+        first_t = first
+    nfrags = first_t.numel() - 1
+    if out is None:
+        out = torch.empty(max(nfrags, 0), dtype=torch.int32, device=pieces.device)
+    check(lib().lampi_chain_csum_batch(pieces.data_ptr(), npieces, first_t.data_ptr(), nfrags, out.data_ptr(), mode,
+                                       _stream_handle(stream)), "lampi_chain_csum_batch")
     return out
 
 
