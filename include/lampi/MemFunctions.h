@@ -55,6 +55,24 @@ inline unsigned int bcopy_uicsum(const void *source, void *destination, unsigned
     unsigned int pint = 0, plen = 0;
     return lampi_bcopy_uicsum(source, destination, copylen, csumlen, &pint, &plen);
 }
+// 64-bit additive checksums (MemFunctions.h:43-50; no path caller in the reference)
+inline unsigned long csum(const void *source, unsigned long csumlen, unsigned long *lastPartialLong,
+                          unsigned long *lastPartialLength) {
+    return lampi_csum(source, csumlen, lastPartialLong, lastPartialLength);
+}
+inline unsigned long csum(const void *source, unsigned long csumlen) {
+    unsigned long plong = 0, plen = 0;
+    return lampi_csum(source, csumlen, &plong, &plen);
+}
+inline unsigned long bcopy_csum(const void *source, void *destination, unsigned long copylen, unsigned long csumlen,
+                                unsigned long *lastPartialLong, unsigned long *lastPartialLength) {
+    return lampi_bcopy_csum(source, destination, copylen, csumlen, lastPartialLong, lastPartialLength);
+}
+inline unsigned long bcopy_csum(const void *source, void *destination, unsigned long copylen,
+                                unsigned long csumlen) {
+    unsigned long plong = 0, plen = 0;
+    return lampi_bcopy_csum(source, destination, copylen, csumlen, &plong, &plen);
+}
 
 #endif /* __cplusplus */
 #endif /* LAMPI_DROPIN_MEMFUNCTIONS_H */

@@ -74,6 +74,19 @@ unsigned int lampi_uicsum(const void *src, unsigned long csumlen, unsigned int *
 unsigned int lampi_bcopy_uicsum(const void *src, void *dst, unsigned long copylen,
                                 unsigned long csumlen, unsigned int *pint, unsigned int *plen);
 
+/* replaces unsigned long csum(const void*, unsigned long, unsigned long*, unsigned long*)
+ *   ref src/util/MemFunctions.cc:913-1071 (_Z4csumPKvmPmS1_): sum mod 2^64 of little-endian
+ *   64-bit words with the trailing partial word zero-padded; (*plong, *plen) chain it like
+ *   uicsum's state (*plen in 0..7; 8 or more is treated as 0).  No path caller in the reference. */
+unsigned long lampi_csum(const void *src, unsigned long csumlen, unsigned long *plong, unsigned long *plen);
+
+/* replaces unsigned long bcopy_csum(const void*, void*, unsigned long, unsigned long,
+ *                                   unsigned long*, unsigned long*)
+ *   ref src/util/MemFunctions.cc:142-516 (_Z10bcopy_csumPKvPvmmPmS2_).
+ *   Copies copylen bytes; the sum covers max(copylen, csumlen) bytes of src. */
+unsigned long lampi_bcopy_csum(const void *src, void *dst, unsigned long copylen, unsigned long csumlen,
+                               unsigned long *plong, unsigned long *plen);
+
 /* ------------------------------------------------------------------------------------
  * Device-resident batched entry points.
  * ---------------------------------------------------------------------------------- */
@@ -94,6 +107,9 @@ typedef struct lampi_frag_desc {
  * checksum-only send (src/path/quadrics/sendFrag.h:861-872). */
 int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out,
                           int mode, void *stream);
+
+/* out[i] = csum (64-bit words, fresh state) of fragment d[i]; d[i].partial is ignored. */
+int lampi_frag_csum64_batch(const lampi_frag_desc *d_descs, size_t n, uint64_t *d_out, void *stream);
 
 /* One fused copy + checksum (32 bytes, little-endian): offset 0 src, 8 dst, 16 copylen,
  * 20 csumlen, 24 partial, 28 reserved. */

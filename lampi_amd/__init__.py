@@ -11,7 +11,7 @@ kernels for gfx950 behind the C ABI in include/lampi_csum.h (liblampi_csum.so).
   (imported lazily: it needs torch).
 """
 from ._lib import CRC32, CRC_INITIAL_REGISTER, CRC_POLYNOMIAL, SUM32, FragDesc, lib  # noqa: F401
-from .memfunctions import (PartialState, bcopy_uicrc, bcopy_uicsum, header_checksum, uicrc,  # noqa: F401
-                           uicsum)
+from .memfunctions import (PartialState, PartialState64, bcopy_csum, bcopy_uicrc, bcopy_uicsum,  # noqa: F401
+                           csum, header_checksum, uicrc, uicsum)
 
 __version__ = "0.1.0"

@@ -46,6 +46,7 @@ c_uint = ctypes.c_uint
 c_void_p = ctypes.c_void_p
 c_size_t = ctypes.c_size_t
 PUINT = ctypes.POINTER(ctypes.c_uint)
+PULONG = ctypes.POINTER(ctypes.c_ulong)
 
 # name -> (restype, argtypes); the full exported C ABI.
 PROTOTYPES = {
@@ -53,6 +54,9 @@ PROTOTYPES = {
     "lampi_bcopy_uicrc": (c_uint, [c_void_p, c_void_p, c_ulong, c_ulong, c_uint]),
     "lampi_uicsum": (c_uint, [c_void_p, c_ulong, PUINT, PUINT]),
     "lampi_bcopy_uicsum": (c_uint, [c_void_p, c_void_p, c_ulong, c_ulong, PUINT, PUINT]),
+    "lampi_csum": (c_ulong, [c_void_p, c_ulong, PULONG, PULONG]),
+    "lampi_bcopy_csum": (c_ulong, [c_void_p, c_void_p, c_ulong, c_ulong, PULONG, PULONG]),
+    "lampi_frag_csum64_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_void_p]),
     "lampi_frag_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_frag_bcopy_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_msg_bcopy": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, ctypes.c_uint32, c_void_p,

@@ -93,6 +93,17 @@ struct CopySource {
     }
 };
 
+// host-path pieces of one chained 64-bit csum: partial = the piece's byte phase (0..7)
+struct PhaseDescSource {
+    static constexpr bool kCopy = false;
+    static constexpr bool kPhase = true;
+    const lampi_frag_desc *d;
+    __device__ FragInfo get(size_t f) const {
+        const lampi_frag_desc x = d[f];
+        return {(gbyte *)(uintptr_t)x.addr, x.length, x.partial, nullptr, 0u};
+    }
+};
+
 struct MsgSource {
     static constexpr bool kCopy = false;
     static constexpr bool kPhase = false;
@@ -873,8 +884,10 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
 }
 
 // ---- SUM -------------------------------------------------------------------------------
-template <class Src>
-__global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uint32_t fpw, uint32_t *__restrict__ out) {
+// Acc = uint32_t: uicsum (32-bit words); Acc = uint64_t: csum (64-bit words, ref
+// MemFunctions.cc:142-516, 913-1071).  Phase (kPhase sources) is taken mod the word size.
+template <class Src, class Acc = uint32_t>
+__global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uint32_t fpw, Acc *__restrict__ out) {
     const int lane = threadIdx.x & 63;
     const size_t f0 = wg_first(fpw);
     const size_t fend = f0 + (size_t)kWaves * fpw;
@@ -888,14 +901,15 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
         }
         // byte phase of the first byte in the word grid (chained pieces); the frame starts
         // `ph` bytes early and those bytes read as zero
-        const uint32_t ph = Src::kPhase ? (uniform(fi.partial) & 3u) : 0u;
+        const uint32_t ph = Src::kPhase ? (uniform(fi.partial) & (uint32_t)(sizeof(Acc) - 1)) : 0u;
         gbyte *fb = fi.addr - ph;
         const uint32_t span = fi.len + ph;
         const uint32_t R = (span + (kRowBytes - 1)) / kRowBytes;
         const uint32_t s16 = (uint32_t)((uintptr_t)fb & 15u);
         uint8_t *db = fi.dst - ph;
         const uint32_t dm = (uint32_t)((uintptr_t)db & 15u);
-        uint32_t acc = 0, carry = 0;
+        Acc acc = 0;
+        uint32_t carry = 0;
         for (uint32_t r = 0; r < R; ++r) {
             const long long o = (long long)r * kRowBytes + lane * kLaneBytes;
             const bool mask = (r == 0 && ph != 0) || (r + 1 == R && span % kRowBytes != 0) || s16 != 0;
@@ -908,10 +922,20 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
                     carry = __builtin_amdgcn_readlane(d[15], 63);
                 }
             }
+            if constexpr (sizeof(Acc) == 4) {
 #pragma unroll
-            for (int w = 0; w < 16; ++w) acc += d[w];
+                for (int w = 0; w < 16; ++w) acc += d[w];
+            } else {  // 64-bit words: the frame is 8-byte aligned to the fragment's word grid
+#pragma unroll
+                for (int w = 0; w < 16; w += 2) acc += (uint64_t)d[w] | ((uint64_t)d[w + 1] << 32);
+            }
         }
-        acc = wave_add(acc);
+        if constexpr (sizeof(Acc) == 4) {
+            acc = wave_add(acc);
+        } else {
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+        }
         if (lane == 0) out[f] = acc;
     }
 }
@@ -1180,6 +1204,34 @@ __global__ void __launch_bounds__(256) chain_fold_kernel(const lampi_copy_desc *
     }
 }
 
+// ---- 64-bit csum over a chained stream -----------------------------------------------------
+// Host path of csum / bcopy_csum: the pieces' phase-shifted sums add up to the increment; the
+// new (lastPartialLong, lastPartialLength) is the trailing partial word of the virtual stream
+// [old partial bytes | the len new bytes].  out3 = {sum, plong, plen}.
+__global__ void sum64_finish_kernel(const uint64_t *__restrict__ vals, uint32_t nv, const uint8_t *__restrict__ src,
+                                    uint64_t len, uint64_t plong, uint64_t plen, uint64_t *__restrict__ out3) {
+    uint64_t acc = 0;
+    for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) acc += vals[i];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+    __shared__ uint64_t part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    uint64_t total = 0;
+    for (uint32_t w = 0; w < (blockDim.x + 63) / 64; ++w) total += part[w];
+    const uint64_t end = plen + len;  // virtual stream length
+    const uint64_t nl = end & 7u;
+    uint64_t np = 0;
+    for (uint64_t b = end - nl; b < end; ++b) {
+        const uint64_t byte = b < plen ? (plong >> (8 * b)) & 0xFFu : src[b - plen];
+        np |= byte << (8 * (b & 7u));
+    }
+    out3[0] = total;
+    out3[1] = np;
+    out3[2] = nl;
+}
+
 // ---- synthetic stream fill ----------------------------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z ^= z >> 30;
@@ -1390,6 +1442,24 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
     else
         hipLaunchKernelGGL(sum_rows_kernel<CopySource>, grid_for(n, fpw), dim3(kBlock), 0, s, CopySource{d}, n, fpw,
                            out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum64_desc(const lampi_frag_desc *d, size_t n, uint64_t *out, bool phased, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t fpw = pick_fpw(n, 1);
+    if (phased)
+        hipLaunchKernelGGL((sum_rows_kernel<PhaseDescSource, uint64_t>), grid_for(n, fpw), dim3(kBlock), 0, s,
+                           PhaseDescSource{d}, n, fpw, out);
+    else
+        hipLaunchKernelGGL((sum_rows_kernel<DescSource, uint64_t>), grid_for(n, fpw), dim3(kBlock), 0, s, DescSource{d},
+                           n, fpw, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t *src, uint64_t len, uint64_t plong,
+                               uint64_t plen, uint64_t *out3, hipStream_t s) {
+    hipLaunchKernelGGL(sum64_finish_kernel, dim3(1), dim3(256), 0, s, vals, nv, src, len, plong, plen, out3);
     return hipGetLastError();
 }
 

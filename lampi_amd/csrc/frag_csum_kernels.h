@@ -38,6 +38,10 @@ hipError_t launch_check_data(const uint32_t *calc, const uint8_t *expected, size
 // Chained checksums over typemap pieces; vals / phase: npieces words of scratch each.
 hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t *first, size_t nfrags, uint32_t *out,
                         int mode, const uint32_t *img, uint32_t *vals, uint32_t *phase, hipStream_t s);
+// 64-bit csum: per-descriptor sums (phased: desc.partial = byte phase 0..7) and the chained finish.
+hipError_t launch_sum64_desc(const lampi_frag_desc *d, size_t n, uint64_t *out, bool phased, hipStream_t s);
+hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t *src, uint64_t len, uint64_t plong,
+                               uint64_t plen, uint64_t *out3, hipStream_t s);
 hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, int grid, hipStream_t s);
 hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out, int grid,
                           hipStream_t s);

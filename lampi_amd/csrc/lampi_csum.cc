@@ -83,6 +83,8 @@ struct HostCtx {
     size_t vcap = 0;
     lampi_frag_desc *ddesc = nullptr;
     size_t desccap = 0;
+    uint64_t *dvals64 = nullptr;  // 64-bit csum: per-piece sums + 3 result words
+    size_t v64cap = 0;
     std::vector<lampi_frag_desc> hdesc;
     std::map<uint64_t, uint32_t *> combine_tabs;  // piece size -> device nibble tables
 };
@@ -204,6 +206,41 @@ uint32_t device_sum(HostCtx &c, uint64_t len, unsigned int *pint, unsigned int *
     return h[0];
 }
 
+// csum (64-bit words) of c.dbuf[0..len) with chaining state, computed on the GPU: every piece
+// is summed at its byte phase in the caller's word grid, the finish kernel adds them up and
+// forms the new trailing partial word.
+uint64_t device_sum64(HostCtx &c, uint64_t len, unsigned long *plong, unsigned long *plen) {
+    const uint64_t k = *plen >= 8 ? 0u : *plen;
+    const uint64_t B = piece_size(len);
+    const uint32_t n = (uint32_t)((len + B - 1) / B);
+    c.hdesc.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        c.hdesc[i].addr = (uint64_t)(uintptr_t)(c.dbuf + (uint64_t)i * B);
+        c.hdesc[i].length = (uint32_t)std::min<uint64_t>(B, len - (uint64_t)i * B);
+        c.hdesc[i].partial = (uint32_t)((k + (uint64_t)i * B) & 7u);
+    }
+    ensure(c.ddesc, c.desccap, std::max<uint32_t>(n, 1));
+    ensure(c.dvals64, c.v64cap, (size_t)n + 3);
+    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc.data(), n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice, c.stream));
+    LAMPI_CHECK(launch_sum64_desc(c.ddesc, n, c.dvals64, true, c.stream));
+    uint64_t *out3 = c.dvals64 + n;
+    LAMPI_CHECK(launch_sum64_finish(c.dvals64, n, c.dbuf, len, k ? (uint64_t)*plong : 0u, k, out3, c.stream));
+    uint64_t h[3];
+    LAMPI_CHECK(hipMemcpyAsync(h, out3, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    *plong = (unsigned long)h[1];
+    *plen = (unsigned long)h[2];
+    return h[0];
+}
+
+unsigned long empty_sum64(unsigned long *plong, unsigned long *plen) {
+    if (*plen == 0 || *plen >= 8) {
+        *plong = 0;
+        *plen = 0;
+    }
+    return 0;
+}
+
 void stage_in(HostCtx &c, const void *src, uint64_t len) {
     ensure(c.dbuf, c.dcap, (size_t)len);
     LAMPI_CHECK(hipMemcpyAsync(c.dbuf, src, len, hipMemcpyHostToDevice, c.stream));
@@ -266,6 +303,33 @@ unsigned int lampi_bcopy_uicsum(const void *src, void *dst, unsigned long copyle
     const uint32_t r = device_sum(c, n, pint, plen);
     stage_out(c, dst, copylen);
     return r;
+}
+
+unsigned long lampi_csum(const void *src, unsigned long csumlen, unsigned long *plong, unsigned long *plen) {
+    if (csumlen == 0) return empty_sum64(plong, plen);
+    HostCtx &c = host_ctx();
+    stage_in(c, src, csumlen);
+    return device_sum64(c, csumlen, plong, plen);
+}
+
+unsigned long lampi_bcopy_csum(const void *src, void *dst, unsigned long copylen, unsigned long csumlen,
+                               unsigned long *plong, unsigned long *plen) {
+    const uint64_t n = std::max<uint64_t>(copylen, csumlen);
+    if (n == 0) return empty_sum64(plong, plen);
+    HostCtx &c = host_ctx();
+    stage_in(c, src, n);
+    const uint64_t r = device_sum64(c, n, plong, plen);
+    stage_out(c, dst, copylen);
+    return r;
+}
+
+int lampi_frag_csum64_batch(const lampi_frag_desc *d_descs, size_t n, uint64_t *d_out, void *stream) {
+    if (n == 0) return 0;
+    if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_sum64_desc(d_descs, n, d_out, false, (hipStream_t)stream));
 }
 
 int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {

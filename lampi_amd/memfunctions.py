@@ -10,6 +10,8 @@ this module                reference                                           C
 ``bcopy_uicrc``            ``bcopy_uicrc`` MemFunctions.cc:1263-1329           ``lampi_bcopy_uicrc``
 ``uicsum``                 ``uicsum`` MemFunctions.cc:1073-1231                ``lampi_uicsum``
 ``bcopy_uicsum``           ``bcopy_uicsum`` MemFunctions.cc:518-893            ``lampi_bcopy_uicsum``
+``csum``                   ``csum`` MemFunctions.cc:913-1071 (64-bit words)    ``lampi_csum``
+``bcopy_csum``             ``bcopy_csum`` MemFunctions.cc:142-516              ``lampi_bcopy_csum``
 ``header_checksum``        ``BasePath_t::headerChecksum`` path/common/path.h:280-314
 =========================  ==================================================  =====================
 
@@ -27,8 +29,8 @@ import numpy as np
 from ._lib import CRC_INITIAL_REGISTER, lib
 
 __all__ = [
-    "CRC_INITIAL_REGISTER", "PartialState", "uicrc", "bcopy_uicrc", "uicsum", "bcopy_uicsum",
-    "header_checksum",
+    "CRC_INITIAL_REGISTER", "PartialState", "PartialState64", "uicrc", "bcopy_uicrc", "uicsum", "bcopy_uicsum",
+    "csum", "bcopy_csum", "header_checksum",
 ]
 
 
@@ -41,6 +43,14 @@ class PartialState:
     """
 
     pint: int = 0
+    plen: int = 0
+
+
+@dataclass
+class PartialState64:
+    """(lastPartialLong, lastPartialLength) of the 64-bit ``csum`` chaining (plen in 0..7)."""
+
+    plong: int = 0
     plen: int = 0
 
 
@@ -111,6 +121,34 @@ def bcopy_uicsum(source, destination, copylen: int, csumlen: int, state: Partial
     st, pi, pl = _state_args(state)
     r = int(lib().lampi_bcopy_uicsum(ps, pd, copylen, csumlen, ctypes.byref(pi), ctypes.byref(pl)))
     st.pint, st.plen = pi.value, pl.value
+    return r
+
+
+def _state64_args(state: PartialState64 | None):
+    st = state if state is not None else PartialState64()
+    return st, ctypes.c_ulong(st.plong & (2**64 - 1)), ctypes.c_ulong(st.plen & (2**64 - 1))
+
+
+def csum(source, csumlen: int | None = None, state: PartialState64 | None = None) -> int:
+    """64-bit additive checksum increment of ``csumlen`` bytes; ``state`` chains calls (``+=`` mod 2^64)."""
+    p, arr = _ro_ptr(source)
+    n = arr.size if csumlen is None else int(csumlen)
+    _check_len(arr, n, "csumlen")
+    st, pl, pn = _state64_args(state)
+    r = int(lib().lampi_csum(p, n, ctypes.byref(pl), ctypes.byref(pn)))
+    st.plong, st.plen = pl.value, pn.value
+    return r
+
+
+def bcopy_csum(source, destination, copylen: int, csumlen: int, state: PartialState64 | None = None) -> int:
+    """Copy ``copylen`` bytes; 64-bit additive checksum of ``max(copylen, csumlen)`` bytes."""
+    ps, a = _ro_ptr(source)
+    pd, b = _rw_ptr(destination)
+    _check_len(a, max(copylen, csumlen), "csumlen")
+    _check_len(b, copylen, "copylen")
+    st, pl, pn = _state64_args(state)
+    r = int(lib().lampi_bcopy_csum(ps, pd, copylen, csumlen, ctypes.byref(pl), ctypes.byref(pn)))
+    st.plong, st.plen = pl.value, pn.value
     return r
 
 

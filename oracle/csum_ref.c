@@ -131,6 +131,55 @@ uint32_t oracle_bcopy_uicsum(const void *src, void *dst, size_t copylen, size_t 
     return oracle_uicsum(src, copylen > csumlen ? copylen : csumlen, pint, plen);
 }
 
+/* csum (ref MemFunctions.cc:913-1071): the same chaining with 64-bit little-endian words
+ * (unsigned long on LP64), sum mod 2^64; lastPartialLength in 0..7 (8+ treated as 0). */
+uint64_t oracle_csum64(const void *src, size_t len, uint64_t *plong, uint64_t *plen)
+{
+    const uint8_t *p = (const uint8_t *)src;
+    uint64_t sum = 0;
+    uint64_t k = *plen;
+    if (k >= 8) k = 0;
+    if (k) {
+        uint64_t old = *plong, w = old;
+        size_t take = 8 - (size_t)k;
+        if (take > len) take = len;
+        for (size_t j = 0; j < take; ++j) {
+            unsigned sh = 8u * (unsigned)(k + j);
+            w = (w & ~(0xFFull << sh)) | ((uint64_t)p[j] << sh);
+        }
+        sum += w - old;
+        p += take;
+        len -= take;
+        if (k + take < 8) {
+            *plong = w;
+            *plen = k + take;
+            return sum;
+        }
+    }
+    size_t nw = len / 8;
+    for (size_t i = 0; i < nw; ++i) {
+        uint64_t w = 0;
+        for (int j = 0; j < 8; ++j) w |= (uint64_t)p[8 * i + (size_t)j] << (8 * j);
+        sum += w;
+    }
+    p += 8 * nw;
+    size_t r = len & 7u;
+    uint64_t tail = 0;
+    for (size_t j = 0; j < r; ++j) tail |= (uint64_t)p[j] << (8 * j);
+    sum += tail;
+    *plong = tail;
+    *plen = r;
+    return sum;
+}
+
+/* bcopy_csum (ref MemFunctions.cc:142-516): copy copylen bytes, csum max(copylen, csumlen). */
+uint64_t oracle_bcopy_csum64(const void *src, void *dst, size_t copylen, size_t csumlen, uint64_t *plong,
+                             uint64_t *plen)
+{
+    if (copylen) memcpy(dst, src, copylen);
+    return oracle_csum64(src, copylen > csumlen ? copylen : csumlen, plong, plen);
+}
+
 uint32_t oracle_header_checksum(const void *header, size_t crclen, int word_count, int usecrc)
 {
     if (usecrc) {

@@ -46,6 +46,9 @@ uint32_t oracle_uicsum(const void *src, size_t len, uint32_t *pint, uint32_t *pl
 
 /* bcopy_uicsum: copy copylen bytes, sum max(copylen, csumlen) bytes of src
  * (ref: MemFunctions.cc:518-875; wrapper :882-893). */
+uint64_t oracle_csum64(const void *src, size_t len, uint64_t *plong, uint64_t *plen);
+uint64_t oracle_bcopy_csum64(const void *src, void *dst, size_t copylen, size_t csumlen, uint64_t *plong,
+                             uint64_t *plen);
 uint32_t oracle_bcopy_uicsum(const void *src, void *dst, size_t copylen, size_t csumlen,
                              uint32_t *pint, uint32_t *plen);
 

@@ -29,6 +29,7 @@ _u = ctypes.c_uint
 _ul = ctypes.c_ulong
 _vp = ctypes.c_void_p
 _pu = ctypes.POINTER(ctypes.c_uint)
+_pul = ctypes.POINTER(ctypes.c_ulong)
 
 
 def _buf(b):
@@ -62,6 +63,20 @@ class _Api:
         r = self._bcopy_uicsum(ps, pd, copylen, csumlen, ctypes.byref(pi), ctypes.byref(pl))
         return int(r), pi.value, pl.value
 
+    def csum(self, data, n=None, plong=0, plen=0):
+        """64-bit csum: returns (sum_increment, plong', plen')."""
+        p, a = _buf(data)
+        pi, pl = _ul(plong), _ul(plen)
+        r = self._csum(p, a.size if n is None else n, ctypes.byref(pi), ctypes.byref(pl))
+        return int(r), pi.value, pl.value
+
+    def bcopy_csum(self, src, dst, copylen, csumlen, plong=0, plen=0):
+        ps, _ = _buf(src)
+        pd, _ = _buf(dst)
+        pi, pl = _ul(plong), _ul(plen)
+        r = self._bcopy_csum(ps, pd, copylen, csumlen, ctypes.byref(pi), ctypes.byref(pl))
+        return int(r), pi.value, pl.value
+
 
 class Restatement(_Api):
     def __init__(self, path: str = RESTATEMENT_SO):
@@ -79,6 +94,11 @@ class Restatement(_Api):
         self._bcopy_uicsum = L.oracle_bcopy_uicsum
         self._bcopy_uicsum.restype = _u
         self._bcopy_uicsum.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _pu, _pu]
+        self._csum = L.oracle_csum64
+        self._csum.restype, self._csum.argtypes = ctypes.c_uint64, [_vp, ctypes.c_size_t, _pul, _pul]
+        self._bcopy_csum = L.oracle_bcopy_csum64
+        self._bcopy_csum.restype = ctypes.c_uint64
+        self._bcopy_csum.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, _pul, _pul]
         L.oracle_fill_stream.argtypes = [_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t]
         L.oracle_uniform_batch.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_size_t,
                                            ctypes.c_int, ctypes.c_int, _vp]
@@ -168,6 +188,10 @@ class Reference(_Api):
         self._uicsum.restype, self._uicsum.argtypes = _u, [_vp, _ul, _pu, _pu]
         self._bcopy_uicsum = getattr(L, "_Z12bcopy_uicsumPKvPvmmPjS2_")
         self._bcopy_uicsum.restype, self._bcopy_uicsum.argtypes = _u, [_vp, _vp, _ul, _ul, _pu, _pu]
+        self._csum = getattr(L, "_Z4csumPKvmPmS1_")
+        self._csum.restype, self._csum.argtypes = _ul, [_vp, _ul, _pul, _pul]
+        self._bcopy_csum = getattr(L, "_Z10bcopy_csumPKvPvmmPmS2_")
+        self._bcopy_csum.restype, self._bcopy_csum.argtypes = _ul, [_vp, _vp, _ul, _ul, _pul, _pul]
 
 
 def splitmix_stream(seed: int, byte_off: int, n: int) -> np.ndarray:

@@ -111,7 +111,11 @@ unsigned int send_typemap(const void *s, void *d, unsigned long n) {
     return csum + uicsum(s, n) + uicsum(s, n, &ui1, &ui2) + uicrc(s, n) + uicrc(s, n, csum) +
            bcopy_uicsum(s, d, n, n);
 }
-int main(int argc, char **) { return argc > 5 ? (int)send_contig(0, 0, 0) : 0; }
+unsigned long sum64(const void *s, void *d, unsigned long n) {  // MemFunctions.h:43-50 overloads
+    unsigned long pl = 0, pn = 0;
+    return csum(s, n) + csum(s, n, &pl, &pn) + bcopy_csum(s, d, n, n) + bcopy_csum(s, d, n, n, &pl, &pn);
+}
+int main(int argc, char **) { return argc > 5 ? (int)(send_contig(0, 0, 0) + sum64(0, 0, 0)) : 0; }
 ''')
     c_src = tmp_path / "caller.c"
     c_src.write_text(r'''

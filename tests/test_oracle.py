@@ -168,3 +168,32 @@ def test_cpu_baseline_speed_matches_reference(oracle, reference):
     tp = min(oracle.time_crc_fn(oracle.uicrc_addr(), buf, 16384, 1024, 1)[0] for _ in range(3))
     tr = min(oracle.time_crc_fn(reference.uicrc_addr(), buf, 16384, 1024, 1)[0] for _ in range(3))
     assert 0.8 < tp / tr < 1.25, (tp, tr)
+
+
+def test_csum64_fixtures(oracle):
+    """64-bit csum / bcopy_csum restatement vs the reference's own results (tests/golden/csum64.json)."""
+    from oracle.oracle import splitmix_stream
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "csum64.json")) as f:
+        g = json.load(f)
+    for c in g["single"]:
+        got = oracle.csum(splitmix_stream(c["seed"], c["off"], c["len"]), c["len"], c["plong"], c["plen"])
+        assert got == (c["sum"], c["plong_out"], c["plen_out"])
+    for c in g["chain"]:
+        buf = splitmix_stream(c["seed"], c["off"], c["len"])
+        bounds = [0] + c["cuts"] + [c["len"]]
+        tot, pl, pn = 0, 0, 0
+        for a, b in zip(bounds, bounds[1:]):
+            s, pl, pn = oracle.csum(buf[a:], b - a, pl, pn)
+            tot = (tot + s) % 2**64
+        assert tot == c["sum"] == c["sum_whole"]
+    for c in g["bcopy"]:
+        total = max(c["copylen"], c["clen"])
+        src = np.zeros(total + 16, np.uint8)
+        src[c["src_align"]:c["src_align"] + total] = splitmix_stream(c["seed"], c["off"], total)
+        dst = np.zeros(total + 16, np.uint8)
+        got = oracle.bcopy_csum(src[c["src_align"]:], dst[c["dst_align"]:], c["copylen"], c["clen"], c["plong"],
+                                c["plen"])
+        assert got == (c["sum"], c["plong_out"], c["plen_out"])
+        assert np.array_equal(dst[c["dst_align"]:c["dst_align"] + c["copylen"]],
+                              src[c["src_align"]:c["src_align"] + c["copylen"]])

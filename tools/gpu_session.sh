@@ -42,6 +42,7 @@ for step in "$@"; do
            run bcopysum 600 python bench.py --bcopy --mode sum --steps 10 ;;
     tests_bcopy) run pytest_bcopy 600 python -m pytest tests/test_gpu_bcopy.py -m gpu -x -q ;;
     tests_chain) run pytest_chain 600 python -m pytest tests/test_gpu_chain.py -m gpu -x -q ;;
+    tests_csum64) run pytest_csum64 600 python -m pytest tests/test_gpu_csum64.py -m gpu -x -q ;;
     tests_verify) run pytest_verify 600 python -m pytest tests/test_gpu_verify.py -m gpu -x -q ;;
     ablation) run ablation 500 tools/microbench/crc_ablation ;;
     microbench) run microbench 300 tools/microbench/readbw ;;
