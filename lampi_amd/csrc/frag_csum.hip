@@ -36,6 +36,8 @@
 // 64-byte pieces, funnel-shifted to the fragment's own word grid, zero-padded tail,
 // 32-bit adds reduced across the wave.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <cstdint>
 
 #include "crc_tables.h"
@@ -639,14 +641,19 @@ struct RowsK {
 
 template <int N, int K>
 __device__ __forceinline__ void wait_rows(RowsK<K> &b) {
-    if constexpr (K == 2) {
+    if constexpr (K == 1) {
+        asm volatile("s_waitcnt vmcnt(%4)"
+                     : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3])
+                     : "n"(N)
+                     : "memory");
+    } else if constexpr (K == 2) {
         asm volatile("s_waitcnt vmcnt(%8)"
                      : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
                        "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3])
                      : "n"(N)
                      : "memory");
     } else {
-        static_assert(K == 4, "kChains is 2 or 4");
+        static_assert(K == 4, "kChains is 1, 2 or 4");
         asm volatile("s_waitcnt vmcnt(%16)"
                      : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
                        "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3]),
@@ -728,7 +735,7 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // them (first pass: 8K / 12K / 16K younger operations, then 16K).  Rows move in the coalesced
 // layout (crc_chunks): lane-contiguous 64-byte stores run at 51% of the HBM roofline on
 // MI355X against 71% for 1 KiB-per-instruction stores (profiles/r01_copy_patterns.txt).
-template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy>
+template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3>
 __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
                                                              uint32_t fpw, size_t frag_len, uint32_t partial,
                                                              const uint32_t *__restrict__ img,
@@ -765,20 +772,22 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
         for (int c = 0; c < K; ++c) issue_row<kS>(row_ptr(frag(t.i, c), t.r), b.x[c]);
     };
 
-    GroupTask ta{0u, 0u};
-    GroupTask tb = advance(ta);
-    GroupTask tc = advance(tb);
-    RowsK<K> A, B, Cb;
+    constexpr int D = kDepth;  // ring slots: D - 1 steps in flight while one is checksummed
+    static_assert(D >= 2 && D <= 6, "ring depth");
+    GroupTask t[D];
+    RowsK<K> ring[D];
+    t[0] = GroupTask{0u, 0u};
+#pragma unroll
+    for (int q = 1; q < D; ++q) t[q] = advance(t[q - 1]);
     auto issue_all = [&] {
-        issue(ta, A);
-        issue(tb, B);
-        issue(tc, Cb);
+#pragma unroll
+        for (int q = 0; q < D; ++q) issue(t[q], ring[q]);
     };
     constexpr size_t kComb = kCoal ? kImgCombine16Cols : kImgCombineCols;
     constexpr size_t kHorn = kCoal ? kImgHorner16Cols : kImgHornerCols;
     if (kAblate != 2) {
-        // all three ring slots are in flight while the workgroup builds its tables
-        stage_tables<12 * K, decltype(issue_all), 7, kComb, kHorn>(lds, img, issue_all);
+        // every ring slot is in flight while the workgroup builds its tables
+        stage_tables<4 * K * D, decltype(issue_all), 7, kComb, kHorn>(lds, img, issue_all);
     } else {
         stage_tables<0>(lds, img, [] {});
     }
@@ -840,46 +849,49 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
         }
     };
     if (kAblate == 2) {  // same lookups on register data, no HBM traffic
+        RowsK<K> &A = ring[0];
 #pragma unroll
         for (int c = 0; c < K; ++c)
             for (int w = 0; w < 4; ++w) A.x[c].q[w] = u32x4{lane_off + w + 7u * c, lane_off ^ 0x5A5Au, 7u * w, f0 + c};
-        for (GroupTask t = ta;; t = advance(t)) {
-            process(A, t);
+        for (GroupTask u = t[0];; u = advance(u)) {
+            process(A, u);
 #pragma unroll
             for (int c = 0; c < K; ++c) A.x[c].q[0].x ^= C[c];
-            if (is_last(t)) break;
+            if (is_last(u)) break;
         }
         return;
     }
-    // steady state: while one slot is checksummed the other two are in flight
+    // steady state: slot S is waited for, checksummed (and stored) and refilled with the task
+    // after the most recently issued one.  vmcnt counts loads and stores in issue order: the
+    // operations younger than slot S's loads are (D-1)*kL loads, plus with kCopy the stores
+    // in between -- (D-1+S)*kL on the first pass, 2(D-1)*kL after.
     constexpr int kL = 4 * K;  // loads (and, with kCopy, stores) per step
     bool first = true;
-    for (;;) {
-        if (!kCopy || first)
-            wait_rows<2 * kL, K>(A);
-        else
-            wait_rows<4 * kL, K>(A);
-        process(A, ta);
-        if (is_last(ta)) break;
-        ta = advance(tc);
-        issue(ta, A);
-        if (!kCopy)
-            wait_rows<2 * kL, K>(B);
-        else if (first)
-            wait_rows<3 * kL, K>(B);
-        else
-            wait_rows<4 * kL, K>(B);
-        process(B, tb);
-        if (is_last(tb)) break;
-        tb = advance(ta);
-        issue(tb, B);
-        first = false;
-        wait_rows<(kCopy ? 4 : 2) * kL, K>(Cb);
-        process(Cb, tc);
-        if (is_last(tc)) break;
-        tc = advance(tb);
-        issue(tc, Cb);
+#define LAMPI_RING_STEP(S)                                                  \
+    if constexpr ((S) < D) {                                                \
+        if constexpr (kCopy) {                                              \
+            if (first)                                                      \
+                wait_rows<(D - 1 + (S)) * kL, K>(ring[(S) % D]);            \
+            else                                                            \
+                wait_rows<2 * (D - 1) * kL, K>(ring[(S) % D]);              \
+        } else {                                                            \
+            wait_rows<(D - 1) * kL, K>(ring[(S) % D]);                      \
+        }                                                                   \
+        process(ring[(S) % D], t[(S) % D]);                                 \
+        if (is_last(t[(S) % D])) break;                                     \
+        t[(S) % D] = advance(t[((S) + D - 1) % D]);                         \
+        issue(t[(S) % D], ring[(S) % D]);                                   \
     }
+    for (;;) {
+        LAMPI_RING_STEP(0)
+        LAMPI_RING_STEP(1)
+        LAMPI_RING_STEP(2)
+        LAMPI_RING_STEP(3)
+        LAMPI_RING_STEP(4)
+        LAMPI_RING_STEP(5)
+        first = false;
+    }
+#undef LAMPI_RING_STEP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped re-loads before exit
 }
 

@@ -83,16 +83,18 @@ int main(int argc, char **argv) {
     for (size_t L : {4096ul, 16384ul}) {
         const uint32_t n = (uint32_t)(bytes / L);
         const int chains = 2;
-        for (int coal : {0, 1})  // 1: coalesced row layout (the fused-copy kernel's), read only
-        for (uint32_t fpw : (L == 4096 ? std::vector<uint32_t>{16u, 32u, 48u} : std::vector<uint32_t>{8u, 12u})) {
+        for (int depth : {3})  // register ring slots
+        for (uint32_t fpw : (L == 4096 ? std::vector<uint32_t>{16u, 32u, 64u} : std::vector<uint32_t>{4u, 8u, 16u})) {
             const dim3 grid((n + kWaves * fpw - 1) / (kWaves * fpw));
-            for (int v = 0; v < 3; ++v) {
+            for (int v = 0; v < 2; ++v) {  // product, loads-only
                 auto launch = [&] {
-#define LK(V, C) hipLaunchKernelGGL((crc_regular_kernel<V, 2, false, C>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu, dimg, out, nullptr, (size_t)0)
-                    if (coal == 0) {
-                        if (v == 0) LK(0, false); else if (v == 1) LK(1, false); else LK(2, false);
+#define LK(V, DD) hipLaunchKernelGGL((crc_regular_kernel<V, 2, false, false, DD>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L, 0xFFFFFFFFu, dimg, out, nullptr, (size_t)0)
+                    if (depth == 3) {
+                        if (v == 0) LK(0, 3); else if (v == 1) LK(1, 3); else LK(2, 3);
+                    } else if (depth == 4) {
+                        if (v == 0) LK(0, 4); else if (v == 1) LK(1, 4); else LK(2, 4);
                     } else {
-                        if (v == 0) LK(0, true); else if (v == 1) LK(1, true); else LK(2, true);
+                        if (v == 0) LK(0, 5); else if (v == 1) LK(1, 5); else LK(2, 5);
                     }
 #undef LK
                 };
@@ -106,8 +108,8 @@ int main(int argc, char **argv) {
                 float ms;
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 const double s = ms / 1e3 / reps;
-                printf("K=%d %s L=%5zu fpw=%2u %-13s grid=%6u  %8.3f ms  %8.1f GB/s  %5.1f%% of 8 TB/s\n", chains,
-                       coal ? "coal" : "lane", L, fpw, names[v],
+                printf("K=%d D=%d L=%5zu fpw=%2u %-13s grid=%6u  %8.3f ms  %8.1f GB/s  %5.1f%% of 8 TB/s\n", chains,
+                       depth, L, fpw, names[v],
                        grid.x, s * 1e3, bytes / s / 1e9, bytes / s / 8e12 * 100);
                 fflush(stdout);
                 (void)0;
