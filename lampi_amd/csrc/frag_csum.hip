@@ -1394,7 +1394,8 @@ int crc_grid(int device) {
 // fragments per wave for the non-persistent grids: enough work per workgroup to amortise the
 // 64.5 KiB table staging, small enough to keep the chip's read window compact
 static uint32_t pick_fpw(size_t n, uint32_t R) {
-    uint32_t fpw = R >= 4 ? 8u : 32u;
+    // measured on MI355X (profiles/r01_ablation*.txt): 4 KiB fragments fpw 32, >= 16 KiB fpw 12
+    uint32_t fpw = R >= 4 ? 12u : 32u;
     while (fpw > 1 && (size_t)kWaves * fpw * 512 > n) fpw >>= 1;  // small batches: more workgroups
     return fpw;
 }
