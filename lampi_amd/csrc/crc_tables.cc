@@ -1,6 +1,11 @@
 // crc_tables.cc -- see crc_tables.h.
 #include "crc_tables.h"
 
+#include <cstdio>
+#include <cstdlib>
+
+#include "crc_const.h"
+
 #include <cstring>
 #include <mutex>
 
@@ -112,6 +117,22 @@ std::vector<uint32_t> build_table_image() {
     }
     const Gf2Mat h16 = swapped(shift_matrix(kChunkStep));
     for (int b = 0; b < 32; ++b) img[kImgHorner16Cols + b] = h16.col[b];
+
+    // the kernels build the slicing and Horner tables from compile-time constants (crc_const.h):
+    // they must equal the run-time algebra here, bit for bit
+    constexpr cx::SliceBasis sb = cx::slice_basis();
+    constexpr cx::Mat ch = cx::swapped(cx::shift(kRowBytes - kLaneBytes));
+    constexpr cx::Mat ch16 = cx::swapped(cx::shift(kChunkStep));
+    bool same = true;
+    for (int j = 0; j < 4; ++j) {
+        for (int b = 0; b < 5; ++b) same &= sb.lo[j][b] == S[j][1u << b];
+        for (int k = 0; k < 8; ++k) same &= sb.hi[j][k] == S[j][32 * k];
+    }
+    for (int b = 0; b < 32; ++b) same &= ch.c[b] == h.col[b] && ch16.c[b] == h16.col[b];
+    if (!same) {
+        fprintf(stderr, "lampi: compile-time CRC tables differ from the run-time ones\n");
+        abort();
+    }
 
     // powers of two for arbitrary shifts, normal domain (squaring from one byte)
     Gf2Mat pw = shift_matrix(1);

@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <cstdint>
 
+#include "crc_const.h"
 #include "crc_tables.h"
 #include "frag_csum_kernels.h"
 
@@ -230,47 +231,82 @@ __device__ __forceinline__ void store_row(gwbyte *p, const Row &r) {
 }
 
 // ---- LDS table staging --------------------------------------------------------------
-// Loads the basis image with asm loads, lets `pre` issue kPre more asm loads (the first
-// rows of the workgroup, so their HBM latency overlaps the staging), then waits for the
-// basis only (vmcnt(kPre)) and builds the tables.  Ends with an LDS-only barrier: a
-// __syncthreads() would also wait for the row loads.
+// The slicing and Horner tables are built from compile-time constants (crc_const.h): no
+// memory wait.  Only the per-lane combine tables come from the basis image (64 lanes x 32
+// columns, 8 KiB, L2-resident): two dwordx4 loads per thread, issued before anything else so
+// their latency overlaps the rows the workgroup issues next (`pre`) and the constant builds.
 // kParts (diagnostics only, tools/microbench/crc_ablation.hip): bit 0 slicing, bit 1 combine,
 // bit 2 Horner tables; the product always builds all three.
-template <int kPre, class Pre, int kParts = 7, size_t kComb = kImgCombineCols, size_t kHorn = kImgHornerCols>
-__device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__restrict__ img, Pre pre) {
-    const uint32_t t = threadIdx.x;  // 256 threads
-    gbyte *g = (gbyte *)img;
-    // slicing: thread t fills 16-byte slot t & 7 of rows (t >> 3) + 32k, k = 0..7, i.e. table
-    // j = (t & 7) >> 1; consecutive lanes write consecutive slots (a thread-per-row fill put
-    // every lane of a ds_write_b128 on the same banks: 1.2 us per workgroup, measured)
-    const uint32_t sj = (t & 7u) >> 1, r0 = t >> 3;
-    uint32_t sv[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
-        asm volatile("global_load_dword %0, %1, off" : "=&v"(sv[kk]) : "v"(g + 4 * (kImgSliceT + 4 * (r0 + 32 * kk) + sj)) : "memory");
-    // combine: lane l = t & 63, nibble positions p0 = t >> 6 and p0 + 4 (4 columns each)
-    const uint32_t l = t & 63u, p0 = t >> 6;
-    u32x4 ca = issue_b128(g + 4 * (kComb + l * 32 + 4 * p0));
-    u32x4 cb = issue_b128(g + 4 * (kComb + l * 32 + 4 * (p0 + 4)));
-    // Horner: threads 0..127, p = t >> 4 (loads beyond 127 re-read a valid column)
-    u32x4 hc = issue_b128(g + 4 * (kHorn + 4 * ((t >> 4) & 7u)));
-    pre();
-    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(ca), "+v"(cb), "+v"(hc), "+v"(sv[0]) : "n"(kPre) : "memory");
-    asm volatile("" : "+v"(sv[1]), "+v"(sv[2]), "+v"(sv[3]), "+v"(sv[4]), "+v"(sv[5]), "+v"(sv[6]), "+v"(sv[7]));
+constexpr cx::SliceBasis kSliceBasis = cx::slice_basis();
+constexpr cx::Mat kHornerMat = cx::swapped(cx::shift(kRowBytes - kLaneBytes));  // 4032 bytes
+constexpr cx::Mat kHorner16Mat = cx::swapped(cx::shift(kChunkStep));           // 1008 bytes
 
-    char *b = reinterpret_cast<char *>(lds);
-    // rows r0 + 32k, slot t & 7 (bytes 16*(t&7) .. +16 = copies 4*(t&1) .. +3 of S_sj)
+__device__ __forceinline__ uint32_t sel4(uint32_t s, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return (s & 2u) ? ((s & 1u) ? d : c) : ((s & 1u) ? b : a);
+}
+
+struct CombineBasis {
+    u32x4 a, b;  // columns 4*p0 .. +3 and 4*(p0 + 4) .. +3 of lane t & 63, p0 = t >> 6
+};
+
+template <bool kCoal = false>
+__device__ __forceinline__ CombineBasis issue_combine_basis(const uint32_t *__restrict__ img) {
+    constexpr size_t kComb = kCoal ? kImgCombine16Cols : kImgCombineCols;
+    const uint32_t t = threadIdx.x, l = t & 63u, p0 = t >> 6;
+    gbyte *g = (gbyte *)img;
+    CombineBasis cb;
+    cb.a = issue_b128(g + 4 * (kComb + l * 32 + 4 * p0));
+    cb.b = issue_b128(g + 4 * (kComb + l * 32 + 4 * (p0 + 4)));
+    return cb;
+}
+
+// slicing tables: thread t fills 16-byte slot t & 7 (copies 4*(t&1) .. +3 of S_j, j = (t&7) >> 1)
+// of rows (t >> 3) + 32k, k = 0..7; consecutive lanes write consecutive slots (a thread-per-row
+// fill put every lane of a ds_write_b128 on the same banks: 1.2 us per workgroup, measured).
+// S_j[r0 + 32k] = S_j[r0] ^ S_j[32k] by linearity.
+__device__ __forceinline__ void build_slices(char *b) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t sj = (t & 7u) >> 1, r0 = t >> 3;
+    uint32_t base = 0;
 #pragma unroll
-    for (int kk = 0; kk < ((kParts & 1) ? 8 : 0); ++kk) {
-        const uint32_t v = sv[kk];
-        const u32x4 r4 = {v, v, v, v};
-        *reinterpret_cast<u32x4 *>(b + (r0 + 32 * kk) * 256 + (t & 7u) * 16) = r4;
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t k = sel4(sj, kSliceBasis.lo[0][i], kSliceBasis.lo[1][i], kSliceBasis.lo[2][i],
+                                kSliceBasis.lo[3][i]);
+        base ^= ((r0 >> i) & 1u) ? k : 0u;
     }
-    // combine entries (l, p, v) = XOR of columns 4p+bit for the set bits of v
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+        const uint32_t v = base ^ sel4(sj, kSliceBasis.hi[0][kk], kSliceBasis.hi[1][kk], kSliceBasis.hi[2][kk],
+                                       kSliceBasis.hi[3][kk]);
+        *reinterpret_cast<u32x4 *>(b + (r0 + 32 * kk) * 256 + (t & 7u) * 16) = u32x4{v, v, v, v};
+    }
+}
+
+// Horner nibble tables at kLdsHorner + p*64 + 4v: wave w builds p = w and w + 4 (lanes 0..15)
+template <bool kCoal = false>
+__device__ __forceinline__ void build_horner(char *b) {
+    const uint32_t t = threadIdx.x, w = t >> 6, v = t & 63u;
+    if (v >= 16) return;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        if ((uint32_t)(p & 3) != w) continue;
+        uint32_t e = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t col = kCoal ? kHorner16Mat.c[4 * p + i] : kHornerMat.c[4 * p + i];
+            e ^= ((v >> i) & 1u) ? col : 0u;
+        }
+        *reinterpret_cast<uint32_t *>(b + kLdsHorner + p * 64 + v * 4) = e;
+    }
+}
+
+// combine entries (l, p, v) = XOR of columns 4p+bit for the set bits of v
+__device__ __forceinline__ void build_combine(char *b, const CombineBasis &cb) {
+    const uint32_t t = threadIdx.x, l = t & 63u, p0 = t >> 6;
     const uint32_t lane_base = (l >> 5) * 256 + 128 + (l & 31u) * 4;
 #pragma unroll
-    for (int h = 0; h < ((kParts & 2) ? 2 : 0); ++h) {
-        const u32x4 c = h ? cb : ca;
+    for (int h = 0; h < 2; ++h) {
+        const u32x4 c = h ? cb.b : cb.a;
         const uint32_t p = p0 + 4 * h;
 #pragma unroll
         for (uint32_t v = 0; v < 16; ++v) {
@@ -282,16 +318,24 @@ __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__re
             *reinterpret_cast<uint32_t *>(b + p * 8192 + v * 512 + lane_base) = e;
         }
     }
-    if ((kParts & 4) && t < 128) {
-        const uint32_t v = t & 15u;
-        uint32_t e = 0;
-        if (v & 1) e ^= hc.x;
-        if (v & 2) e ^= hc.y;
-        if (v & 4) e ^= hc.z;
-        if (v & 8) e ^= hc.w;
-        *reinterpret_cast<uint32_t *>(b + kLdsHorner + (t >> 4) * 64 + v * 4) = e;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// LDS-only barrier: a __syncthreads() would also wait for the asm-issued row loads
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Issues the combine basis, lets `pre` issue kPre more asm loads (the first rows of the
+// workgroup), builds the constant tables, waits for the basis only (vmcnt(kPre)), builds the
+// combine tables and ends with an LDS-only barrier.
+template <int kPre, class Pre, int kParts = 7, bool kCoal = false>
+__device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__restrict__ img, Pre pre) {
+    CombineBasis cb = issue_combine_basis<kCoal>(img);
+    pre();
+    char *b = reinterpret_cast<char *>(lds);
+    if (kParts & 1) build_slices(b);
+    if (kParts & 4) build_horner<kCoal>(b);
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(cb.a), "+v"(cb.b) : "n"(kPre) : "memory");
+    if (kParts & 2) build_combine(b, cb);
+    lds_barrier();
 }
 
 // ---- loads --------------------------------------------------------------------------
@@ -783,11 +827,9 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
 #pragma unroll
         for (int q = 0; q < D; ++q) issue(t[q], ring[q]);
     };
-    constexpr size_t kComb = kCoal ? kImgCombine16Cols : kImgCombineCols;
-    constexpr size_t kHorn = kCoal ? kImgHorner16Cols : kImgHornerCols;
     if (kAblate != 2) {
         // every ring slot is in flight while the workgroup builds its tables
-        stage_tables<4 * K * D, decltype(issue_all), 7, kComb, kHorn>(lds, img, issue_all);
+        stage_tables<4 * K * D, decltype(issue_all), 7, kCoal>(lds, img, issue_all);
     } else {
         stage_tables<0>(lds, img, [] {});
     }

@@ -26,7 +26,7 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     bench) run bench 600 python bench.py ;;
     bench16k) run bench16k 600 python bench.py --frags 1048576 --frag-bytes 16384 --no-cpu-baseline ;;
     benchsum) run benchsum 600 python bench.py --mode sum --no-cpu-baseline ;;

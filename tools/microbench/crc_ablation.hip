@@ -93,16 +93,19 @@ int main(int argc, char **argv) {
             CK(hipMemcpy(want.data(), out, (size_t)n * 4, hipMemcpyDeviceToHost));
         }
         // fpw sweep of the product configuration (K = 2 chains, 3-slot ring)
-        for (uint32_t fpw : (L == 4096 ? std::vector<uint32_t>{16u, 24u, 32u, 48u} : std::vector<uint32_t>{8u, 12u, 16u})) {
+        for (uint32_t fpw : (L == 4096 ? std::vector<uint32_t>{8u, 16u, 32u} : std::vector<uint32_t>{4u, 8u, 12u})) {
             if (fpw == 0 || n == 0) return 2;
             const dim3 grid((n + kWaves * fpw - 1) / (kWaves * fpw));
-            for (int v = 0; v < 2; ++v) {  // product, loads-only
+            for (int v = 0; v < 3; ++v) {  // product, loads-only, lookups-only
                 auto launch = [&] {
                     if (v == 0)
                         hipLaunchKernelGGL((crc_regular_kernel<0, 2>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L,
                                            0xFFFFFFFFu, dimg, out, nullptr, (size_t)0);
-                    else
+                    else if (v == 1)
                         hipLaunchKernelGGL((crc_regular_kernel<1, 2>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L,
+                                           0xFFFFFFFFu, dimg, out, nullptr, (size_t)0);
+                    else
+                        hipLaunchKernelGGL((crc_regular_kernel<2, 2>), grid, dim3(kBlock), 0, 0, buf, n, fpw, L,
                                            0xFFFFFFFFu, dimg, out, nullptr, (size_t)0);
                 };
                 CK(hipMemset(out, 0, (size_t)n * 4));
@@ -110,7 +113,7 @@ int main(int argc, char **argv) {
                 CK(hipDeviceSynchronize());
                 if (v == 0) {
                     CK(hipMemcpy(got.data(), out, (size_t)n * 4, hipMemcpyDeviceToHost));
-                    if (got != want) printf("!!! fpw=%u: checksums differ from the product launcher\n", fpw);
+                    if (got != want) printf("!!! fpw=%u variant %d: checksums differ from the product launcher\n", fpw, v);
                 }
                 const int reps = 10;
                 CK(hipEventRecord(e0));
