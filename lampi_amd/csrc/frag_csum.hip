@@ -779,7 +779,10 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // them (first pass: 8K / 12K / 16K younger operations, then 16K).  Rows move in the coalesced
 // layout (crc_chunks): lane-contiguous 64-byte stores run at 51% of the HBM roofline on
 // MI355X against 71% for 1 KiB-per-instruction stores (profiles/r01_copy_patterns.txt).
-template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3>
+// kV > 1 (read-only): every row is a whole 4 KiB fragment and rows are visited in the order of a
+// kV*4096-byte fragment (launch with frag_len = kV*4096, n = fragments / kV): chain c of a wave
+// reads kV consecutive fragments one after the other instead of one.
+template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1>
 __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
                                                              uint32_t fpw, size_t frag_len, uint32_t partial,
                                                              const uint32_t *__restrict__ img,
@@ -868,7 +871,7 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
         if constexpr (kCoal) {
             crc_chunks<K>(lds, k, C, b, t.r == 0, (lane == 0) ? vinit : 0u);
         } else {
-            if (t.r == 0) {
+            if (kV > 1 || t.r == 0) {
 #pragma unroll
                 for (int c = 0; c < K; ++c) C[c] = (lane == 0) ? vinit : 0u;
             } else {
@@ -877,7 +880,7 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
             }
             crc_pieces<K>(lds, k, C, b);
         }
-        if (t.r + 1 == R) {
+        if (kV > 1 || t.r + 1 == R) {
             uint32_t x[K];
 #pragma unroll
             for (int c = 0; c < K; ++c) x[c] = lane_combine(lds, k, C[c]);
@@ -886,7 +889,7 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
             if (lane == 0) {
 #pragma unroll
                 for (int c = 0; c < K; ++c)
-                    if (K * t.i + c < nfr) out[frag(t.i, c)] = __builtin_bswap32(x[c]);
+                    if (K * t.i + c < nfr) out[kV > 1 ? frag(t.i, c) * kV + t.r : frag(t.i, c)] = __builtin_bswap32(x[c]);
             }
         }
     };
@@ -1466,14 +1469,39 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     return hipGetLastError();
 }
 
+// Read-kernel schedule, measured on MI355X (tools/microbench/crc_sweep.hip, profiles/r01_sweep.txt):
+// a workgroup covers ~384 KiB (fpw * span = 96 KiB per wave) and its waves walk fragments row by
+// row.  4 KiB fragments are visited in the order of 8 KiB ones (kV = 2: chain c reads two
+// consecutive fragments in turn): 81.4-82.4% of the HBM roofline at every batch offset measured
+// (0, 4 KiB .. 1.5 MiB) against 79.4-79.8% for the previous fpw = 32 fragment-order schedule and
+// 77-79% for the same 384 KiB in fragment order; the 16 KiB order (kV = 4, fpw 6) matched it
+// except at a 64 KiB batch offset (79.8%).  16 KiB fragments: fpw 6, 80.3-82.3% (fpw 12: 78.6%).
+// fpw stays even (two chains, no duplicate ring slots).
+static uint32_t pick_regular_fpw(size_t n, size_t span) {
+    uint32_t fpw = (uint32_t)std::max<size_t>(2, (96u * 1024u / span) & ~(size_t)1);
+    while (fpw > 1 && (size_t)kWaves * fpw * 512 > n) fpw >>= 1;  // small batches: more workgroups
+    return fpw;
+}
+
 hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
                               const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
     if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t fpw = pick_fpw(n, (uint32_t)(frag_len / kRowBytes));
-    hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains>), grid_for(n, fpw), dim3(kBlock), 0, s, base, (uint32_t)n,
-                       fpw, frag_len, partial, img, out, nullptr, (size_t)0);
+    constexpr int kV = 2;
+    size_t done = 0;
+    if (frag_len == (size_t)kRowBytes && n >= (size_t)kV) {
+        const size_t nv = n / kV;
+        const uint32_t fpw = pick_regular_fpw(nv, kV * frag_len);
+        hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains, false, false, 3, kV>), grid_for(nv, fpw), dim3(kBlock),
+                           0, s, base, (uint32_t)nv, fpw, kV * frag_len, partial, img, out, nullptr, (size_t)0);
+        done = nv * kV;
+        if (done == n) return hipGetLastError();
+    }
+    const size_t m = n - done;  // fragment-order schedule (and the last n % kV fragments of a 4 KiB batch)
+    const uint32_t fpw = pick_regular_fpw(m, frag_len);
+    hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains>), grid_for(m, fpw), dim3(kBlock), 0, s,
+                       base + done * frag_len, (uint32_t)m, fpw, frag_len, partial, img, out + done, nullptr, (size_t)0);
     return hipGetLastError();
 }
 

@@ -188,6 +188,37 @@ __global__ void __launch_bounds__(256) il_d(const u32x4 *__restrict__ p, unsigne
     }
 }
 
+// superblock mapping: workgroups are grouped S at a time; workgroup p of superblock s reads,
+// at step i (i < nsteps), block s*S*nsteps + p + i*S (a block = 8 consecutive 4 KiB fragments,
+// wave w takes fragments w and w+4 of it).  The S workgroups of a superblock run together and
+// sweep one compact window instead of S separate streams.  4-B store per fragment.
+__global__ void __launch_bounds__(256) il_sb(const u32x4 *__restrict__ p, unsigned nfrag, unsigned nsteps,
+                                             unsigned S, unsigned *out) {
+    const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned s = blockIdx.x / S, pp = blockIdx.x % S;
+    const unsigned nblk = nfrag / 8;
+    for (unsigned i = 0; i < nsteps; ++i) {
+        const unsigned B = s * S * nsteps + pp + i * S;
+        if (B >= nblk) break;
+        const unsigned f0 = B * 8 + w, f1 = f0 + 4;
+        const u32x4 *q0 = p + (size_t)f0 * 256 + lane * 4;
+        const u32x4 *q1 = p + (size_t)f1 * 256 + lane * 4;
+        u32x4 v[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = q0[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 + k] = q1[k];
+        unsigned a0 = 0, a1 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a0 ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a1 ^= v[4 + k].x ^ v[4 + k].y ^ v[4 + k].z ^ v[4 + k].w;
+        a0 ^= __shfl_xor(a0, 1);
+        a1 ^= __shfl_xor(a1, 1);
+        if (lane == 0) { out[f0] = a0; out[f1] = a1; }
+    }
+}
+
 int main(int argc, char **argv) {
     const size_t bytes = argc > 1 ? strtoull(argv[1], 0, 0) : (16ull << 30);
     void *buf;
@@ -208,15 +239,21 @@ int main(int argc, char **argv) {
         int lds;
     };
     std::vector<Cfg> cfgs;
-    for (int lds : {65536, 98304})
-        for (int d : {1, 2, 4})
-            for (int fpw : {8, 16, 32, 64}) cfgs.push_back({1000 + d * 100 + fpw, 4096, lds});
+    for (int fpw : {8, 16, 32}) cfgs.push_back({100 + fpw, 4096, 65536});
+    for (int S : {256, 512, 1024})
+        for (int fpw : {16, 32, 64, 128}) cfgs.push_back({100000 + S * 1000 + fpw, 4096, 65536});
+    for (int fpw : {8, 16, 32}) cfgs.push_back({100 + fpw, 4096, 65536});
     for (const Cfg &c : cfgs) {
         const unsigned nfrag = (unsigned)(bytes / c.L);
-        const unsigned fpw = c.kind >= 1000 ? c.kind % 100 : c.kind >= 100 ? c.kind - 100 : c.kind >= 30 ? 32 : 16;
-        const unsigned grid = c.kind >= 20 ? (nfrag + 4 * fpw - 1) / (4 * fpw) : c.kind <= 14 ? (nfrag + 3) / 4 : (nfrag + 255) / 256;
+        const unsigned fpw = c.kind >= 100000 ? c.kind % 1000 : c.kind >= 1000 ? c.kind % 100 : c.kind >= 100 ? c.kind - 100 : c.kind >= 30 ? 32 : 16;
+        const unsigned S = c.kind >= 100000 ? (c.kind - 100000) / 1000 : 0;
+        const unsigned grid = c.kind >= 100000 ? (nfrag + 4 * fpw - 1) / (4 * fpw) : c.kind >= 20 ? (nfrag + 4 * fpw - 1) / (4 * fpw) : c.kind <= 14 ? (nfrag + 3) / 4 : (nfrag + 255) / 256;
         auto launch = [&] {
             const u32x4 *b = (const u32x4 *)buf;
+            if (c.kind >= 100000) {
+                hipLaunchKernelGGL(il_sb, dim3(grid), dim3(256), c.lds, 0, b, nfrag, fpw / 2, S, out);
+                return;
+            }
             switch (c.kind) {
                 case 11: hipLaunchKernelGGL(wpf_o<1>, dim3(grid), dim3(256), c.lds, 0, b, nfrag, c.L, out); break;
                 case 12: hipLaunchKernelGGL(wpf_o<2>, dim3(grid), dim3(256), c.lds, 0, b, nfrag, c.L, out); break;
@@ -254,7 +291,7 @@ int main(int argc, char **argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double s = ms / 1e3 / reps;
         if (c.kind >= 10)
-            printf("variant %4d (fpw %2u)     L=%5u lds=%6d grid=%7u  %7.3f ms  %7.1f GB/s (%5.1f%%)\n", c.kind, c.kind >= 20 ? fpw : 1, c.L, c.lds, grid, s * 1e3,
+            printf("variant %6d (fpw %3u)     L=%5u lds=%6d grid=%7u  %7.3f ms  %7.1f GB/s (%5.1f%%)\n", c.kind, c.kind >= 20 ? fpw : 1, c.L, c.lds, grid, s * 1e3,
                    bytes / s / 1e9, bytes / s / 8e10);
         else if (c.kind <= 1)
             printf("wave-per-frag%s L=%5u lds=%6d grid=%7u  %7.3f ms  %7.1f GB/s (%5.1f%%)\n", c.kind ? "+out" : "    ", c.L, c.lds, grid, s * 1e3,
