@@ -50,7 +50,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--frags", type=int, default=4194304, help="fragments per GPU")
     ap.add_argument("--frag-bytes", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=2)
@@ -247,6 +247,7 @@ def run_device(args):
                 "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
                 "kernel": "crc_regular_kernel" if mode == dv.CRC32 else "sum_rows_kernel",
                 "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+                "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2], max(kern_ms))],
                 "algorithmic_bytes_per_launch": n * L,
                 "traffic_source": None if traffic is None else traffic.get("source"),
             },
@@ -304,7 +305,8 @@ def run_mixed(args):
                                "one wavefront per fragment", "fragments": int(lens.size), "bytes": total},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "crc_rows_kernel",
-                     "kernel_avg_ms": round(kern_avg_s * 1e3, 4), "algorithmic_bytes_per_launch": total},
+                     "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
+                "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2], max(kern_ms))], "algorithmic_bytes_per_launch": total},
         "parity": {"check": "full digest vs tests/golden/fixtures.json (config C)", "xor": f"{got[0]:08x}",
                    "wsum": f"{got[1]:08x}", "ok": got == (gold["crc_xor"], gold["crc_wsum"])},
         "cpu_baseline": None}))

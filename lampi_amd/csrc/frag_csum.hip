@@ -782,7 +782,10 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // kV > 1 (read-only): every row is a whole 4 KiB fragment and rows are visited in the order of a
 // kV*4096-byte fragment (launch with frag_len = kV*4096, n = fragments / kV): chain c of a wave
 // reads kV consecutive fragments one after the other instead of one.
-template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1>
+// kSum: the same schedule computes uicsum instead (no tables; the LDS stays allocated so the
+// kernel keeps the two-workgroups-per-CU occupancy the schedule was measured at).
+template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
+          bool kSum = false>
 __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
                                                              uint32_t fpw, size_t frag_len, uint32_t partial,
                                                              const uint32_t *__restrict__ img,
@@ -830,7 +833,10 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
 #pragma unroll
         for (int q = 0; q < D; ++q) issue(t[q], ring[q]);
     };
-    if (kAblate != 2) {
+    if constexpr (kSum) {
+        issue_all();
+        asm volatile("" ::"v"(lds) : "memory");  // the LDS array escapes: it stays allocated
+    } else if (kAblate != 2) {
         // every ring slot is in flight while the workgroup builds its tables
         stage_tables<4 * K * D, decltype(issue_all), 7, kCoal>(lds, img, issue_all);
     } else {
@@ -852,6 +858,26 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
                     store_row<kS>(
                         (gwbyte *)(dst + (uint64_t)frag(t.i, c) * dst_stride + (uint64_t)t.r * kRowBytes + lane_off),
                         b.x[c]);
+        }
+        if constexpr (kSum) {  // uicsum: 32-bit LE words of the fragment, summed mod 2^32
+#pragma unroll
+            for (int c = 0; c < K; ++c) {
+                uint32_t y = (kV > 1 || t.r == 0) ? 0u : C[c];
+#pragma unroll
+                for (int w = 0; w < 16; ++w) y += row_word(b.x[c], w);
+                C[c] = y;
+            }
+            if (kV > 1 || t.r + 1 == R) {
+                uint32_t x[K];
+#pragma unroll
+                for (int c = 0; c < K; ++c) x[c] = wave_add(C[c]);
+                if (lane == 0) {
+#pragma unroll
+                    for (int c = 0; c < K; ++c)
+                        if (K * t.i + c < nfr) out[kV > 1 ? frag(t.i, c) * kV + t.r : frag(t.i, c)] = x[c];
+                }
+            }
+            return;
         }
         if (kAblate == 1) {
 #pragma unroll
@@ -1483,9 +1509,9 @@ static uint32_t pick_regular_fpw(size_t n, size_t span) {
     return fpw;
 }
 
-hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
-                              const uint32_t *img, int grid, hipStream_t s) {
-    (void)grid;
+template <bool kSum>
+static hipError_t launch_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
+                                 const uint32_t *img, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
     constexpr int kV = 2;
@@ -1493,16 +1519,24 @@ hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, ui
     if (frag_len == (size_t)kRowBytes && n >= (size_t)kV) {
         const size_t nv = n / kV;
         const uint32_t fpw = pick_regular_fpw(nv, kV * frag_len);
-        hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains, false, false, 3, kV>), grid_for(nv, fpw), dim3(kBlock),
-                           0, s, base, (uint32_t)nv, fpw, kV * frag_len, partial, img, out, nullptr, (size_t)0);
+        hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains, false, false, 3, kV, kSum>), grid_for(nv, fpw),
+                           dim3(kBlock), 0, s, base, (uint32_t)nv, fpw, kV * frag_len, partial, img, out, nullptr,
+                           (size_t)0);
         done = nv * kV;
         if (done == n) return hipGetLastError();
     }
     const size_t m = n - done;  // fragment-order schedule (and the last n % kV fragments of a 4 KiB batch)
     const uint32_t fpw = pick_regular_fpw(m, frag_len);
-    hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains>), grid_for(m, fpw), dim3(kBlock), 0, s,
-                       base + done * frag_len, (uint32_t)m, fpw, frag_len, partial, img, out + done, nullptr, (size_t)0);
+    hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains, false, false, 3, 1, kSum>), grid_for(m, fpw),
+                       dim3(kBlock), 0, s, base + done * frag_len, (uint32_t)m, fpw, frag_len, partial, img, out + done,
+                       nullptr, (size_t)0);
     return hipGetLastError();
+}
+
+hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
+                              const uint32_t *img, int grid, hipStream_t s) {
+    (void)grid;
+    return launch_regular<false>(base, n, frag_len, partial, out, img, s);
 }
 
 hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint8_t *dst,
@@ -1560,9 +1594,7 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (n == 0) return hipSuccess;
     if (msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 && ((uintptr_t)base & 15u) == 0 &&
         n <= 0xFFFFFFFFull) {
-        hipLaunchKernelGGL(sum_regular_kernel<false>, dim3((unsigned)((n + kWaves - 1) / kWaves)), dim3(kBlock), 0, s,
-                           base, (uint32_t)n, frag_len, out, nullptr, (size_t)0);
-        return hipGetLastError();
+        return launch_regular<true>(base, n, frag_len, 0u, out, nullptr, s);
     }
     const uint32_t fpw = pick_fpw(n, 1);
     hipLaunchKernelGGL(sum_rows_kernel<MsgSource>, grid_for(n, fpw), dim3(kBlock), 0, s,

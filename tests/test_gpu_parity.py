@@ -47,11 +47,12 @@ def test_uniform_batches(cuda, oracle, mode, L):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 @pytest.mark.parametrize("L", [4096, 8192, 12288, 16384, 32768, 65536])
-def test_regular_batches_every_schedule(cuda, oracle, L):
-    """The regular read kernel's schedules: 4 KiB batches in 16 KiB order plus the n % 4 tail
-    launch, fragment-order batches for the other multiples of 4 KiB, small-batch fpw halving;
-    a random starting register each."""
+def test_regular_batches_every_schedule(cuda, oracle, L, mode):
+    """The regular read kernel's schedules (CRC and SUM): 4 KiB batches in 8 KiB row order plus
+    the n % 2 tail launch, fragment-order batches for the other multiples of 4 KiB, small-batch
+    fpw halving; a random starting register each (CRC)."""
     import torch
 
     dv = _dv()
@@ -61,12 +62,12 @@ def test_regular_batches_every_schedule(cuda, oracle, L):
         part = int(rng.integers(0, 2**32))
         buf = torch.empty(n * L, dtype=torch.uint8, device=cuda)
         dv.fill_stream(buf, seed=L + n)
-        got = dv.as_u32(dv.msg_csum(buf, L, partial=part, mode=0))
+        got = dv.as_u32(dv.msg_csum(buf, L, partial=part, mode=mode))
         host = buf.cpu().numpy()
         offs = np.arange(n, dtype=np.uint64) * L
         lens = np.full(n, L, np.uint32)
-        want = oracle.desc_batch(host, offs, lens, np.full(n, part, np.uint32), 0)
-        assert np.array_equal(got, want), (L, n)
+        want = oracle.desc_batch(host, offs, lens, np.full(n, part, np.uint32) if mode == 0 else None, mode)
+        assert np.array_equal(got, want), (L, n, mode)
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])

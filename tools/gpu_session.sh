@@ -32,7 +32,7 @@ for step in "$@"; do
     benchsum) run benchsum 600 python bench.py --mode sum --no-cpu-baseline ;;
     benchC) run benchC 600 python bench.py --config C --steps 10 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-            -- python3 bench.py --steps 10 --no-cpu-baseline ;;
+            -- python3 bench.py --steps 20 --no-cpu-baseline ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \
             -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline &&
          run pmc_ea 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv \
