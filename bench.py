@@ -245,7 +245,7 @@ def run_device(args):
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
-                "kernel": "crc_regular_kernel" if mode == dv.CRC32 else "sum_rows_kernel",
+                "kernel": "crc_regular_kernel" if mode == dv.CRC32 else "crc_regular_kernel (kSum: uicsum on the same schedule)",
                 "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                 "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2], max(kern_ms))],
                 "algorithmic_bytes_per_launch": n * L,
