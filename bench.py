@@ -291,7 +291,8 @@ def run_mixed(args):
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_avg_s = sum(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) / args.steps / 1e3
+    kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
     with open(os.path.join(ROOT, "tests", "golden", "fixtures.json")) as f:
         gold = json.load(f)["digests"]["C"]
     got = digest(dv.as_u32(out))
@@ -306,7 +307,9 @@ def run_mixed(args):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "crc_rows_kernel",
                      "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
-                "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2], max(kern_ms))], "algorithmic_bytes_per_launch": total},
+                     "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2],
+                                                                          max(kern_ms))],
+                     "algorithmic_bytes_per_launch": total},
         "parity": {"check": "full digest vs tests/golden/fixtures.json (config C)", "xor": f"{got[0]:08x}",
                    "wsum": f"{got[1]:08x}", "ok": got == (gold["crc_xor"], gold["crc_wsum"])},
         "cpu_baseline": None}))

@@ -667,6 +667,207 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
     }
 }
 
+// ---- CRC, general fragments, pipelined (descriptor batches, ragged messages) --------------
+// The frame of crc_rows_kernel (one wavefront per fragment, right-aligned 4 KiB rows), but the
+// wave's rows stream through a kD-slot register ring of asm-issued loads -- kD-1 rows in
+// flight while one is checksummed, across fragment boundaries -- instead of one compiler
+// prefetch, and the wave's descriptors are read once, one per lane, while the tables are
+// staged.  Every row is exactly five dwordx4 loads: the aligned 16-byte chunks covering the
+// lane's 64-byte window (shifted into place by v_alignbyte for misaligned fragments); a chunk
+// wholly outside the fragment is redirected to the fragment's first chunk and never used, so
+// nothing outside an aligned chunk holding a fragment byte is read and the waits count the
+// ring exactly.
+struct RawRow {
+    u32x4 q[5];
+};
+
+struct FragGeom {  // wave-uniform
+    gbyte *addr;
+    uint32_t len, partial, R, P, s16;
+};
+
+template <int N>
+__device__ __forceinline__ void wait_raw(RawRow &r) {
+    asm volatile("s_waitcnt vmcnt(%5)"
+                 : "+v"(r.q[0]), "+v"(r.q[1]), "+v"(r.q[2]), "+v"(r.q[3]), "+v"(r.q[4])
+                 : "n"(N)
+                 : "memory");
+}
+
+// window [o, o + 64) relative to addr; addr + o - s16 is 16-byte aligned.  Chunks wholly outside
+// the fragment load 16 zero bytes (`zero`, in the table image), so with a 16-byte-aligned
+// fragment the row-0 padding needs no masking.
+__device__ __forceinline__ void issue_frag_row(const FragGeom &g, uint32_t r, int lane, gbyte *zero, RawRow &raw) {
+    const long long o = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P;
+    const long long cb = o - (long long)g.s16;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const long long c = cb + 16 * k;
+        const bool inside = c + 16 > 0 && c < (long long)g.len;
+        raw.q[k] = issue_b128(inside ? g.addr + c : zero);
+    }
+}
+
+// the lane's 16 LE words of the frame row; bytes before the fragment (row 0 padding) read as 0
+// (only a fragment that does not start on a 16-byte boundary has a chunk holding bytes on both
+// sides of its start: that row 0 is masked byte by byte)
+__device__ __forceinline__ void finish_frag_row(const FragGeom &g, uint32_t r, int lane, const RawRow &raw,
+                                                uint32_t d[16]) {
+    uint32_t a[20];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        a[4 * k + 0] = raw.q[k].x;
+        a[4 * k + 1] = raw.q[k].y;
+        a[4 * k + 2] = raw.q[k].z;
+        a[4 * k + 3] = raw.q[k].w;
+    }
+    const uint32_t sb = g.s16 & 3u;
+    switch (g.s16 >> 2) {  // wave-uniform
+#define LAMPI_SHIFT_CASE(W)                                                                  \
+    case W:                                                                                  \
+        _Pragma("unroll") for (int w = 0; w < 16; ++w) d[w] =                                \
+            __builtin_amdgcn_alignbyte(a[w + (W) + 1], a[w + (W)], sb);                      \
+        break;
+        LAMPI_SHIFT_CASE(0)
+        LAMPI_SHIFT_CASE(1)
+        LAMPI_SHIFT_CASE(2)
+        LAMPI_SHIFT_CASE(3)
+#undef LAMPI_SHIFT_CASE
+    }
+    if (r == 0 && ((uintptr_t)g.addr & 15u) != 0) {
+        const long long o = (long long)lane * kLaneBytes - (long long)g.P;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) d[w] &= byte_keep_mask(o + 4 * w, 0, (long long)g.len);
+    }
+}
+
+// Work split: a workgroup owns kFragsPerWg consecutive fragments; every wave reads all their
+// descriptors (lane j <-> fragment j), and the fragments are cut into four contiguous runs of
+// about equal row counts, one per wave (Zipf-sized batches: interleaving fragments over the
+// waves left the slowest wave of a workgroup 24% above the mean).
+constexpr uint32_t kFragsPerWg = 64;
+
+template <class Src, int kD = 4>
+__global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, const uint32_t *__restrict__ img,
+                                                           uint32_t *__restrict__ out) {
+    static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * kFragsPerWg;
+    const uint32_t nwg = (uint32_t)min((size_t)kFragsPerWg, n - base);
+    const size_t fl = base + (size_t)lane;
+    FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
+    if ((uint32_t)lane < nwg) mine = src.get(fl);
+    stage_tables<0>(lds, img, [] {});  // waits for the descriptors too
+    if (wave == 0 && (uint32_t)lane < nwg && mine.len == 0) out[fl] = mine.partial;  // uicrc(p, 0, s) == s
+    const uint32_t myR = (mine.len + (kRowBytes - 1)) / kRowBytes;
+    // exclusive prefix of the row counts over the workgroup's fragments
+    uint32_t incl = myR;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, s, 64);
+        if (lane >= s) incl += v;
+    }
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t start = incl - myR;
+    const uint32_t owner = total ? min(3u, (uint32_t)(((uint64_t)start * kWaves) / total)) : 0u;
+    uint64_t todo = __ballot((uint32_t)lane < nwg && mine.len != 0 && owner == wave);
+    if (todo == 0) return;
+    const uint32_t myP = myR * kRowBytes - mine.len;
+    const uint32_t myS = (uint32_t)(((uintptr_t)mine.addr - myP) & 15u);
+    const uint64_t myA = (uint64_t)(uintptr_t)mine.addr;
+
+    struct Task {
+        uint32_t j, r;
+        FragGeom g;
+    };
+    auto geom = [&](uint32_t j) -> FragGeom {
+        FragGeom g;
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)myA, j);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(myA >> 32), j);
+        g.addr = (gbyte *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+        g.len = __builtin_amdgcn_readlane(mine.len, j);
+        g.partial = __builtin_amdgcn_readlane(mine.partial, j);
+        g.R = __builtin_amdgcn_readlane(myR, j);
+        g.P = __builtin_amdgcn_readlane(myP, j);
+        g.s16 = __builtin_amdgcn_readlane(myS, j);
+        return g;
+    };
+    auto next_frag = [&](uint32_t j) -> uint32_t {  // next fragment to checksum after j, or 64
+        const uint64_t rest = j >= 63 ? 0ull : (todo & ~((2ull << j) - 1ull));
+        return rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
+    };
+    const uint32_t jlast = 63u - (uint32_t)__builtin_clzll(todo);
+    auto advance = [&](const Task &t) -> Task {
+        if (t.r + 1 < t.g.R) return {t.j, t.r + 1, t.g};
+        const uint32_t nj = next_frag(t.j);
+        if (nj >= 64) return t;  // past the end: re-issue the last row (never processed)
+        return {nj, 0u, geom(nj)};
+    };
+    auto is_last = [&](const Task &t) -> bool { return t.j == jlast && t.r + 1 >= t.g.R; };
+
+    gbyte *zero = (gbyte *)(img + kImgZero);
+    Task t[kD];
+    RawRow ring[kD];
+    {
+        const uint32_t j0 = (uint32_t)__builtin_ctzll(todo);
+        t[0] = Task{j0, 0u, geom(j0)};
+    }
+#pragma unroll
+    for (int q = 1; q < kD; ++q) t[q] = advance(t[q - 1]);
+#pragma unroll
+    for (int q = 0; q < kD; ++q) issue_frag_row(t[q].g, t[q].r, lane, zero, ring[q]);
+
+    const CrcLane k = make_lane(lane);
+    uint32_t C = 0;
+    auto process = [&](const RawRow &raw, const Task &tk) {
+        uint32_t d[16];
+        finish_frag_row(tk.g, tk.r, lane, raw, d);
+        if (tk.r == 0) {
+            if ((tk.g.P & 63u) == 0) {  // the register enters as lane P/64's starting value
+                C = ((uint32_t)lane == (tk.g.P >> 6)) ? __builtin_bswap32(tk.g.partial) : 0u;
+            } else {
+                C = 0;
+                RowGeom rg{tk.g.R, tk.g.P, tk.g.s16};
+                crc_inject(d, rg, tk.g.partial, lane);
+            }
+        } else {
+            C = horner_shift(lds, C);
+            if (tk.r == 1 && tk.g.P > (uint32_t)kRowBytes - 4 && lane == 0)  // register bytes spill into row 1
+                d[0] ^= __builtin_bswap32(tk.g.partial) >> (8 * (kRowBytes - tk.g.P));
+        }
+        C = crc_piece(lds, k, C, d);
+        if (tk.r + 1 == tk.g.R) {
+            const uint32_t x = wave_xor(lane_combine(lds, k, C));
+            if (lane == 0) {
+                uint32_t res = __builtin_bswap32(x);
+                if (tk.g.len < 4) res ^= tk.g.partial << (8 * tk.g.len);
+                out[base + tk.j] = res;
+            }
+        }
+    };
+    constexpr int kL = 5;  // loads per row
+#define LAMPI_FRAG_STEP(S)                                           \
+    if constexpr ((S) < kD) {                                        \
+        wait_raw<(kD - 1) * kL>(ring[(S) % kD]);                     \
+        process(ring[(S) % kD], t[(S) % kD]);                        \
+        if (is_last(t[(S) % kD])) break;                             \
+        t[(S) % kD] = advance(t[((S) + kD - 1) % kD]);               \
+        issue_frag_row(t[(S) % kD].g, t[(S) % kD].r, lane, zero, ring[(S) % kD]); \
+    }
+    for (;;) {
+        LAMPI_FRAG_STEP(0)
+        LAMPI_FRAG_STEP(1)
+        LAMPI_FRAG_STEP(2)
+        LAMPI_FRAG_STEP(3)
+        LAMPI_FRAG_STEP(4)
+        LAMPI_FRAG_STEP(5)
+    }
+#undef LAMPI_FRAG_STEP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the re-issued rows before exit
+}
+
 // ---- CRC fast path: regular batches -------------------------------------------------------
 // Fragment f = base + f*frag_len, frag_len = R*4096, base 16-byte aligned (P = 0, no masks).
 // A wave checksums kChains of its fragments at once (independent lookup chains interleaved:
@@ -1473,15 +1674,15 @@ static uint32_t pick_fpw(size_t n, uint32_t R) {
 
 constexpr int kRegularChains = 2;
 
+static dim3 frags_grid(size_t n) { return dim3((unsigned)((n + kFragsPerWg - 1) / kFragsPerWg)); }
+
 static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size_t)kWaves * fpw - 1) / ((size_t)kWaves * fpw))); }
 
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
                            hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
-    const uint32_t fpw = pick_fpw(n, 1);
-    hipLaunchKernelGGL(crc_rows_kernel<DescSource>, grid_for(n, fpw), dim3(kBlock), 0, s, DescSource{d}, n, fpw, img,
-                       out);
+    hipLaunchKernelGGL(crc_frags_kernel<DescSource>, frags_grid(n), dim3(kBlock), 0, s, DescSource{d}, n, img, out);
     return hipGetLastError();
 }
 
@@ -1489,9 +1690,8 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
-    const uint32_t fpw = pick_fpw(n, (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes));
-    hipLaunchKernelGGL(crc_rows_kernel<MsgSource>, grid_for(n, fpw), dim3(kBlock), 0, s,
-                       MsgSource{base, msg_len, frag_len, partial}, n, fpw, img, out);
+    hipLaunchKernelGGL(crc_frags_kernel<MsgSource>, frags_grid(n), dim3(kBlock), 0, s,
+                       MsgSource{base, msg_len, frag_len, partial}, n, img, out);
     return hipGetLastError();
 }
 
