@@ -506,12 +506,18 @@ __device__ __forceinline__ uint32_t lane_combine(const uint32_t *lds, const CrcL
     return r;
 }
 
-// XOR of v over the 64 lanes: DPP butterflies inside each row of 16, then 4 readlanes.
-__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+// XOR of v over each row of 16 lanes (every lane of the row gets it): DPP butterflies.
+__device__ __forceinline__ uint32_t row16_xor(uint32_t v) {
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+    return v;
+}
+
+// XOR of v over the 64 lanes: the four row XORs combined by readlane.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+    v = row16_xor(v);
     return __builtin_amdgcn_readlane(v, 0) ^ __builtin_amdgcn_readlane(v, 16) ^ __builtin_amdgcn_readlane(v, 32) ^
            __builtin_amdgcn_readlane(v, 48);
 }
@@ -697,15 +703,36 @@ __device__ __forceinline__ void wait_raw(RawRow &r) {
 // window [o, o + 64) relative to addr; addr + o - s16 is 16-byte aligned.  Chunks wholly outside
 // the fragment load 16 zero bytes (`zero`, in the table image), so with a 16-byte-aligned
 // fragment the row-0 padding needs no masking.
-__device__ __forceinline__ void issue_frag_row(const FragGeom &g, uint32_t r, int lane, gbyte *zero, RawRow &raw) {
+// The five loads of a ring slot are one asm block fed with addresses computed beforehand: a
+// slot's registers must be defined at a single point -- loads issued on two branches would
+// meet in a phi, and a register copy of data still in flight reads garbage.
+struct RowAddrs {
+    gbyte *p[5];
+};
+
+__device__ __forceinline__ void issue_row5(const RowAddrs &a, RawRow &raw) {
+    asm volatile(
+        "global_load_dwordx4 %0, %5, off\n\t"
+        "global_load_dwordx4 %1, %6, off\n\t"
+        "global_load_dwordx4 %2, %7, off\n\t"
+        "global_load_dwordx4 %3, %8, off\n\t"
+        "global_load_dwordx4 %4, %9, off"
+        : "=&v"(raw.q[0]), "=&v"(raw.q[1]), "=&v"(raw.q[2]), "=&v"(raw.q[3]), "=&v"(raw.q[4])
+        : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(a.p[3]), "v"(a.p[4])
+        : "memory");
+}
+
+__device__ __forceinline__ RowAddrs frag_row_addrs(const FragGeom &g, uint32_t r, int lane, gbyte *zero) {
     const long long o = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P;
     const long long cb = o - (long long)g.s16;
+    RowAddrs a;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         const long long c = cb + 16 * k;
-        const bool inside = c + 16 > 0 && c < (long long)g.len;
-        raw.q[k] = issue_b128(inside ? g.addr + c : zero);
+        const bool inside = (k < 4 || g.s16 != 0) && c + 16 > 0 && c < (long long)g.len;
+        a.p[k] = inside ? g.addr + c : zero;
     }
+    return a;
 }
 
 // the lane's 16 LE words of the frame row; bytes before the fragment (row 0 padding) read as 0
@@ -743,9 +770,34 @@ __device__ __forceinline__ void finish_frag_row(const FragGeom &g, uint32_t r, i
 
 // Work split: a workgroup owns kFragsPerWg consecutive fragments; every wave reads all their
 // descriptors (lane j <-> fragment j), and the fragments are cut into four contiguous runs of
-// about equal row counts, one per wave (Zipf-sized batches: interleaving fragments over the
-// waves left the slowest wave of a workgroup 24% above the mean).
+// about equal cost, one per wave (Zipf-sized batches: interleaving fragments over the waves
+// left the slowest wave of a workgroup 24% above the mean).
+//
+// Small fragments go in lane groups ("packs"): a fragment of 16..1024 bytes, a multiple of 16
+// and 16-byte aligned, is checksummed by 16 lanes as one 1 KiB row (right-aligned frame,
+// P = 1024 - len), four fragments per row.  Group lane g's combine shift, 64*(15-g) bytes, is
+// lane 48+g's table (lanes g and g+16 share a bank: 2-way); the group XOR is the 16-lane DPP
+// row reduction.  A 64-byte fragment then costs a quarter row of lookups instead of a row.
 constexpr uint32_t kFragsPerWg = 64;
+constexpr uint32_t kPackBytes = 1024;
+
+__device__ __forceinline__ bool pack_ok(uint32_t len, uint64_t addr) {
+    return len >= 16 && len <= kPackBytes && (len & 15u) == 0 && (addr & 15u) == 0;
+}
+
+// pack row: group lane g of a fragment of `len` bytes at `addr` (len 0: an empty group); the
+// fifth chunk is never used by a 16-byte-aligned frame and reads the zero chunk
+__device__ __forceinline__ RowAddrs pack_row_addrs(gbyte *addr, uint32_t len, uint32_t g, gbyte *zero) {
+    const long long o = (long long)g * kLaneBytes - (long long)(kPackBytes - len);
+    RowAddrs a;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const long long c = o + 16 * k;
+        const bool inside = k < 4 && c + 16 > 0 && c < (long long)len;
+        a.p[k] = inside ? addr + c : zero;
+    }
+    return a;
+}
 
 template <class Src, int kD = 4>
 __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, const uint32_t *__restrict__ img,
@@ -761,24 +813,30 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, co
     if ((uint32_t)lane < nwg) mine = src.get(fl);
     stage_tables<0>(lds, img, [] {});  // waits for the descriptors too
     if (wave == 0 && (uint32_t)lane < nwg && mine.len == 0) out[fl] = mine.partial;  // uicrc(p, 0, s) == s
+    const uint64_t myA = (uint64_t)(uintptr_t)mine.addr;
+    const bool myPack = (uint32_t)lane < nwg && pack_ok(mine.len, myA);
     const uint32_t myR = (mine.len + (kRowBytes - 1)) / kRowBytes;
-    // exclusive prefix of the row counts over the workgroup's fragments
-    uint32_t incl = myR;
+    // exclusive prefix of the costs (quarter rows: a pack member 1, a fragment 4 per row)
+    const uint32_t myCost = myPack ? 1u : 4u * myR;
+    uint32_t incl = myCost;
 #pragma unroll
     for (int s = 1; s < 64; s <<= 1) {
         const uint32_t v = (uint32_t)__shfl_up((int)incl, s, 64);
         if (lane >= s) incl += v;
     }
     const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    const uint32_t start = incl - myR;
+    const uint32_t start = incl - myCost;
     const uint32_t owner = total ? min(3u, (uint32_t)(((uint64_t)start * kWaves) / total)) : 0u;
-    uint64_t todo = __ballot((uint32_t)lane < nwg && mine.len != 0 && owner == wave);
-    if (todo == 0) return;
+    const uint64_t mineAll = __ballot((uint32_t)lane < nwg && mine.len != 0 && owner == wave);
+    if (mineAll == 0) return;
+    const uint64_t qall = mineAll & __ballot(myPack);  // pack members, in index order
+    const uint64_t todo = mineAll & ~qall;             // fragments in whole 4 KiB rows
     const uint32_t myP = myR * kRowBytes - mine.len;
     const uint32_t myS = (uint32_t)(((uintptr_t)mine.addr - myP) & 15u);
-    const uint64_t myA = (uint64_t)(uintptr_t)mine.addr;
 
     struct Task {
+        uint32_t pk;  // 1: a pack of up to four members (qm), 0: row r of fragment j
+        uint64_t qm;
         uint32_t j, r;
         FragGeom g;
     };
@@ -794,34 +852,121 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, co
         g.s16 = __builtin_amdgcn_readlane(myS, j);
         return g;
     };
-    auto next_frag = [&](uint32_t j) -> uint32_t {  // next fragment to checksum after j, or 64
-        const uint64_t rest = j >= 63 ? 0ull : (todo & ~((2ull << j) - 1ull));
-        return rest ? (uint32_t)__builtin_ctzll(rest) : 64u;
+    auto above = [](uint64_t set, uint32_t j) -> uint64_t {  // members of set after bit j
+        return j >= 63 ? 0ull : (set & ~((2ull << j) - 1ull));
     };
-    const uint32_t jlast = 63u - (uint32_t)__builtin_clzll(todo);
+    auto first4 = [](uint64_t set) -> uint64_t {  // the (up to) four lowest members of set
+        uint64_t pm = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t b = set & (0ull - set);
+            pm |= b;
+            set &= ~b;
+        }
+        return pm;
+    };
+    auto first_row = [&]() -> Task {
+        const uint32_t j0 = (uint32_t)__builtin_ctzll(todo);
+        return Task{0u, 0ull, j0, 0u, geom(j0)};
+    };
+    const uint64_t last_pack = qall ? (1ull << (63 - __builtin_clzll(qall))) : 0ull;
+    const uint32_t jlast = todo ? 63u - (uint32_t)__builtin_clzll(todo) : 64u;
     auto advance = [&](const Task &t) -> Task {
-        if (t.r + 1 < t.g.R) return {t.j, t.r + 1, t.g};
-        const uint32_t nj = next_frag(t.j);
-        if (nj >= 64) return t;  // past the end: re-issue the last row (never processed)
-        return {nj, 0u, geom(nj)};
+        if (t.pk) {
+            const uint64_t rest = above(qall, 63u - (uint32_t)__builtin_clzll(t.qm));
+            if (rest) return Task{1u, first4(rest), 0u, 0u, t.g};
+            if (todo) return first_row();
+            return t;  // past the end: re-issue the last task (never processed)
+        }
+        if (t.r + 1 < t.g.R) return Task{0u, 0ull, t.j, t.r + 1, t.g};
+        const uint64_t rest = above(todo, t.j);
+        if (!rest) return t;
+        const uint32_t nj = (uint32_t)__builtin_ctzll(rest);
+        return Task{0u, 0ull, nj, 0u, geom(nj)};
     };
-    auto is_last = [&](const Task &t) -> bool { return t.j == jlast && t.r + 1 >= t.g.R; };
+    auto is_last = [&](const Task &t) -> bool {
+        if (todo) return !t.pk && t.j == jlast && t.r + 1 >= t.g.R;
+        return t.pk && (t.qm & last_pack) != 0;
+    };
 
+    // this lane's pack member: the (lane >> 4)-th lowest bit of qm (none: j = 64, len 0)
+    struct Member {
+        uint32_t j, len, partial;
+        gbyte *addr;
+    };
+    auto member = [&](uint64_t qm) -> Member {
+        uint32_t js[4];
+        uint64_t m = qm;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            js[i] = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+            m &= m - 1ull;
+        }
+        Member p;
+        p.j = sel4((uint32_t)lane >> 4, js[0], js[1], js[2], js[3]);
+        const int srcl = (int)(p.j & 63u);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)myA, srcl, 64);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(myA >> 32), srcl, 64);
+        p.addr = (gbyte *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+        // every lane takes part in the shuffles (a shuffle inside a lane-divergent condition
+        // reads 0 from source lanes that are switched off)
+        const uint32_t len = (uint32_t)__shfl((int)mine.len, srcl, 64);
+        p.len = p.j < 64 ? len : 0u;
+        p.partial = (uint32_t)__shfl((int)mine.partial, srcl, 64);
+        return p;
+    };
     gbyte *zero = (gbyte *)(img + kImgZero);
+    auto issue = [&](const Task &t, RawRow &raw) {
+        RowAddrs a;
+        if (t.pk) {
+            const Member p = member(t.qm);
+            a = pack_row_addrs(p.addr, p.len, (uint32_t)lane & 15u, zero);
+        } else {
+            a = frag_row_addrs(t.g, t.r, lane, zero);
+        }
+        issue_row5(a, raw);
+    };
+
     Task t[kD];
     RawRow ring[kD];
-    {
-        const uint32_t j0 = (uint32_t)__builtin_ctzll(todo);
-        t[0] = Task{j0, 0u, geom(j0)};
-    }
+    t[0] = qall ? Task{1u, first4(qall), 0u, 0u, FragGeom{}} : first_row();
 #pragma unroll
     for (int q = 1; q < kD; ++q) t[q] = advance(t[q - 1]);
 #pragma unroll
-    for (int q = 0; q < kD; ++q) issue_frag_row(t[q].g, t[q].r, lane, zero, ring[q]);
+    for (int q = 0; q < kD; ++q) issue(t[q], ring[q]);
 
     const CrcLane k = make_lane(lane);
     uint32_t C = 0;
+    auto process_pack = [&](const RawRow &raw, const Task &tk) {
+        const Member p = member(tk.qm);
+        uint32_t d[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            d[4 * q + 0] = raw.q[q].x;
+            d[4 * q + 1] = raw.q[q].y;
+            d[4 * q + 2] = raw.q[q].z;
+            d[4 * q + 3] = raw.q[q].w;
+        }
+        const uint32_t g = (uint32_t)lane & 15u, P = kPackBytes - p.len;
+        uint32_t c;
+        if ((P & 63u) == 0) {
+            c = (g == (P >> 6)) ? __builtin_bswap32(p.partial) : 0u;
+        } else {
+            c = 0;
+            RowGeom rg{1u, P, 0u};
+            crc_inject(d, rg, p.partial, (int)g);
+        }
+        c = crc_piece(lds, k, c, d);
+        CrcLane kq = k;
+        kq.comb_base = 448u + 4u * g;  // lane 48 + g's combine column: shift by 64*(15-g)
+        const uint32_t x = row16_xor(lane_combine(lds, kq, c));
+        if (g == 0 && p.j < 64) out[base + p.j] = __builtin_bswap32(x);
+    };
     auto process = [&](const RawRow &raw, const Task &tk) {
+        if (tk.pk) {
+            process_pack(raw, tk);
+            return;
+        }
         uint32_t d[16];
         finish_frag_row(tk.g, tk.r, lane, raw, d);
         if (tk.r == 0) {
@@ -854,7 +999,7 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, co
         process(ring[(S) % kD], t[(S) % kD]);                        \
         if (is_last(t[(S) % kD])) break;                             \
         t[(S) % kD] = advance(t[((S) + kD - 1) % kD]);               \
-        issue_frag_row(t[(S) % kD].g, t[(S) % kD].r, lane, zero, ring[(S) % kD]); \
+        issue(t[(S) % kD], ring[(S) % kD]);                          \
     }
     for (;;) {
         LAMPI_FRAG_STEP(0)
@@ -1139,10 +1284,15 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
     // in between -- (D-1+S)*kL on the first pass, 2(D-1)*kL after.
     constexpr int kL = 4 * K;  // loads (and, with kCopy, stores) per step
     bool first = true;
+    // a wave whose fragment count is not a multiple of K skips the stores of its missing chain
+    // in the last group: fewer younger operations than the counts assume, so those steps drain
+    const bool short_tail = kCopy && (nfr % K) != 0;
 #define LAMPI_RING_STEP(S)                                                  \
     if constexpr ((S) < D) {                                                \
         if constexpr (kCopy) {                                              \
-            if (first)                                                      \
+            if (short_tail && t[(S) % D].i + 1 >= ngrp)                     \
+                wait_rows<0, K>(ring[(S) % D]);                             \
+            else if (first)                                                 \
                 wait_rows<(D - 1 + (S)) * kL, K>(ring[(S) % D]);            \
             else                                                            \
                 wait_rows<2 * (D - 1) * kL, K>(ring[(S) % D]);              \

@@ -46,13 +46,15 @@ def combine_digests(parts) -> tuple[int, int]:
 
 
 def allreduce_digest(local: tuple[int, int], group=None) -> tuple[int, int]:
-    """Combine this rank's shard digest with every other rank's (torch.distributed)."""
+    """Combine this rank's shard digest with every other rank's (torch.distributed).
+
+    The per-rank digests are all-gathered and combined here: RCCL/NCCL have no bitwise-XOR
+    reduction, so an all_reduce(BXOR) would only work on gloo."""
     import torch
     import torch.distributed as dist
 
     dev = "cpu" if dist.get_backend(group) == "gloo" else "cuda"
-    x = torch.tensor([local[0]], dtype=torch.int64, device=dev)
-    s = torch.tensor([local[1]], dtype=torch.int64, device=dev)
-    dist.all_reduce(x, op=dist.ReduceOp.BXOR, group=group)
-    dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
-    return int(x.item()) & 0xFFFFFFFF, int(s.item()) & 0xFFFFFFFF
+    mine = torch.tensor([local[0], local[1]], dtype=torch.int64, device=dev)
+    parts = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, mine, group=group)
+    return combine_digests([(int(p[0].item()), int(p[1].item())) for p in parts])

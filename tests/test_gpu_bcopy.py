@@ -144,6 +144,8 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     (4096 * 50000, 4096, 4096, 0),          # regular fast path, plain copy
     (4096 * 20000, 4096, 8192, 0),          # regular, staging slots with gaps
     (16384 * 3000, 16384, 16384 + 64, 16),  # regular, 4-row fragments
+    (16384 * 3001, 16384, 16384 + 16, 0),   # regular, a last wave with an odd fragment count
+    (4096 * 4097, 4096, 4096 + 32, 0),      # regular, 4 KiB, odd count in the last wave
     (65456 * 300 + 17, 65456, 65528, 0),    # GM payload into 72 + 65456-byte slots (general path)
     (1000003, 4096, 4100, 3),               # ragged everything
     (5, 4096, 4096, 1),                     # one short fragment

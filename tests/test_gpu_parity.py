@@ -131,6 +131,33 @@ def test_descriptor_batch_random(cuda, oracle):
         assert np.array_equal(got, want)
 
 
+def test_descriptor_batch_small_fragment_packs(cuda, oracle):
+    """Fragments of 16..1024 bytes (multiples of 16, 16-byte aligned) go four to a row in lane
+    groups; mixed with unaligned, odd-length, empty and multi-row fragments in one batch, every
+    register random, so packs, partial packs and whole-row fragments interleave in every wave."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(2024)
+    base = torch.empty(32 << 20, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=44)
+    host = base.cpu().numpy()
+    n = 30000
+    kind = rng.integers(0, 10, size=n)
+    lens = np.where(kind < 6, 16 * rng.integers(1, 65, size=n),            # pack members
+                    np.where(kind < 8, rng.integers(1, 1100, size=n),       # small, any length
+                             rng.integers(0, 20000, size=n))).astype(np.uint64)
+    offs = rng.integers(0, (32 << 20) - 20100, size=n).astype(np.uint64)
+    offs[kind < 6] &= ~np.uint64(15)                                         # aligned members
+    offs[kind == 6] |= np.uint64(1)                                          # misaligned small ones
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    descs = dv.make_descs(base, offs, lens, parts)
+    got = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.CRC32))
+    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32), 0)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+
+
 def test_kat_check_values(cuda):
     import torch
 
