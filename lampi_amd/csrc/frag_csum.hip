@@ -723,14 +723,24 @@ __device__ __forceinline__ void issue_row5(const RowAddrs &a, RawRow &raw) {
 }
 
 __device__ __forceinline__ RowAddrs frag_row_addrs(const FragGeom &g, uint32_t r, int lane, gbyte *zero) {
-    const long long o = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P;
-    const long long cb = o - (long long)g.s16;
+    // aligned chunk base of the lane's window, relative to addr
+    const long long cb = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P - (long long)g.s16;
+    gbyte *b = g.addr + cb;
     RowAddrs a;
+    if (g.s16 == 0 && (r > 0 || g.P == 0)) {  // every lane's four chunks inside, the fifth unused
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a.p[k] = b + 16 * k;
+        a.p[4] = zero;
+        return a;
+    }
+    // row 0 of a padded frame or a misaligned fragment: chunk c = cb + 16k is inside iff
+    // -16 < c < len, i.e. (unsigned)(c + 15) < len + 15 while |c| < 2^31
+    const bool small = g.len < 0x80000000u;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         const long long c = cb + 16 * k;
-        const bool inside = (k < 4 || g.s16 != 0) && c + 16 > 0 && c < (long long)g.len;
-        a.p[k] = inside ? g.addr + c : zero;
+        const bool in = small ? ((uint32_t)c + 15u < g.len + 15u) : (c + 16 > 0 && c < (long long)g.len);
+        a.p[k] = ((k < 4 || g.s16 != 0) && in) ? b + 16 * k : zero;
     }
     return a;
 }
@@ -749,7 +759,10 @@ __device__ __forceinline__ void finish_frag_row(const FragGeom &g, uint32_t r, i
         a[4 * k + 3] = raw.q[k].w;
     }
     const uint32_t sb = g.s16 & 3u;
-    switch (g.s16 >> 2) {  // wave-uniform
+    if (g.s16 == 0) {
+#pragma unroll
+        for (int w = 0; w < 16; ++w) d[w] = a[w];
+    } else switch (g.s16 >> 2) {  // wave-uniform
 #define LAMPI_SHIFT_CASE(W)                                                                  \
     case W:                                                                                  \
         _Pragma("unroll") for (int w = 0; w < 16; ++w) d[w] =                                \
