@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--e2e", action="store_true", help="host-memory end-to-end path (config E)")
     ap.add_argument("--bcopy", action="store_true",
                     help="fused copy + checksum batch (lampi_frag_bcopy_batch) on the config B shape")
+    ap.add_argument("--desc", action="store_true",
+                    help="run the batch through descriptors (lampi_frag_csum_batch, the general kernel) "
+                         "instead of the contiguous-message entry point (diagnostic)")
     return ap.parse_args()
 
 
@@ -167,10 +170,15 @@ def run_device(args):
     buf = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     dv.fill_stream_frags(buf, n, L, args.seed, k0=rank, kstep=world)  # shard k = rank (mod world)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
+    if args.desc:
+        descs = dv.make_descs(buf, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint64))
+        run = lambda: dv.frag_csum_batch(descs, mode=mode, out=out)  # noqa: E731
+    else:
+        run = lambda: dv.msg_csum(buf, L, mode=mode, out=out)  # noqa: E731
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        dv.msg_csum(buf, L, mode=mode, out=out)
+        run()
     torch.cuda.synchronize()
 
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
@@ -179,7 +187,7 @@ def run_device(args):
     t0 = time.perf_counter()
     evs[0].record(stream)
     for i in range(args.steps):
-        dv.msg_csum(buf, L, mode=mode, out=out)
+        run()
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     barrier(world)
@@ -245,7 +253,10 @@ def run_device(args):
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
-                "kernel": "crc_regular_kernel" if mode == dv.CRC32 else "crc_regular_kernel (kSum: uicsum on the same schedule)",
+                "kernel": ("crc_frags_kernel (descriptors)" if args.desc and mode == dv.CRC32 else
+                           "sum_rows_kernel (descriptors)" if args.desc else
+                           "crc_regular_kernel" if mode == dv.CRC32 else
+                           "crc_regular_kernel (kSum: uicsum on the same schedule)"),
                 "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                 "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2], max(kern_ms))],
                 "algorithmic_bytes_per_launch": n * L,

@@ -782,16 +782,16 @@ __device__ __forceinline__ void finish_frag_row(const FragGeom &g, uint32_t r, i
 }
 
 // Work split: a workgroup owns kFragsPerWg consecutive fragments; every wave reads all their
-// descriptors (lane j <-> fragment j), and the fragments are cut into four contiguous runs of
-// about equal cost, one per wave (Zipf-sized batches: interleaving fragments over the waves
-// left the slowest wave of a workgroup 24% above the mean).
+// descriptors, and the fragments are cut into contiguous runs of about equal cost (Zipf-sized
+// batches: interleaving fragments over the waves left the slowest wave of a workgroup 24% above
+// the mean; interleaving reads uniform 4 KiB batches 3 points faster but costs config C 5).
 //
 // Small fragments go in lane groups ("packs"): a fragment of 16..1024 bytes, a multiple of 16
 // and 16-byte aligned, is checksummed by 16 lanes as one 1 KiB row (right-aligned frame,
 // P = 1024 - len), four fragments per row.  Group lane g's combine shift, 64*(15-g) bytes, is
 // lane 48+g's table (lanes g and g+16 share a bank: 2-way); the group XOR is the 16-lane DPP
 // row reduction.  A 64-byte fragment then costs a quarter row of lookups instead of a row.
-constexpr uint32_t kFragsPerWg = 64;
+constexpr uint32_t kFragsPerWg = 128;
 constexpr uint32_t kPackBytes = 1024;
 
 __device__ __forceinline__ bool pack_ok(uint32_t len, uint64_t addr) {
@@ -812,7 +812,28 @@ __device__ __forceinline__ RowAddrs pack_row_addrs(gbyte *addr, uint32_t len, ui
     return a;
 }
 
-template <class Src, int kD = 4>
+// Two chains per wave: the workgroup's 128 fragments are two halves of 64 (one descriptor of
+// each per lane), each cut into four runs of about equal cost; wave w walks run w of both halves
+// side by side, one row of each per step, so the two dependent lookup chains interleave (as the
+// two fragments per step of crc_regular_kernel).  A run that is finished (or empty) gets null
+// tasks: its ring loads read the zero chunk and nothing is processed.
+__device__ __forceinline__ void crc_piece2(const uint32_t *lds, const CrcLane &k, uint32_t &C0, const uint32_t d0[16],
+                                           uint32_t &C1, const uint32_t d1[16]) {
+    uint32_t X0 = C0 ^ d0[0], X1 = C1 ^ d1[0];
+#pragma unroll
+    for (int w = 0; w < 15; ++w) {
+        const Look4 t0 = look4(lds, k, X0);
+        const Look4 t1 = look4(lds, k, X1);
+        X0 = xor3(xor3(t0.t0, t0.t1, t0.t2), t0.t3, d0[w + 1]);
+        X1 = xor3(xor3(t1.t0, t1.t1, t1.t2), t1.t3, d1[w + 1]);
+    }
+    const Look4 t0 = look4(lds, k, X0);
+    const Look4 t1 = look4(lds, k, X1);
+    C0 = xor3(t0.t0, t0.t1, t0.t2) ^ t0.t3;
+    C1 = xor3(t1.t0, t1.t1, t1.t2) ^ t1.t3;
+}
+
+template <class Src, int kD = 3>
 __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, const uint32_t *__restrict__ img,
                                                            uint32_t *__restrict__ out) {
     static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
@@ -821,48 +842,61 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, co
     const uint32_t wave = threadIdx.x >> 6;
     const size_t base = (size_t)blockIdx.x * kFragsPerWg;
     const uint32_t nwg = (uint32_t)min((size_t)kFragsPerWg, n - base);
-    const size_t fl = base + (size_t)lane;
-    FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
-    if ((uint32_t)lane < nwg) mine = src.get(fl);
+    // lane j holds fragments base + j (half 0) and base + 64 + j (half 1); chain c walks half c
+    FragInfo mine0{nullptr, 0u, 0u, nullptr, 0u}, mine1{nullptr, 0u, 0u, nullptr, 0u};
+    if ((uint32_t)lane < nwg) mine0 = src.get(base + (size_t)lane);
+    if ((uint32_t)lane + 64u < nwg) mine1 = src.get(base + 64 + (size_t)lane);
     stage_tables<0>(lds, img, [] {});  // waits for the descriptors too
-    if (wave == 0 && (uint32_t)lane < nwg && mine.len == 0) out[fl] = mine.partial;  // uicrc(p, 0, s) == s
-    const uint64_t myA = (uint64_t)(uintptr_t)mine.addr;
-    const bool myPack = (uint32_t)lane < nwg && pack_ok(mine.len, myA);
-    const uint32_t myR = (mine.len + (kRowBytes - 1)) / kRowBytes;
-    // exclusive prefix of the costs (quarter rows: a pack member 1, a fragment 4 per row)
-    const uint32_t myCost = myPack ? 1u : 4u * myR;
-    uint32_t incl = myCost;
+    if (wave == 0 && (uint32_t)lane < nwg && mine0.len == 0) out[base + lane] = mine0.partial;  // uicrc(p, 0, s) == s
+    if (wave == 1 && (uint32_t)lane + 64u < nwg && mine1.len == 0) out[base + 64 + lane] = mine1.partial;
+    const uint64_t myA0 = (uint64_t)(uintptr_t)mine0.addr, myA1 = (uint64_t)(uintptr_t)mine1.addr;
+    const bool myPack0 = (uint32_t)lane < nwg && pack_ok(mine0.len, myA0);
+    const bool myPack1 = (uint32_t)lane + 64u < nwg && pack_ok(mine1.len, myA1);
+    const uint32_t myR0 = (mine0.len + (kRowBytes - 1)) / kRowBytes, myR1 = (mine1.len + (kRowBytes - 1)) / kRowBytes;
+    // per half: exclusive prefix of the costs (quarter rows: a pack member 1, a fragment 4 per
+    // row), cut into four runs of about equal cost, one per wave
+    auto owner = [&](uint32_t cost) -> uint32_t {
+        uint32_t incl = cost;
 #pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-        const uint32_t v = (uint32_t)__shfl_up((int)incl, s, 64);
-        if (lane >= s) incl += v;
-    }
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    const uint32_t start = incl - myCost;
-    const uint32_t owner = total ? min(3u, (uint32_t)(((uint64_t)start * kWaves) / total)) : 0u;
-    const uint64_t mineAll = __ballot((uint32_t)lane < nwg && mine.len != 0 && owner == wave);
-    if (mineAll == 0) return;
-    const uint64_t qall = mineAll & __ballot(myPack);  // pack members, in index order
-    const uint64_t todo = mineAll & ~qall;             // fragments in whole 4 KiB rows
-    const uint32_t myP = myR * kRowBytes - mine.len;
-    const uint32_t myS = (uint32_t)(((uintptr_t)mine.addr - myP) & 15u);
+        for (int s = 1; s < 64; s <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, s, 64);
+            if (lane >= s) incl += v;
+        }
+        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        return total ? min(3u, (uint32_t)(((uint64_t)(incl - cost) * kWaves) / total)) : 0u;
+    };
+    const uint32_t own0 = owner(myPack0 ? 1u : 4u * myR0), own1 = owner(myPack1 ? 1u : 4u * myR1);
+    const uint64_t set0 = __ballot((uint32_t)lane < nwg && mine0.len != 0 && own0 == wave);
+    const uint64_t set1 = __ballot((uint32_t)lane + 64u < nwg && mine1.len != 0 && own1 == wave);
+    if ((set0 | set1) == 0) return;
+    const uint64_t packs0 = __ballot(myPack0), packs1 = __ballot(myPack1);
+    const uint32_t myP0 = myR0 * kRowBytes - mine0.len, myP1 = myR1 * kRowBytes - mine1.len;
+    const uint32_t myS0 = (uint32_t)(((uintptr_t)mine0.addr - myP0) & 15u);
+    const uint32_t myS1 = (uint32_t)(((uintptr_t)mine1.addr - myP1) & 15u);
 
     struct Task {
-        uint32_t pk;  // 1: a pack of up to four members (qm), 0: row r of fragment j
+        uint32_t kind;  // 0: row r of fragment j, 1: a pack of up to four members (qm), 2: null
+        uint32_t h;     // half (= chain)
         uint64_t qm;
         uint32_t j, r;
         FragGeom g;
     };
-    auto geom = [&](uint32_t j) -> FragGeom {
+    struct Seq {
+        uint32_t h;
+        uint64_t qall, todo;  // pack members, fragments in whole rows (packs go first)
+    };
+    const Seq sq[2] = {{0u, set0 & packs0, set0 & ~packs0}, {1u, set1 & packs1, set1 & ~packs1}};
+    auto geom = [&](uint32_t h, uint32_t j) -> FragGeom {
         FragGeom g;
-        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)myA, j);
-        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(myA >> 32), j);
+        const uint64_t a = h ? myA1 : myA0;
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)a, j);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(a >> 32), j);
         g.addr = (gbyte *)(uintptr_t)(((uint64_t)hi << 32) | lo);
-        g.len = __builtin_amdgcn_readlane(mine.len, j);
-        g.partial = __builtin_amdgcn_readlane(mine.partial, j);
-        g.R = __builtin_amdgcn_readlane(myR, j);
-        g.P = __builtin_amdgcn_readlane(myP, j);
-        g.s16 = __builtin_amdgcn_readlane(myS, j);
+        g.len = __builtin_amdgcn_readlane(h ? mine1.len : mine0.len, j);
+        g.partial = __builtin_amdgcn_readlane(h ? mine1.partial : mine0.partial, j);
+        g.R = __builtin_amdgcn_readlane(h ? myR1 : myR0, j);
+        g.P = __builtin_amdgcn_readlane(h ? myP1 : myP0, j);
+        g.s16 = __builtin_amdgcn_readlane(h ? myS1 : myS0, j);
         return g;
     };
     auto above = [](uint64_t set, uint32_t j) -> uint64_t {  // members of set after bit j
@@ -878,28 +912,24 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, co
         }
         return pm;
     };
-    auto first_row = [&]() -> Task {
-        const uint32_t j0 = (uint32_t)__builtin_ctzll(todo);
-        return Task{0u, 0ull, j0, 0u, geom(j0)};
+    const Task null_task{2u, 0u, 0ull, 0u, 0u, FragGeom{}};
+    auto row_task = [&](uint32_t h, uint32_t j) -> Task { return Task{0u, h, 0ull, j, 0u, geom(h, j)}; };
+    auto first_task = [&](const Seq &s) -> Task {
+        if (s.qall) return Task{1u, s.h, first4(s.qall), 0u, 0u, FragGeom{}};
+        if (s.todo) return row_task(s.h, (uint32_t)__builtin_ctzll(s.todo));
+        return null_task;
     };
-    const uint64_t last_pack = qall ? (1ull << (63 - __builtin_clzll(qall))) : 0ull;
-    const uint32_t jlast = todo ? 63u - (uint32_t)__builtin_clzll(todo) : 64u;
-    auto advance = [&](const Task &t) -> Task {
-        if (t.pk) {
-            const uint64_t rest = above(qall, 63u - (uint32_t)__builtin_clzll(t.qm));
-            if (rest) return Task{1u, first4(rest), 0u, 0u, t.g};
-            if (todo) return first_row();
-            return t;  // past the end: re-issue the last task (never processed)
+    auto advance = [&](const Seq &s, const Task &t) -> Task {
+        if (t.kind == 2u) return t;
+        if (t.kind == 1u) {
+            const uint64_t rest = above(s.qall, 63u - (uint32_t)__builtin_clzll(t.qm));
+            if (rest) return Task{1u, s.h, first4(rest), 0u, 0u, FragGeom{}};
+            if (s.todo) return row_task(s.h, (uint32_t)__builtin_ctzll(s.todo));
+            return null_task;
         }
-        if (t.r + 1 < t.g.R) return Task{0u, 0ull, t.j, t.r + 1, t.g};
-        const uint64_t rest = above(todo, t.j);
-        if (!rest) return t;
-        const uint32_t nj = (uint32_t)__builtin_ctzll(rest);
-        return Task{0u, 0ull, nj, 0u, geom(nj)};
-    };
-    auto is_last = [&](const Task &t) -> bool {
-        if (todo) return !t.pk && t.j == jlast && t.r + 1 >= t.g.R;
-        return t.pk && (t.qm & last_pack) != 0;
+        if (t.r + 1 < t.g.R) return Task{0u, t.h, 0ull, t.j, t.r + 1, t.g};
+        const uint64_t rest = above(s.todo, t.j);
+        return rest ? row_task(s.h, (uint32_t)__builtin_ctzll(rest)) : null_task;
     };
 
     // this lane's pack member: the (lane >> 4)-th lowest bit of qm (none: j = 64, len 0)
@@ -907,7 +937,7 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, co
         uint32_t j, len, partial;
         gbyte *addr;
     };
-    auto member = [&](uint64_t qm) -> Member {
+    auto member = [&](uint32_t h, uint64_t qm) -> Member {
         uint32_t js[4];
         uint64_t m = qm;
 #pragma unroll
@@ -918,101 +948,145 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, co
         Member p;
         p.j = sel4((uint32_t)lane >> 4, js[0], js[1], js[2], js[3]);
         const int srcl = (int)(p.j & 63u);
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)myA, srcl, 64);
-        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(myA >> 32), srcl, 64);
-        p.addr = (gbyte *)(uintptr_t)(((uint64_t)hi << 32) | lo);
         // every lane takes part in the shuffles (a shuffle inside a lane-divergent condition
         // reads 0 from source lanes that are switched off)
-        const uint32_t len = (uint32_t)__shfl((int)mine.len, srcl, 64);
+        const uint64_t a = h ? myA1 : myA0;
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)a, srcl, 64);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(a >> 32), srcl, 64);
+        const uint32_t len = (uint32_t)__shfl((int)(h ? mine1.len : mine0.len), srcl, 64);
+        p.addr = (gbyte *)(uintptr_t)(((uint64_t)hi << 32) | lo);
         p.len = p.j < 64 ? len : 0u;
-        p.partial = (uint32_t)__shfl((int)mine.partial, srcl, 64);
+        p.partial = (uint32_t)__shfl((int)(h ? mine1.partial : mine0.partial), srcl, 64);
         return p;
     };
     gbyte *zero = (gbyte *)(img + kImgZero);
-    auto issue = [&](const Task &t, RawRow &raw) {
+    auto addrs = [&](const Task &t) -> RowAddrs {
         RowAddrs a;
-        if (t.pk) {
-            const Member p = member(t.qm);
+        if (t.kind == 1u) {
+            const Member p = member(t.h, t.qm);
             a = pack_row_addrs(p.addr, p.len, (uint32_t)lane & 15u, zero);
-        } else {
+        } else if (t.kind == 0u) {
             a = frag_row_addrs(t.g, t.r, lane, zero);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) a.p[q] = zero;
         }
-        issue_row5(a, raw);
+        return a;
     };
 
-    Task t[kD];
-    RawRow ring[kD];
-    t[0] = qall ? Task{1u, first4(qall), 0u, 0u, FragGeom{}} : first_row();
+    Task t[kD][2];
+    RawRow ring[kD][2];
 #pragma unroll
-    for (int q = 1; q < kD; ++q) t[q] = advance(t[q - 1]);
+    for (int c = 0; c < 2; ++c) {
+        t[0][c] = first_task(sq[c]);
 #pragma unroll
-    for (int q = 0; q < kD; ++q) issue(t[q], ring[q]);
+        for (int q = 1; q < kD; ++q) t[q][c] = advance(sq[c], t[q - 1][c]);
+    }
+#pragma unroll
+    for (int q = 0; q < kD; ++q) {
+        const RowAddrs a0 = addrs(t[q][0]), a1 = addrs(t[q][1]);
+        issue_row5(a0, ring[q][0]);
+        issue_row5(a1, ring[q][1]);
+    }
 
     const CrcLane k = make_lane(lane);
-    uint32_t C = 0;
-    auto process_pack = [&](const RawRow &raw, const Task &tk) {
-        const Member p = member(tk.qm);
-        uint32_t d[16];
+    uint32_t C[2] = {0u, 0u};  // registers of the chains' current multi-row fragments
+    // data and starting register of a task's row (pack rows: the group's own frame)
+    auto prepare = [&](const RawRow &raw, const Task &tk, uint32_t &c0, uint32_t d[16]) {
+        if (tk.kind == 1u) {
+            const Member p = member(tk.h, tk.qm);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            d[4 * q + 0] = raw.q[q].x;
-            d[4 * q + 1] = raw.q[q].y;
-            d[4 * q + 2] = raw.q[q].z;
-            d[4 * q + 3] = raw.q[q].w;
-        }
-        const uint32_t g = (uint32_t)lane & 15u, P = kPackBytes - p.len;
-        uint32_t c;
-        if ((P & 63u) == 0) {
-            c = (g == (P >> 6)) ? __builtin_bswap32(p.partial) : 0u;
-        } else {
-            c = 0;
-            RowGeom rg{1u, P, 0u};
-            crc_inject(d, rg, p.partial, (int)g);
-        }
-        c = crc_piece(lds, k, c, d);
-        CrcLane kq = k;
-        kq.comb_base = 448u + 4u * g;  // lane 48 + g's combine column: shift by 64*(15-g)
-        const uint32_t x = row16_xor(lane_combine(lds, kq, c));
-        if (g == 0 && p.j < 64) out[base + p.j] = __builtin_bswap32(x);
-    };
-    auto process = [&](const RawRow &raw, const Task &tk) {
-        if (tk.pk) {
-            process_pack(raw, tk);
+            for (int q = 0; q < 4; ++q) {
+                d[4 * q + 0] = raw.q[q].x;
+                d[4 * q + 1] = raw.q[q].y;
+                d[4 * q + 2] = raw.q[q].z;
+                d[4 * q + 3] = raw.q[q].w;
+            }
+            const uint32_t g = (uint32_t)lane & 15u, P = kPackBytes - p.len;
+            if ((P & 63u) == 0) {
+                c0 = (g == (P >> 6)) ? __builtin_bswap32(p.partial) : 0u;
+            } else {
+                c0 = 0;
+                RowGeom rg{1u, P, 0u};
+                crc_inject(d, rg, p.partial, (int)g);
+            }
             return;
         }
-        uint32_t d[16];
         finish_frag_row(tk.g, tk.r, lane, raw, d);
         if (tk.r == 0) {
             if ((tk.g.P & 63u) == 0) {  // the register enters as lane P/64's starting value
-                C = ((uint32_t)lane == (tk.g.P >> 6)) ? __builtin_bswap32(tk.g.partial) : 0u;
+                c0 = ((uint32_t)lane == (tk.g.P >> 6)) ? __builtin_bswap32(tk.g.partial) : 0u;
             } else {
-                C = 0;
+                c0 = 0;
                 RowGeom rg{tk.g.R, tk.g.P, tk.g.s16};
                 crc_inject(d, rg, tk.g.partial, lane);
             }
         } else {
-            C = horner_shift(lds, C);
+            c0 = horner_shift(lds, c0);
             if (tk.r == 1 && tk.g.P > (uint32_t)kRowBytes - 4 && lane == 0)  // register bytes spill into row 1
                 d[0] ^= __builtin_bswap32(tk.g.partial) >> (8 * (kRowBytes - tk.g.P));
         }
-        C = crc_piece(lds, k, C, d);
-        if (tk.r + 1 == tk.g.R) {
-            const uint32_t x = wave_xor(lane_combine(lds, k, C));
+    };
+    auto finish = [&](const Task &tk, uint32_t c) {
+        if (tk.kind == 1u) {
+            const Member p = member(tk.h, tk.qm);
+            const uint32_t g = (uint32_t)lane & 15u;
+            CrcLane kq = k;
+            kq.comb_base = 448u + 4u * g;  // lane 48 + g's combine column: shift by 64*(15-g)
+            const uint32_t x = row16_xor(lane_combine(lds, kq, c));
+            if (g == 0 && p.j < 64) out[base + 64 * tk.h + p.j] = __builtin_bswap32(x);
+        } else if (tk.r + 1 == tk.g.R) {
+            const uint32_t x = wave_xor(lane_combine(lds, k, c));
             if (lane == 0) {
                 uint32_t res = __builtin_bswap32(x);
                 if (tk.g.len < 4) res ^= tk.g.partial << (8 * tk.g.len);
-                out[base + tk.j] = res;
+                out[base + 64 * tk.h + tk.j] = res;
             }
         }
     };
-    constexpr int kL = 5;  // loads per row
-#define LAMPI_FRAG_STEP(S)                                           \
-    if constexpr ((S) < kD) {                                        \
-        wait_raw<(kD - 1) * kL>(ring[(S) % kD]);                     \
-        process(ring[(S) % kD], t[(S) % kD]);                        \
-        if (is_last(t[(S) % kD])) break;                             \
-        t[(S) % kD] = advance(t[((S) + kD - 1) % kD]);               \
-        issue(t[(S) % kD], ring[(S) % kD]);                          \
+    auto process = [&](RawRow (&raw)[2], const Task (&tk)[2]) {
+        uint32_t d0[16], d1[16];
+        uint32_t c0 = C[0], c1 = C[1];
+        if (tk[0].kind != 2u) {
+            prepare(raw[0], tk[0], c0, d0);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 16; ++w) d0[w] = 0u;
+        }
+        if (tk[1].kind != 2u) {
+            prepare(raw[1], tk[1], c1, d1);
+        } else {
+#pragma unroll
+            for (int w = 0; w < 16; ++w) d1[w] = 0u;
+        }
+        crc_piece2(lds, k, c0, d0, c1, d1);  // a null chain computes garbage, never used
+        if (tk[0].kind == 0u) C[0] = c0;
+        if (tk[1].kind == 0u) C[1] = c1;
+        if (tk[0].kind != 2u) finish(tk[0], c0);
+        if (tk[1].kind != 2u) finish(tk[1], c1);
+    };
+    constexpr int kL = 10;  // loads per step (two rows)
+#define LAMPI_FRAG_STEP(S)                                                            \
+    if constexpr ((S) < kD) {                                                         \
+        asm volatile("s_waitcnt vmcnt(%10)"                                           \
+                     : "+v"(ring[(S) % kD][0].q[0]), "+v"(ring[(S) % kD][0].q[1]),    \
+                       "+v"(ring[(S) % kD][0].q[2]), "+v"(ring[(S) % kD][0].q[3]),    \
+                       "+v"(ring[(S) % kD][0].q[4]), "+v"(ring[(S) % kD][1].q[0]),    \
+                       "+v"(ring[(S) % kD][1].q[1]), "+v"(ring[(S) % kD][1].q[2]),    \
+                       "+v"(ring[(S) % kD][1].q[3]), "+v"(ring[(S) % kD][1].q[4])     \
+                     : "n"((kD - 1) * kL)                                             \
+                     : "memory");                                                     \
+        if (t[(S) % kD][0].kind == 2u && t[(S) % kD][1].kind == 2u) break;            \
+        process(ring[(S) % kD], t[(S) % kD]);                                         \
+        {                                                                             \
+            const Task n0 = advance(sq[0], t[((S) + kD - 1) % kD][0]);                \
+            const Task n1 = advance(sq[1], t[((S) + kD - 1) % kD][1]);                \
+            t[(S) % kD][0] = n0;                                                      \
+            t[(S) % kD][1] = n1;                                                      \
+            const RowAddrs a0 = addrs(n0), a1 = addrs(n1);                            \
+            issue_row5(a0, ring[(S) % kD][0]);                                        \
+            issue_row5(a1, ring[(S) % kD][1]);                                        \
+        }                                                                             \
     }
     for (;;) {
         LAMPI_FRAG_STEP(0)
@@ -1023,7 +1097,7 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, co
         LAMPI_FRAG_STEP(5)
     }
 #undef LAMPI_FRAG_STEP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the re-issued rows before exit
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the rows in flight before exit
 }
 
 // ---- CRC fast path: regular batches -------------------------------------------------------

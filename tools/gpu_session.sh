@@ -37,8 +37,8 @@ for step in "$@"; do
             -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline &&
          run pmc_ea 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv \
             -d gpurun_out/pmc_ea -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
-    pmcsq) for cfg in B C; do
-             extra="--no-cpu-baseline"; [ $cfg = C ] && extra="--config C"
+    pmcsq) for cfg in B C D; do
+             extra="--no-cpu-baseline"; [ $cfg = C ] && extra="--config C"; [ $cfg = D ] && extra="--desc --no-cpu-baseline"
              run pmc_sq$cfg 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
                  SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv \
                  -d gpurun_out/pmc_sq$cfg -o run -- python3 bench.py --steps 3 --warmup 1 $extra
