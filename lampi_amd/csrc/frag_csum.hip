@@ -834,14 +834,15 @@ __device__ __forceinline__ void crc_piece2(const uint32_t *lds, const CrcLane &k
 }
 
 template <class Src, int kD = 3>
-__global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, const uint32_t *__restrict__ img,
+__global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, uint32_t fpg,
+                                                           const uint32_t *__restrict__ img,
                                                            uint32_t *__restrict__ out) {
     static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
-    const size_t base = (size_t)blockIdx.x * kFragsPerWg;
-    const uint32_t nwg = (uint32_t)min((size_t)kFragsPerWg, n - base);
+    const size_t base = (size_t)blockIdx.x * fpg;  // fpg <= kFragsPerWg fragments per workgroup
+    const uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
     // lane j holds fragments base + j (half 0) and base + 64 + j (half 1); chain c walks half c
     FragInfo mine0{nullptr, 0u, 0u, nullptr, 0u}, mine1{nullptr, 0u, 0u, nullptr, 0u};
     if ((uint32_t)lane < nwg) mine0 = src.get(base + (size_t)lane);
@@ -1911,7 +1912,16 @@ static uint32_t pick_fpw(size_t n, uint32_t R) {
 
 constexpr int kRegularChains = 2;
 
-static dim3 frags_grid(size_t n) { return dim3((unsigned)((n + kFragsPerWg - 1) / kFragsPerWg)); }
+// fragments per workgroup of crc_frags_kernel: 128, halved for small batches so that they still
+// spread over the chip (a 16 MiB chunk of 65,456-byte fragments is 256 fragments: 64
+// workgroups of four, one fragment per wave)
+static uint32_t frags_per_wg(size_t n) {
+    uint32_t fpg = kFragsPerWg;
+    while (fpg > 4 && n / fpg < 2048) fpg >>= 1;
+    return fpg;
+}
+
+static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg - 1) / fpg)); }
 
 static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size_t)kWaves * fpw - 1) / ((size_t)kWaves * fpw))); }
 
@@ -1919,7 +1929,9 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
                            hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(crc_frags_kernel<DescSource>, frags_grid(n), dim3(kBlock), 0, s, DescSource{d}, n, img, out);
+    const uint32_t fpg = frags_per_wg(n);
+    hipLaunchKernelGGL(crc_frags_kernel<DescSource>, frags_grid(n, fpg), dim3(kBlock), 0, s, DescSource{d}, n, fpg, img,
+                       out);
     return hipGetLastError();
 }
 
@@ -1927,8 +1939,9 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(crc_frags_kernel<MsgSource>, frags_grid(n), dim3(kBlock), 0, s,
-                       MsgSource{base, msg_len, frag_len, partial}, n, img, out);
+    const uint32_t fpg = frags_per_wg(n);
+    hipLaunchKernelGGL(crc_frags_kernel<MsgSource>, frags_grid(n, fpg), dim3(kBlock), 0, s,
+                       MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
     return hipGetLastError();
 }
 

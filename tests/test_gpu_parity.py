@@ -131,10 +131,12 @@ def test_descriptor_batch_random(cuda, oracle):
         assert np.array_equal(got, want)
 
 
-def test_descriptor_batch_small_fragment_packs(cuda, oracle):
+@pytest.mark.parametrize("n", [30000, 300000])
+def test_descriptor_batch_small_fragment_packs(cuda, oracle, n):
     """Fragments of 16..1024 bytes (multiples of 16, 16-byte aligned) go four to a row in lane
     groups; mixed with unaligned, odd-length, empty and multi-row fragments in one batch, every
-    register random, so packs, partial packs and whole-row fragments interleave in every wave."""
+    register random, so packs, partial packs and whole-row fragments interleave in every wave.
+    30,000 runs with 8 fragments per workgroup, 300,000 with the full 128 (frags_per_wg)."""
     import torch
 
     dv = _dv()
@@ -142,7 +144,6 @@ def test_descriptor_batch_small_fragment_packs(cuda, oracle):
     base = torch.empty(32 << 20, dtype=torch.uint8, device=cuda)
     dv.fill_stream(base, seed=44)
     host = base.cpu().numpy()
-    n = 30000
     kind = rng.integers(0, 10, size=n)
     lens = np.where(kind < 6, 16 * rng.integers(1, 65, size=n),            # pack members
                     np.where(kind < 8, rng.integers(1, 1100, size=n),       # small, any length
