@@ -108,6 +108,14 @@ typedef struct lampi_frag_desc {
 int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out,
                           int mode, void *stream);
 
+/* As lampi_frag_csum_batch, with checksum i written to (char *)d_out + i*out_stride (d_out and
+ * out_stride 4-byte aligned, out_stride >= 4) -- e.g. straight into the dataChecksum field of
+ * an array of 72-byte gmHeaderData records: d_out = hdrs + 64, out_stride = 72
+ * (src/path/gm/header.h:56-70; the send side stores it at gm/sendFrag.cc:147-155).  Other
+ * bytes of the records are not touched.  Uses 4 * n bytes of stream-ordered scratch. */
+int lampi_frag_csum_batch_strided(const lampi_frag_desc *d_descs, size_t n, void *d_out, size_t out_stride,
+                                  int mode, void *stream);
+
 /* out[i] = csum (64-bit words, fresh state) of fragment d[i]; d[i].partial is ignored. */
 int lampi_frag_csum64_batch(const lampi_frag_desc *d_descs, size_t n, uint64_t *d_out, void *stream);
 

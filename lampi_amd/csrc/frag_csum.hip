@@ -1599,6 +1599,14 @@ __global__ void __launch_bounds__(256) check_data_kernel(const uint32_t *__restr
     emit_mask(i, n, bad, mask, nbad);
 }
 
+// Checksums into records: dst + i*stride gets vals[i] (e.g. gmHeaderData.dataChecksum @64 of a
+// 72-byte header array, SURVEY.md 8(b) optional strided output).
+__global__ void __launch_bounds__(256) scatter_u32_kernel(const uint32_t *__restrict__ vals, uint32_t n, uint8_t *dst,
+                                                          size_t stride) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) *(uint32_t *)(dst + (size_t)i * stride) = vals[i];
+}
+
 // ---- chained checksums over typemap pieces ------------------------------------------------
 // Fragment f = pieces first[f] .. first[f+1]-1 concatenated (ref src/path/gm/sendFrag.cc:157-217,
 // src/path/common/BaseDesc.cc:72-163).  Pass 1 (SUM only): byte phase of every piece.  Pass 2:
@@ -2100,6 +2108,13 @@ hipError_t launch_check_data(const uint32_t *calc, const uint8_t *expected, size
     if (e != hipSuccess || n == 0) return e;
     hipLaunchKernelGGL(check_data_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, calc, expected,
                        exp_stride, lengths, len_stride, (uint32_t)n, mask, nbad);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_u32(const uint32_t *vals, size_t n, uint8_t *dst, size_t stride, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(scatter_u32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, vals, (uint32_t)n, dst,
+                       stride);
     return hipGetLastError();
 }
 

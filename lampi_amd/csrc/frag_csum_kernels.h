@@ -35,6 +35,8 @@ hipError_t launch_header_check(const uint8_t *hdrs, size_t n, size_t stride, uin
                                hipStream_t s);
 hipError_t launch_check_data(const uint32_t *calc, const uint8_t *expected, size_t exp_stride, const uint8_t *lengths,
                              size_t len_stride, size_t n, uint32_t *mask, uint32_t *nbad, hipStream_t s);
+// dst + i*stride = vals[i] (4-byte aligned records).
+hipError_t launch_scatter_u32(const uint32_t *vals, size_t n, uint8_t *dst, size_t stride, hipStream_t s);
 // Chained checksums over typemap pieces; vals / phase: npieces words of scratch each.
 hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t *first, size_t nfrags, uint32_t *out,
                         int mode, const uint32_t *img, uint32_t *vals, uint32_t *phase, hipStream_t s);

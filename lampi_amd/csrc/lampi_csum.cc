@@ -347,6 +347,23 @@ int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_
     return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s));
 }
 
+int lampi_frag_csum_batch_strided(const lampi_frag_desc *d_descs, size_t n, void *d_out, size_t out_stride, int mode,
+                                  void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (n == 0) return 0;
+    if (!d_descs || !d_out || ((uintptr_t)d_out & 3u) || (out_stride & 3u) || out_stride < 4 || n > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
+    if (out_stride == 4) return lampi_frag_csum_batch(d_descs, n, (uint32_t *)d_out, mode, stream);
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t *vals = nullptr;
+    hipError_t e = hipMallocAsync((void **)&vals, n * sizeof(uint32_t), s);
+    if (e != hipSuccess) return to_int(e);
+    int r = lampi_frag_csum_batch(d_descs, n, vals, mode, stream);
+    if (r == 0) r = to_int(launch_scatter_u32(vals, n, (uint8_t *)d_out, out_stride, s));
+    const hipError_t f = hipFreeAsync(vals, s);
+    return r != 0 ? r : to_int(f);
+}
+
 int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;

@@ -112,6 +112,19 @@ def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32
     return out
 
 
+def frag_csum_batch_strided(descs: torch.Tensor, dst: torch.Tensor, stride: int, offset: int = 0,
+                            n: int | None = None, mode: int = CRC32,
+                            stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Checksum i of the batch written at byte offset + i*stride of ``dst`` (e.g. the
+    dataChecksum field, offset 64, of 72-byte gmHeaderData records); returns ``dst``."""
+    _require_cuda(descs, "descs")
+    count = descs.numel() * descs.element_size() // 16 if n is None else int(n)
+    _records(dst[offset:] if dst.element_size() == 1 else dst.view(torch.uint8)[offset:], count, stride, "dst")
+    check(lib().lampi_frag_csum_batch_strided(descs.data_ptr(), count, dst.data_ptr() + offset, stride, mode,
+                                              _stream_handle(stream)), "lampi_frag_csum_batch_strided")
+    return dst
+
+
 def frag_csum64_batch(descs: torch.Tensor, n: int | None = None, out: torch.Tensor | None = None,
                       stream: torch.cuda.Stream | None = None) -> torch.Tensor:
     """out[i] = 64-bit csum (fresh state) of fragment descs[i] (int64 storage, read as uint64)."""

@@ -132,6 +132,25 @@ def test_receive_pipeline_check_data(cuda, mode):
     assert np.array_equal(np.nonzero(dv.mask_bits(mask, n))[0], np.union1d(bad, zero))
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_checksums_stamped_into_headers(cuda, mode):
+    """lampi_frag_csum_batch_strided writes checksum i into record i's dataChecksum field
+    (gm/sendFrag.cc:147-155 stores it there) and leaves every other byte alone."""
+    dv = _dv()
+    n, payload = 9000, 1976
+    rec, v, stride = _gm_records(cuda, n, payload, seed=74)
+    rng = np.random.default_rng(9)
+    lens = rng.integers(0, payload + 1, size=n).astype(np.uint32)
+    descs = dv.make_descs(rec, np.arange(n, dtype=np.uint64) * stride + HDR, lens)
+    want = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
+    before = v.cpu().numpy().copy()
+    dv.frag_csum_batch_strided(descs, rec, stride, offset=DCSUM_OFF, mode=mode)
+    after = v.cpu().numpy()
+    assert np.array_equal(after[:, DCSUM_OFF:DCSUM_OFF + 4].copy().view("<u4").ravel(), want)
+    before[:, DCSUM_OFF:DCSUM_OFF + 4] = after[:, DCSUM_OFF:DCSUM_OFF + 4]
+    assert np.array_equal(before, after)
+
+
 def test_verify_rejects_misaligned(cuda):
     import torch
 
@@ -142,4 +161,8 @@ def test_verify_rejects_misaligned(cuda):
     assert rc != 0
     rc = lampi_amd.lib().lampi_header_check_batch(buf.data_ptr(), 4, 70, 72, 18, 68, buf.data_ptr(),
                                                   buf.data_ptr() + 64, 0, None)
+    assert rc != 0
+    rc = lampi_amd.lib().lampi_frag_csum_batch_strided(buf.data_ptr(), 4, buf.data_ptr() + 2, 72, 0, None)
+    assert rc != 0
+    rc = lampi_amd.lib().lampi_frag_csum_batch_strided(buf.data_ptr(), 4, buf.data_ptr(), 70, 0, None)
     assert rc != 0
