@@ -544,7 +544,7 @@ struct RowGeom {
 
 __device__ __forceinline__ RowGeom crc_geom(const FragInfo &fi) {
     RowGeom g;
-    g.R = (fi.len + (kRowBytes - 1)) / kRowBytes;
+    g.R = (uint32_t)(((uint64_t)fi.len + (kRowBytes - 1)) / kRowBytes);
     g.P = g.R * kRowBytes - fi.len;
     g.s16 = (uint32_t)(((uintptr_t)fi.addr - g.P) & 15u);
     return g;
@@ -781,17 +781,12 @@ __device__ __forceinline__ void finish_frag_row(const FragGeom &g, uint32_t r, i
     }
 }
 
-// Work split: a workgroup owns kFragsPerWg consecutive fragments; every wave reads all their
-// descriptors, and the fragments are cut into contiguous runs of about equal cost (Zipf-sized
-// batches: interleaving fragments over the waves left the slowest wave of a workgroup 24% above
-// the mean; interleaving reads uniform 4 KiB batches 3 points faster but costs config C 5).
-//
 // Small fragments go in lane groups ("packs"): a fragment of 16..1024 bytes, a multiple of 16
 // and 16-byte aligned, is checksummed by 16 lanes as one 1 KiB row (right-aligned frame,
 // P = 1024 - len), four fragments per row.  Group lane g's combine shift, 64*(15-g) bytes, is
 // lane 48+g's table (lanes g and g+16 share a bank: 2-way); the group XOR is the 16-lane DPP
 // row reduction.  A 64-byte fragment then costs a quarter row of lookups instead of a row.
-constexpr uint32_t kFragsPerWg = 128;
+constexpr uint32_t kFragsPerWg = 256;
 constexpr uint32_t kPackBytes = 1024;
 
 __device__ __forceinline__ bool pack_ok(uint32_t len, uint64_t addr) {
@@ -812,11 +807,9 @@ __device__ __forceinline__ RowAddrs pack_row_addrs(gbyte *addr, uint32_t len, ui
     return a;
 }
 
-// Two chains per wave: the workgroup's 128 fragments are two halves of 64 (one descriptor of
-// each per lane), each cut into four runs of about equal cost; wave w walks run w of both halves
-// side by side, one row of each per step, so the two dependent lookup chains interleave (as the
-// two fragments per step of crc_regular_kernel).  A run that is finished (or empty) gets null
-// tasks: its ring loads read the zero chunk and nothing is processed.
+// Two chains per wave, one row of each per step, so the two dependent lookup chains interleave
+// (as the two fragments per step of crc_regular_kernel).  A chain that is finished (or empty)
+// gets null tasks: its ring loads read the zero chunk and nothing is processed.
 __device__ __forceinline__ void crc_piece2(const uint32_t *lds, const CrcLane &k, uint32_t &C0, const uint32_t d0[16],
                                            uint32_t &C1, const uint32_t d1[16]) {
     uint32_t X0 = C0 ^ d0[0], X1 = C1 ^ d1[0];
@@ -833,141 +826,190 @@ __device__ __forceinline__ void crc_piece2(const uint32_t *lds, const CrcLane &k
     C1 = xor3(t1.t0, t1.t1, t1.t2) ^ t1.t3;
 }
 
-template <class Src, int kD = 3>
+// Work split (per workgroup of up to kFragsPerWg consecutive fragments): thread t reads
+// descriptor t into LDS and takes its cost (quarter rows: a pack member 1, a fragment 4 per
+// row, an empty fragment 0 -- answered at once); a block-wide prefix of the costs cuts the
+// fragments into 2 x kWaves contiguous runs of about equal cost (midpoint rule), one per chain:
+// wave w runs chains 2w and 2w+1.  Two LDS lists (pack members in order, whole-row fragments in
+// order) turn a run into a slice of each; a chain walks its pack rows (four members each), then
+// its fragments' rows.  Eight runs over the whole workgroup balance Zipf-sized batches to ~1.15x
+// the ideal chain length, against ~1.33x for four runs per half.
+// kAbl (tools/microbench/frags_ablation.hip only): 1 = loads and task walk, no row work;
+// 2 = everything but the table lookups
+template <class Src, int kD = 3, int kAbl = 0>
 __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, uint32_t fpg,
                                                            const uint32_t *__restrict__ img,
                                                            uint32_t *__restrict__ out) {
     static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
+    static_assert(kFragsPerWg == kBlock, "one fragment per thread in the set-up");
+    constexpr uint32_t kChains = 2 * kWaves;
+    struct SDesc {
+        uint64_t addr;
+        uint32_t len, partial;
+    };
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
+    __shared__ SDesc sdesc[kFragsPerWg];
+    __shared__ uint16_t plist[kFragsPerWg], rlist[kFragsPerWg];  // pack members / row fragments, in order
+    __shared__ uint32_t spk[kFragsPerWg + 1], srw[kFragsPerWg + 1];  // exclusive counts of each kind
+    __shared__ uint32_t sown[kFragsPerWg];
+    __shared__ uint32_t bound[kChains + 1];  // run c = fragments [bound[c], bound[c+1])
+    __shared__ uint32_t wsum[kWaves][2];
     const int lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t t = threadIdx.x;
     const size_t base = (size_t)blockIdx.x * fpg;  // fpg <= kFragsPerWg fragments per workgroup
     const uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
-    // lane j holds fragments base + j (half 0) and base + 64 + j (half 1); chain c walks half c
-    FragInfo mine0{nullptr, 0u, 0u, nullptr, 0u}, mine1{nullptr, 0u, 0u, nullptr, 0u};
-    if ((uint32_t)lane < nwg) mine0 = src.get(base + (size_t)lane);
-    if ((uint32_t)lane + 64u < nwg) mine1 = src.get(base + 64 + (size_t)lane);
-    stage_tables<0>(lds, img, [] {});  // waits for the descriptors too
-    if (wave == 0 && (uint32_t)lane < nwg && mine0.len == 0) out[base + lane] = mine0.partial;  // uicrc(p, 0, s) == s
-    if (wave == 1 && (uint32_t)lane + 64u < nwg && mine1.len == 0) out[base + 64 + lane] = mine1.partial;
-    const uint64_t myA0 = (uint64_t)(uintptr_t)mine0.addr, myA1 = (uint64_t)(uintptr_t)mine1.addr;
-    const bool myPack0 = (uint32_t)lane < nwg && pack_ok(mine0.len, myA0);
-    const bool myPack1 = (uint32_t)lane + 64u < nwg && pack_ok(mine1.len, myA1);
-    const uint32_t myR0 = (mine0.len + (kRowBytes - 1)) / kRowBytes, myR1 = (mine1.len + (kRowBytes - 1)) / kRowBytes;
-    // per half: exclusive prefix of the costs (quarter rows: a pack member 1, a fragment 4 per
-    // row), cut into four runs of about equal cost, one per wave
-    auto owner = [&](uint32_t cost) -> uint32_t {
-        uint32_t incl = cost;
-#pragma unroll
-        for (int s = 1; s < 64; s <<= 1) {
-            const uint32_t v = (uint32_t)__shfl_up((int)incl, s, 64);
-            if (lane >= s) incl += v;
-        }
-        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-        return total ? min(3u, (uint32_t)(((uint64_t)(incl - cost) * kWaves) / total)) : 0u;
-    };
-    const uint32_t own0 = owner(myPack0 ? 1u : 4u * myR0), own1 = owner(myPack1 ? 1u : 4u * myR1);
-    const uint64_t set0 = __ballot((uint32_t)lane < nwg && mine0.len != 0 && own0 == wave);
-    const uint64_t set1 = __ballot((uint32_t)lane + 64u < nwg && mine1.len != 0 && own1 == wave);
-    if ((set0 | set1) == 0) return;
-    const uint64_t packs0 = __ballot(myPack0), packs1 = __ballot(myPack1);
-    const uint32_t myP0 = myR0 * kRowBytes - mine0.len, myP1 = myR1 * kRowBytes - mine1.len;
-    const uint32_t myS0 = (uint32_t)(((uintptr_t)mine0.addr - myP0) & 15u);
-    const uint32_t myS1 = (uint32_t)(((uintptr_t)mine1.addr - myP1) & 15u);
 
-    struct Task {
-        uint32_t kind;  // 0: row r of fragment j, 1: a pack of up to four members (qm), 2: null
-        uint32_t h;     // half (= chain)
-        uint64_t qm;
+    FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
+    if (t < nwg) mine = src.get(base + t);
+    stage_tables<0>(lds, img, [] {});  // waits for the descriptors too
+    const uint64_t myA = (uint64_t)(uintptr_t)mine.addr;
+    const bool valid = t < nwg;
+    const bool isPack = valid && pack_ok(mine.len, myA);
+    const bool isRow = valid && !isPack && mine.len != 0;
+    if (valid && mine.len == 0) out[base + t] = mine.partial;  // uicrc(p, 0, s) == s
+    const uint32_t myR = (uint32_t)(((uint64_t)mine.len + (kRowBytes - 1)) / kRowBytes);
+    const uint32_t cost = isPack ? 1u : (isRow ? 4u * myR : 0u);
+    const uint32_t kinds = (isPack ? 1u : 0u) | (isRow ? 0x10000u : 0u);
+    sdesc[t] = SDesc{myA, mine.len, mine.partial};
+    // block-wide exclusive prefixes of the cost and of the two kind counts
+    uint32_t ic = cost, ik = kinds;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t vc = (uint32_t)__shfl_up((int)ic, s, 64);
+        const uint32_t vk = (uint32_t)__shfl_up((int)ik, s, 64);
+        if (lane >= s) {
+            ic += vc;
+            ik += vk;
+        }
+    }
+    if (lane == 63) {
+        wsum[wave][0] = ic;
+        wsum[wave][1] = ik;
+    }
+    __syncthreads();
+    uint32_t oc = 0, ok = 0, total = 0, totk = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < (uint32_t)kWaves; ++w) {
+        const uint32_t a = wsum[w][0], b = wsum[w][1];
+        if (w < wave) {
+            oc += a;
+            ok += b;
+        }
+        total += a;
+        totk += b;
+    }
+    const uint32_t excl = oc + ic - cost, exk = ok + ik - kinds;
+    // run = min(7, floor((excl + cost/2) * 8 / total)): monotonic in t
+    const uint32_t own = total ? min(kChains - 1, (uint32_t)(((2ull * excl + cost) * kChains) / (2ull * total))) : 0u;
+    sown[t] = own;
+    spk[t] = exk & 0xFFFFu;
+    srw[t] = exk >> 16;
+    if (t == 0) {
+        spk[kFragsPerWg] = totk & 0xFFFFu;
+        srw[kFragsPerWg] = totk >> 16;
+    }
+    if (isPack) plist[exk & 0xFFFFu] = (uint16_t)t;
+    if (isRow) rlist[exk >> 16] = (uint16_t)t;
+    __syncthreads();
+    if (valid) {  // t opens runs (own(t-1), own(t)]; the last fragment closes the rest
+        const int prev = t == 0 ? -1 : (int)sown[t - 1];
+        for (int c = prev + 1; c <= (int)own; ++c) bound[c] = t;
+        if (t + 1 == nwg)
+            for (uint32_t c = own + 1; c <= kChains; ++c) bound[c] = nwg;
+    }
+    if (t == 0 && nwg < kFragsPerWg) {  // counts at nwg (the slots past the batch end hold 0)
+        spk[nwg] = totk & 0xFFFFu;
+        srw[nwg] = totk >> 16;
+    }
+    __syncthreads();
+
+    // A chain's tasks: pack rows (members plist[p .. p+3], clamped to pe), then row r of
+    // fragment rlist[q] for q < re.  The issue side and the process side walk the same sequence
+    // kD steps apart (ChainPos + next()), so nothing per ring slot is stored beyond the data.
+    struct ChainPos {
+        uint32_t p, pe, q, re;
+        uint32_t kind;  // 0: row r of fragment j, 1: a pack row, 2: null (chain done)
         uint32_t j, r;
-        FragGeom g;
+        gbyte *addr;    // kind 0: fragment j
+        uint32_t len, partial;
     };
-    struct Seq {
-        uint32_t h;
-        uint64_t qall, todo;  // pack members, fragments in whole rows (packs go first)
-    };
-    const Seq sq[2] = {{0u, set0 & packs0, set0 & ~packs0}, {1u, set1 & packs1, set1 & ~packs1}};
-    auto geom = [&](uint32_t h, uint32_t j) -> FragGeom {
+    auto geom = [](const ChainPos &p) -> FragGeom {  // derived on use (scalar ALU), not carried
         FragGeom g;
-        const uint64_t a = h ? myA1 : myA0;
-        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)a, j);
-        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(a >> 32), j);
-        g.addr = (gbyte *)(uintptr_t)(((uint64_t)hi << 32) | lo);
-        g.len = __builtin_amdgcn_readlane(h ? mine1.len : mine0.len, j);
-        g.partial = __builtin_amdgcn_readlane(h ? mine1.partial : mine0.partial, j);
-        g.R = __builtin_amdgcn_readlane(h ? myR1 : myR0, j);
-        g.P = __builtin_amdgcn_readlane(h ? myP1 : myP0, j);
-        g.s16 = __builtin_amdgcn_readlane(h ? myS1 : myS0, j);
+        g.addr = p.addr;
+        g.len = p.len;
+        g.partial = p.partial;
+        g.R = (uint32_t)(((uint64_t)p.len + (kRowBytes - 1)) / kRowBytes);
+        g.P = g.R * kRowBytes - p.len;
+        g.s16 = (uint32_t)(((uintptr_t)p.addr - g.P) & 15u);
         return g;
     };
-    auto above = [](uint64_t set, uint32_t j) -> uint64_t {  // members of set after bit j
-        return j >= 63 ? 0ull : (set & ~((2ull << j) - 1ull));
-    };
-    auto first4 = [](uint64_t set) -> uint64_t {  // the (up to) four lowest members of set
-        uint64_t pm = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint64_t b = set & (0ull - set);
-            pm |= b;
-            set &= ~b;
+    auto to_rows = [&](ChainPos &p) {
+        if (p.q < p.re) {
+            p.kind = 0u;
+            p.j = __builtin_amdgcn_readfirstlane((uint32_t)rlist[p.q]);
+            const SDesc sd = sdesc[p.j];
+            p.addr = (gbyte *)(uintptr_t)uniform64(sd.addr);
+            p.len = uniform(sd.len);
+            p.partial = uniform(sd.partial);
+            p.r = 0u;
+        } else {
+            p.kind = 2u;
         }
-        return pm;
     };
-    const Task null_task{2u, 0u, 0ull, 0u, 0u, FragGeom{}};
-    auto row_task = [&](uint32_t h, uint32_t j) -> Task { return Task{0u, h, 0ull, j, 0u, geom(h, j)}; };
-    auto first_task = [&](const Seq &s) -> Task {
-        if (s.qall) return Task{1u, s.h, first4(s.qall), 0u, 0u, FragGeom{}};
-        if (s.todo) return row_task(s.h, (uint32_t)__builtin_ctzll(s.todo));
-        return null_task;
-    };
-    auto advance = [&](const Seq &s, const Task &t) -> Task {
-        if (t.kind == 2u) return t;
-        if (t.kind == 1u) {
-            const uint64_t rest = above(s.qall, 63u - (uint32_t)__builtin_clzll(t.qm));
-            if (rest) return Task{1u, s.h, first4(rest), 0u, 0u, FragGeom{}};
-            if (s.todo) return row_task(s.h, (uint32_t)__builtin_ctzll(s.todo));
-            return null_task;
+    auto next = [&](ChainPos &p) {
+        if (p.kind == 2u) return;
+        if (p.kind == 0u) {
+            if ((uint64_t)(p.r + 1) * kRowBytes < p.len) {
+                ++p.r;
+                return;
+            }
+            ++p.q;
+        } else {
+            p.p += 4u;
+            if (p.p < p.pe) return;
         }
-        if (t.r + 1 < t.g.R) return Task{0u, t.h, 0ull, t.j, t.r + 1, t.g};
-        const uint64_t rest = above(s.todo, t.j);
-        return rest ? row_task(s.h, (uint32_t)__builtin_ctzll(rest)) : null_task;
+        to_rows(p);
     };
+    auto start = [&](uint32_t ch) -> ChainPos {
+        const uint32_t b0 = bound[ch], b1 = bound[ch + 1];
+        ChainPos p{spk[b0], spk[b1], srw[b0], srw[b1], 1u, 0u, 0u, nullptr, 0u, 0u};
+        p.p = uniform(p.p);
+        p.pe = uniform(p.pe);
+        p.q = uniform(p.q);
+        p.re = uniform(p.re);
+        if (p.p >= p.pe) to_rows(p);
+        return p;
+    };
+    ChainPos pi[2] = {start(2 * wave), start(2 * wave + 1)};
+    if (pi[0].kind == 2u && pi[1].kind == 2u) return;
+    ChainPos pp[2] = {pi[0], pi[1]};  // process side: the same sequence, kD steps behind
 
-    // this lane's pack member: the (lane >> 4)-th lowest bit of qm (none: j = 64, len 0)
+    // this lane's pack member: plist[p + (lane >> 4)] (none past pe: j = kFragsPerWg, len 0)
     struct Member {
         uint32_t j, len, partial;
         gbyte *addr;
     };
-    auto member = [&](uint32_t h, uint64_t qm) -> Member {
-        uint32_t js[4];
-        uint64_t m = qm;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            js[i] = m ? (uint32_t)__builtin_ctzll(m) : 64u;
-            m &= m - 1ull;
+    auto member = [&](const ChainPos &t) -> Member {
+        const uint32_t i = t.p + ((uint32_t)lane >> 4);
+        Member m{kFragsPerWg, 0u, 0u, nullptr};
+        if (i < t.pe) {
+            m.j = plist[i];
+            const SDesc sd = sdesc[m.j];
+            m.addr = (gbyte *)(uintptr_t)sd.addr;
+            m.len = sd.len;
+            m.partial = sd.partial;
         }
-        Member p;
-        p.j = sel4((uint32_t)lane >> 4, js[0], js[1], js[2], js[3]);
-        const int srcl = (int)(p.j & 63u);
-        // every lane takes part in the shuffles (a shuffle inside a lane-divergent condition
-        // reads 0 from source lanes that are switched off)
-        const uint64_t a = h ? myA1 : myA0;
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)a, srcl, 64);
-        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(a >> 32), srcl, 64);
-        const uint32_t len = (uint32_t)__shfl((int)(h ? mine1.len : mine0.len), srcl, 64);
-        p.addr = (gbyte *)(uintptr_t)(((uint64_t)hi << 32) | lo);
-        p.len = p.j < 64 ? len : 0u;
-        p.partial = (uint32_t)__shfl((int)(h ? mine1.partial : mine0.partial), srcl, 64);
-        return p;
+        return m;
     };
     gbyte *zero = (gbyte *)(img + kImgZero);
-    auto addrs = [&](const Task &t) -> RowAddrs {
+    auto addrs = [&](const ChainPos &t) -> RowAddrs {
         RowAddrs a;
         if (t.kind == 1u) {
-            const Member p = member(t.h, t.qm);
+            const Member p = member(t);
             a = pack_row_addrs(p.addr, p.len, (uint32_t)lane & 15u, zero);
         } else if (t.kind == 0u) {
-            a = frag_row_addrs(t.g, t.r, lane, zero);
+            a = frag_row_addrs(geom(t), t.r, lane, zero);
         } else {
 #pragma unroll
             for (int q = 0; q < 5; ++q) a.p[q] = zero;
@@ -975,17 +1017,14 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, ui
         return a;
     };
 
-    Task t[kD][2];
     RawRow ring[kD][2];
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        t[0][c] = first_task(sq[c]);
-#pragma unroll
-        for (int q = 1; q < kD; ++q) t[q][c] = advance(sq[c], t[q - 1][c]);
-    }
-#pragma unroll
     for (int q = 0; q < kD; ++q) {
-        const RowAddrs a0 = addrs(t[q][0]), a1 = addrs(t[q][1]);
+        if (q > 0) {
+            next(pi[0]);
+            next(pi[1]);
+        }
+        const RowAddrs a0 = addrs(pi[0]), a1 = addrs(pi[1]);
         issue_row5(a0, ring[q][0]);
         issue_row5(a1, ring[q][1]);
     }
@@ -993,9 +1032,9 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, ui
     const CrcLane k = make_lane(lane);
     uint32_t C[2] = {0u, 0u};  // registers of the chains' current multi-row fragments
     // data and starting register of a task's row (pack rows: the group's own frame)
-    auto prepare = [&](const RawRow &raw, const Task &tk, uint32_t &c0, uint32_t d[16]) {
-        if (tk.kind == 1u) {
-            const Member p = member(tk.h, tk.qm);
+    auto prepare = [&](const RawRow &raw, const ChainPos &t, uint32_t &c0, uint32_t d[16]) {
+        if (t.kind == 1u) {
+            const Member p = member(t);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 d[4 * q + 0] = raw.q[q].x;
@@ -1013,58 +1052,75 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, ui
             }
             return;
         }
-        finish_frag_row(tk.g, tk.r, lane, raw, d);
-        if (tk.r == 0) {
-            if ((tk.g.P & 63u) == 0) {  // the register enters as lane P/64's starting value
-                c0 = ((uint32_t)lane == (tk.g.P >> 6)) ? __builtin_bswap32(tk.g.partial) : 0u;
+        const FragGeom g = geom(t);
+        finish_frag_row(g, t.r, lane, raw, d);
+        if (t.r == 0) {
+            if ((g.P & 63u) == 0) {  // the register enters as lane P/64's starting value
+                c0 = ((uint32_t)lane == (g.P >> 6)) ? __builtin_bswap32(g.partial) : 0u;
             } else {
                 c0 = 0;
-                RowGeom rg{tk.g.R, tk.g.P, tk.g.s16};
-                crc_inject(d, rg, tk.g.partial, lane);
+                RowGeom rg{g.R, g.P, g.s16};
+                crc_inject(d, rg, g.partial, lane);
             }
         } else {
             c0 = horner_shift(lds, c0);
-            if (tk.r == 1 && tk.g.P > (uint32_t)kRowBytes - 4 && lane == 0)  // register bytes spill into row 1
-                d[0] ^= __builtin_bswap32(tk.g.partial) >> (8 * (kRowBytes - tk.g.P));
+            if (t.r == 1 && g.P > (uint32_t)kRowBytes - 4 && lane == 0)  // register bytes spill into row 1
+                d[0] ^= __builtin_bswap32(g.partial) >> (8 * (kRowBytes - g.P));
         }
     };
-    auto finish = [&](const Task &tk, uint32_t c) {
-        if (tk.kind == 1u) {
-            const Member p = member(tk.h, tk.qm);
+    auto finish = [&](const ChainPos &t, uint32_t c) {
+        if (t.kind == 1u) {
+            const Member p = member(t);
             const uint32_t g = (uint32_t)lane & 15u;
             CrcLane kq = k;
             kq.comb_base = 448u + 4u * g;  // lane 48 + g's combine column: shift by 64*(15-g)
             const uint32_t x = row16_xor(lane_combine(lds, kq, c));
-            if (g == 0 && p.j < 64) out[base + 64 * tk.h + p.j] = __builtin_bswap32(x);
-        } else if (tk.r + 1 == tk.g.R) {
+            if (g == 0 && p.j < kFragsPerWg) out[base + p.j] = __builtin_bswap32(x);
+        } else if ((uint64_t)(t.r + 1) * kRowBytes >= t.len) {
             const uint32_t x = wave_xor(lane_combine(lds, k, c));
             if (lane == 0) {
                 uint32_t res = __builtin_bswap32(x);
-                if (tk.g.len < 4) res ^= tk.g.partial << (8 * tk.g.len);
-                out[base + 64 * tk.h + tk.j] = res;
+                if (t.len < 4) res ^= t.partial << (8 * t.len);
+                out[base + t.j] = res;
             }
         }
     };
-    auto process = [&](RawRow (&raw)[2], const Task (&tk)[2]) {
+    auto process = [&](RawRow (&raw)[2]) {
+        if constexpr (kAbl == 1) {  // keep the loaded data live, nothing else
+            uint32_t x = 0;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) x ^= raw[0].q[q].x ^ raw[1].q[q].w;
+            C[0] ^= x;
+            if (C[0] == 0x9E3779B9u && lane == 64) out[0] = C[1];
+            return;
+        }
         uint32_t d0[16], d1[16];
         uint32_t c0 = C[0], c1 = C[1];
-        if (tk[0].kind != 2u) {
-            prepare(raw[0], tk[0], c0, d0);
+        if (pp[0].kind != 2u) {
+            prepare(raw[0], pp[0], c0, d0);
         } else {
 #pragma unroll
             for (int w = 0; w < 16; ++w) d0[w] = 0u;
         }
-        if (tk[1].kind != 2u) {
-            prepare(raw[1], tk[1], c1, d1);
+        if (pp[1].kind != 2u) {
+            prepare(raw[1], pp[1], c1, d1);
         } else {
 #pragma unroll
             for (int w = 0; w < 16; ++w) d1[w] = 0u;
         }
-        crc_piece2(lds, k, c0, d0, c1, d1);  // a null chain computes garbage, never used
-        if (tk[0].kind == 0u) C[0] = c0;
-        if (tk[1].kind == 0u) C[1] = c1;
-        if (tk[0].kind != 2u) finish(tk[0], c0);
-        if (tk[1].kind != 2u) finish(tk[1], c1);
+        if constexpr (kAbl == 2) {
+#pragma unroll
+            for (int w = 0; w < 16; ++w) {
+                c0 ^= d0[w];
+                c1 ^= d1[w];
+            }
+        } else {
+            crc_piece2(lds, k, c0, d0, c1, d1);  // a null chain computes garbage, never used
+        }
+        if (pp[0].kind == 0u) C[0] = c0;
+        if (pp[1].kind == 0u) C[1] = c1;
+        if (pp[0].kind != 2u) finish(pp[0], c0);
+        if (pp[1].kind != 2u) finish(pp[1], c1);
     };
     constexpr int kL = 10;  // loads per step (two rows)
 #define LAMPI_FRAG_STEP(S)                                                            \
@@ -1077,14 +1133,14 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, ui
                        "+v"(ring[(S) % kD][1].q[3]), "+v"(ring[(S) % kD][1].q[4])     \
                      : "n"((kD - 1) * kL)                                             \
                      : "memory");                                                     \
-        if (t[(S) % kD][0].kind == 2u && t[(S) % kD][1].kind == 2u) break;            \
-        process(ring[(S) % kD], t[(S) % kD]);                                         \
+        if (pp[0].kind == 2u && pp[1].kind == 2u) break;                              \
+        process(ring[(S) % kD]);                                                      \
+        next(pp[0]);                                                                  \
+        next(pp[1]);                                                                  \
+        next(pi[0]);                                                                  \
+        next(pi[1]);                                                                  \
         {                                                                             \
-            const Task n0 = advance(sq[0], t[((S) + kD - 1) % kD][0]);                \
-            const Task n1 = advance(sq[1], t[((S) + kD - 1) % kD][1]);                \
-            t[(S) % kD][0] = n0;                                                      \
-            t[(S) % kD][1] = n1;                                                      \
-            const RowAddrs a0 = addrs(n0), a1 = addrs(n1);                            \
+            const RowAddrs a0 = addrs(pi[0]), a1 = addrs(pi[1]);                      \
             issue_row5(a0, ring[(S) % kD][0]);                                        \
             issue_row5(a1, ring[(S) % kD][1]);                                        \
         }                                                                             \
@@ -1426,7 +1482,7 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
         const uint32_t ph = Src::kPhase ? (uniform(fi.partial) & (uint32_t)(sizeof(Acc) - 1)) : 0u;
         gbyte *fb = fi.addr - ph;
         const uint32_t span = fi.len + ph;
-        const uint32_t R = (span + (kRowBytes - 1)) / kRowBytes;
+        const uint32_t R = (uint32_t)(((uint64_t)fi.len + ph + (kRowBytes - 1)) / kRowBytes);
         const uint32_t s16 = (uint32_t)((uintptr_t)fb & 15u);
         uint8_t *db = fi.dst - ph;
         const uint32_t dm = (uint32_t)((uintptr_t)db & 15u);

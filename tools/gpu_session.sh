@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
-#   smoke | tests | tests_bcopy | bench | bench16k | benchsum | benchC | bcopy | prof | pmc | e2e | microbench
+#   smoke | tests | tests_bcopy | bench | bench16k | benchsum | benchC | benchD | bcopy | prof | pmc | e2e | microbench
 # A test failure (exit 1) lets later steps run; a fault, abort, segfault, timeout or
 # kill (exit >= 124, 134, 139, ...) ends the session immediately.
 set -u
@@ -31,6 +31,7 @@ for step in "$@"; do
     bench16k) run bench16k 600 python bench.py --frags 1048576 --frag-bytes 16384 --no-cpu-baseline ;;
     benchsum) run benchsum 600 python bench.py --mode sum --no-cpu-baseline ;;
     benchC) run benchC 600 python bench.py --config C --steps 10 ;;
+    benchD) run benchD 600 python bench.py --desc --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
             -- python3 bench.py --steps 20 --no-cpu-baseline ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \

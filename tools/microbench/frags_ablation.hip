@@ -1,0 +1,157 @@
+// frags_ablation.hip -- crc_frags_kernel (the general-fragment product kernel) on config C
+// (659,114 Zipf-sized fragments, 4 GiB) and on 4M x 4 KiB descriptors (config B through
+// descriptors), with ablated variants: loads + task walk only, and no table lookups; the
+// regular kernel on the uniform batch for comparison.  Checksums of the product variant are
+// compared with the regular kernel's on the uniform batch.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 frags_ablation.hip -o frags_ablation
+#include "../../lampi_amd/csrc/crc_tables.cc"
+#include "../../lampi_amd/csrc/frag_csum.hip"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <vector>
+
+#define CK(x)                                                                                   \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) {                                                                 \
+            fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            exit(1);                                                                            \
+        }                                                                                       \
+    } while (0)
+
+using namespace lampi;
+
+static uint64_t mix64(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27;
+    z *= 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static std::vector<uint32_t> zipf_lengths(uint64_t min_total) {
+    double cdf[1025], z = 0.0, acc = 0.0;
+    for (int r = 1; r <= 1024; ++r) z += pow((double)r, -1.1);
+    cdf[0] = 0.0;
+    for (int r = 1; r <= 1024; ++r) cdf[r] = (acc += pow((double)r, -1.1) / z);
+    cdf[1024] = 1.0;
+    std::vector<uint32_t> out;
+    uint64_t total = 0;
+    for (uint64_t k = 0; total < min_total; ++k) {
+        const double u = (double)(mix64(0x5A1Full + k) >> 11) * (1.0 / 9007199254740992.0);
+        int lo = 1, hi = 1024;
+        while (lo < hi) {
+            const int mid = (lo + hi) / 2;
+            if (cdf[mid] > u) hi = mid; else lo = mid + 1;
+        }
+        out.push_back(64u * (uint32_t)lo);
+        total += 64u * (uint32_t)lo;
+    }
+    return out;
+}
+
+template <int kAbl, int kD = 3>
+static void launch(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint32_t *out, uint32_t fpg = 0,
+                   size_t pad_lds = 0) {
+    if (fpg == 0) fpg = frags_per_wg(n);
+    hipLaunchKernelGGL((crc_frags_kernel<DescSource, kD, kAbl>), frags_grid(n, fpg), dim3(kBlock), pad_lds, 0,
+                       DescSource{d}, n, fpg, img, out);
+}
+
+template <int kD>
+static int vgprs_of() {
+    hipFuncAttributes a;
+    CK(hipFuncGetAttributes(&a, (const void *)crc_frags_kernel<DescSource, kD, 0>));
+    return a.numRegs;
+}
+
+static double time_ms(const std::function<void()> &go, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 10; ++i) go();
+    CK(hipDeviceSynchronize());
+    std::vector<float> v;
+    for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0));
+        go();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.push_back(ms);
+    }
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+}
+
+int main() {
+    std::vector<uint32_t> img = build_table_image();
+    uint32_t *dimg;
+    CK(hipMalloc(&dimg, img.size() * 4));
+    CK(hipMemcpy(dimg, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+    const size_t bytes = 16ull << 30;
+    uint8_t *buf;
+    CK(hipMalloc(&buf, bytes));
+    launch_fill_stream(buf, bytes, 2, 0, 256, 0);
+    uint32_t *out, *ref;
+    CK(hipMalloc(&out, (4u << 20) * 4));
+    CK(hipMalloc(&ref, (4u << 20) * 4));
+
+    for (int cfg = 0; cfg < 2; ++cfg) {
+        std::vector<lampi_frag_desc> h;
+        uint64_t total = 0;
+        if (cfg == 0) {
+            for (uint32_t L : zipf_lengths(4ull << 30)) {
+                h.push_back({(uint64_t)(uintptr_t)(buf + total), L, 0xFFFFFFFFu});
+                total += L;
+            }
+        } else {
+            for (size_t i = 0; i < (4u << 20); ++i) h.push_back({(uint64_t)(uintptr_t)(buf + 4096 * i), 4096, 0xFFFFFFFFu});
+            total = 16ull << 30;
+        }
+        lampi_frag_desc *d;
+        CK(hipMalloc(&d, h.size() * sizeof(lampi_frag_desc)));
+        CK(hipMemcpy(d, h.data(), h.size() * sizeof(lampi_frag_desc), hipMemcpyHostToDevice));
+        const size_t n = h.size();
+        const char *cname = cfg == 0 ? "config C (Zipf, 4 GiB)" : "4M x 4 KiB descriptors";
+        struct V {
+            const char *name;
+            std::function<void()> go;
+        } vs[] = {{"product", [&] { launch<0>(d, n, dimg, out); }},
+                  {"no lookups", [&] { launch<2>(d, n, dimg, out); }},
+                  {"loads + task walk", [&] { launch<1>(d, n, dimg, out); }}};
+        for (auto &v : vs) {
+            const double ms = time_ms(v.go, 15);
+            printf("%-26s %-20s %8.3f ms  %6.1f%% of 8 TB/s\n", cname, v.name, ms, total / (ms * 1e-3) / 8e12 * 100);
+        }
+        // schedule / occupancy sweep: ring depth (VGPRs), fragments per workgroup, workgroups per CU
+        // (1 per CU forced with extra LDS); waves per CU = 4 x workgroups per CU (LDS-capped)
+        for (int wgcu : {2, 1}) {
+            for (uint32_t fpg : {64u, 128u, 256u}) {
+                const size_t pad = wgcu == 1 ? (16u << 10) : 0;
+                const double m2 = time_ms([&] { launch<0, 2>(d, n, dimg, out, fpg, pad); }, 9);
+                const double m3 = time_ms([&] { launch<0, 3>(d, n, dimg, out, fpg, pad); }, 9);
+                const double m4 = time_ms([&] { launch<0, 4>(d, n, dimg, out, fpg, pad); }, 9);
+                printf("%-26s sweep: %d waves/CU, fpg %3u: kD=2 (%d VGPRs) %5.1f%%  kD=3 (%d) %5.1f%%  kD=4 (%d) %5.1f%%\n",
+                       cname, 4 * wgcu, fpg, vgprs_of<2>(), total / (m2 * 1e-3) / 8e12 * 100, vgprs_of<3>(),
+                       total / (m3 * 1e-3) / 8e12 * 100, vgprs_of<4>(), total / (m4 * 1e-3) / 8e12 * 100);
+            }
+        }
+        if (cfg == 1) {
+            const double ms = time_ms([&] { launch_crc_regular(buf, n, 4096, 0xFFFFFFFFu, ref, dimg, 512, 0); }, 15);
+            printf("%-26s %-20s %8.3f ms  %6.1f%% of 8 TB/s\n", cname, "regular kernel", ms, total / (ms * 1e-3) / 8e12 * 100);
+            launch<0>(d, n, dimg, out);
+            CK(hipDeviceSynchronize());
+            std::vector<uint32_t> a(n), b(n);
+            CK(hipMemcpy(a.data(), out, n * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(b.data(), ref, n * 4, hipMemcpyDeviceToHost));
+            printf("product == regular kernel: %s\n", a == b ? "yes" : "NO");
+        }
+        CK(hipFree(d));
+    }
+    return 0;
+}
