@@ -1157,6 +1157,423 @@ __global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, ui
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the rows in flight before exit
 }
 
+// ---- CRC, general fragments as piece streams (descriptor batches, ragged messages) ---------
+// A workgroup owns up to kFragsPerWg consecutive fragments.  Fragment f is cut into
+// np = ceil(L/64) 64-byte pieces, right-aligned: its first piece starts P = 64*np - L bytes
+// before the fragment (zeros: free for a CRC from a zero register).  The non-empty fragments are
+// split into 2*kWaves contiguous runs of about equal piece count ("chains", two per wave); a
+// chain's pieces, fragment after fragment, form one stream cut into rows of 64 pieces, lane l
+// taking piece l of every row.  Rows are full whatever the fragment sizes: the 4 KiB frame of
+// crc_frags_kernel padded every fragment to whole rows (1.2x the lookups on config C) and needed
+// lane-group packs for small fragments.
+// Per row, lane l CRCs its piece from its start register -- 0; bswap(partial) for a fragment's
+// first piece when P == 0 (otherwise partial is injected as data at byte P); for lane 0, the
+// value carried from the previous row when its piece continues a fragment -- and shifts the
+// result to the end of its segment (the lanes of its fragment in this row, [ss, e]) with the
+// combine column of lane 63 - (e - l) (a shift by 64*(e - l) bytes).  A segmented XOR scan (DPP)
+// leaves each segment's value at its last lane: the fragment's CRC where the fragment ends, the
+// register carried into the next row's lane 0 at lane 63 otherwise.
+// The boundary mask M of a row (bit p: a fragment of the chain starts at piece p) comes from the
+// chain's piece starts in LDS: lane j marks word p_j of a per-chain scratch row, every lane
+// reads its word back and a ballot collects them; a row inside one fragment skips that (M = 0).
+struct StreamDesc {
+    uint64_t addr;
+    uint32_t len, partial;
+};
+
+// per-lane task word: bits 0..8 list position, 9..14 segment end e, 15..20 segment start ss,
+// 21..24 (misaligned variant) the piece's byte misalignment, then the flags
+constexpr uint32_t kTfFirst = 1u << 25, kTfLast = 1u << 26, kTfNull = 1u << 27, kTfSecond = 1u << 28;
+
+template <int N>
+struct RowN {
+    u32x4 q[N];
+};
+template <int N>
+struct AddrN {
+    gbyte *p[N];
+};
+
+__device__ __forceinline__ void issue_rowN(const AddrN<4> &a, RowN<4> &r) {
+    asm volatile(
+        "global_load_dwordx4 %0, %4, off\n\t"
+        "global_load_dwordx4 %1, %5, off\n\t"
+        "global_load_dwordx4 %2, %6, off\n\t"
+        "global_load_dwordx4 %3, %7, off"
+        : "=&v"(r.q[0]), "=&v"(r.q[1]), "=&v"(r.q[2]), "=&v"(r.q[3])
+        : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(a.p[3])
+        : "memory");
+}
+__device__ __forceinline__ void issue_rowN(const AddrN<5> &a, RowN<5> &r) {
+    asm volatile(
+        "global_load_dwordx4 %0, %5, off\n\t"
+        "global_load_dwordx4 %1, %6, off\n\t"
+        "global_load_dwordx4 %2, %7, off\n\t"
+        "global_load_dwordx4 %3, %8, off\n\t"
+        "global_load_dwordx4 %4, %9, off"
+        : "=&v"(r.q[0]), "=&v"(r.q[1]), "=&v"(r.q[2]), "=&v"(r.q[3]), "=&v"(r.q[4])
+        : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(a.p[3]), "v"(a.p[4])
+        : "memory");
+}
+
+// wait until at most N younger loads are outstanding; the two chains' registers of the slot are
+// threaded through so no use is scheduled above the wait
+template <int N>
+__device__ __forceinline__ void wait_rows2(RowN<4> &a, RowN<4> &b) {
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(a.q[0]), "+v"(a.q[1]), "+v"(a.q[2]), "+v"(a.q[3]), "+v"(b.q[0]), "+v"(b.q[1]),
+                   "+v"(b.q[2]), "+v"(b.q[3])
+                 : "n"(N)
+                 : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_rows2(RowN<5> &a, RowN<5> &b) {
+    asm volatile("s_waitcnt vmcnt(%10)"
+                 : "+v"(a.q[0]), "+v"(a.q[1]), "+v"(a.q[2]), "+v"(a.q[3]), "+v"(a.q[4]), "+v"(b.q[0]),
+                   "+v"(b.q[1]), "+v"(b.q[2]), "+v"(b.q[3]), "+v"(b.q[4])
+                 : "n"(N)
+                 : "memory");
+}
+
+// shift by 64*(63 - l') zero bytes with lane l''s combine column (b = comb_col(l'))
+__device__ __forceinline__ uint32_t combine_at(const uint32_t *lds, uint32_t b, uint32_t C) {
+    uint32_t r = lds_u32(lds, ((C << 9) & 0x1E00u) | b);
+    r ^= lds_u32(lds, (((C << 5) & 0x1E00u) | b) + 8192);
+    r ^= lds_u32(lds, (((C << 1) & 0x1E00u) | b) + 2 * 8192);
+#pragma unroll
+    for (int p = 3; p < 8; ++p) r ^= lds_u32(lds, (((C >> (4 * p - 9)) & 0x1E00u) | b) + p * 8192);
+    return r;
+}
+
+__device__ __forceinline__ uint32_t comb_col(uint32_t l) { return (l >> 5) * 256u + 128u + (l & 31u) * 4u; }
+
+// inclusive XOR scan inside segments: lane l gets the XOR of lanes [ss, l] (pos = l - ss).
+// Row-local steps by row_shr (sources outside the row read 0), then row_bcast:15 / :31 carry
+// across rows for lanes whose segment started in an earlier row.
+__device__ __forceinline__ uint32_t seg_scan_xor(uint32_t v, uint32_t pos, uint32_t lane) {
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= pos >= 1u ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= pos >= 2u ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= pos >= 4u ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= pos >= 8u ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v ^= pos > (lane & 15u) ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    v ^= pos > (lane & 31u) ? t : 0u;
+    return v;
+}
+
+template <bool kMis, int kD>
+__device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDesc *sdesc, const uint64_t *sstart,
+                                            const uint16_t *sj, uint32_t *marks, const uint32_t (&ab)[4],
+                                            gbyte *zero, size_t base, uint32_t *__restrict__ out) {
+    constexpr int NL = kMis ? 5 : 4;  // loads per row
+    const uint32_t lane = threadIdx.x & 63u;
+    struct SChain {
+        uint64_t rs, end;  // piece index of the next row's first piece, of the chain's end
+        uint32_t cur, b;   // list position of the fragment holding piece rs - 1; chain end
+    };
+    struct STask {
+        uint32_t info, sreg;  // per lane: task word, start register
+        uint64_t M;           // boundary mask
+        uint32_t fix;         // bit 0: a first piece needs byte masking, bit 1: partial injected as data
+    };
+    SChain cs[2];
+    uint32_t nsteps = 0;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const uint32_t a = ab[2 * c], b = ab[2 * c + 1];
+        cs[c].rs = uniform64(sstart[a]);
+        cs[c].end = uniform64(sstart[b]);
+        cs[c].cur = a - 1u;  // wraps for a == 0: li = cur + (count >= 1)
+        cs[c].b = b;
+        nsteps = max(nsteps, (uint32_t)((cs[c].end - cs[c].rs + 63) >> 6));
+    }
+    if (nsteps == 0) return;
+
+    const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes <= l
+    auto issue_task = [&](SChain &c, uint32_t *mk, STask &t) -> AddrN<NL> {
+        AddrN<NL> A;
+        if (c.rs >= c.end) {  // chain done: null row
+            t.info = kTfNull;
+            t.sreg = 0u;
+            t.M = 0ull;
+            t.fix = 0u;
+#pragma unroll
+            for (int q = 0; q < NL; ++q) A.p[q] = zero;
+            return A;
+        }
+        uint64_t M = 0ull;
+        const uint64_t nb = uniform64(sstart[c.cur + 1u]);
+        if (nb < c.rs + 64u) {  // fragment starts in this row: build the boundary mask
+            const uint32_t i = c.cur + 1u + lane;
+            const bool v = i <= c.b;
+            const uint64_t p = sstart[v ? i : c.b] - c.rs;
+            if (v && p < 64u) mk[(uint32_t)p] = 1u;
+            const uint32_t m = mk[lane];
+            mk[lane] = 0u;
+            M = __builtin_amdgcn_ballot_w64(m != 0u);
+        }
+        const uint32_t li = c.cur + (uint32_t)__popcll(M & le);
+        const bool nul = li >= c.b;
+        const uint32_t lr = nul ? c.b : li;
+        const StreamDesc D = sdesc[lr];
+        const uint32_t k = (uint32_t)(c.rs + lane - sstart[lr]);
+        const uint32_t np = (uint32_t)(((uint64_t)D.len + 63u) >> 6);
+        const uint32_t P = (np << 6) - D.len;  // mod 2^32: always < 64
+        const long long o = (long long)k * 64 - (long long)P;
+        gbyte *pa = (gbyte *)(uintptr_t)D.addr + o;
+        uint32_t sh = 0u;
+        if constexpr (!kMis) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) A.p[q] = (!nul && o + 16 * q + 16 > 0) ? pa + 16 * q : zero;
+        } else {
+            sh = (uint32_t)((uintptr_t)pa & 15u);
+            gbyte *pb = pa - sh;
+            const long long ob = o - (long long)sh;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const long long r = ob + 16 * q;
+                A.p[q] = (!nul && r + 16 > 0 && r < (long long)D.len) ? pb + 16 * q : zero;
+            }
+        }
+        uint32_t e = 63u, ss = 0u;
+        if (M) {
+            const uint64_t above = lane == 63 ? 0ull : (M >> (lane + 1u));
+            e = above ? lane + (uint32_t)__builtin_ctzll(above) : 63u;
+            const uint64_t below = M & le;
+            ss = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+        }
+        const bool first = !nul && k == 0u, last = !nul && k + 1u == np, second = !nul && k == 1u;
+        t.info = (lr & 0x1FFu) | (e << 9) | (ss << 15) | (sh << 21) | (first ? kTfFirst : 0u) |
+                 (last ? kTfLast : 0u) | (nul ? kTfNull : 0u) | (second ? kTfSecond : 0u);
+        t.sreg = (first && P == 0u) ? __builtin_bswap32(D.partial) : 0u;
+        t.M = M;
+        const bool needmask = first && (kMis ? P != 0u : (P & 15u) != 0u);
+        const bool needinj = (first && P != 0u) || (second && P > 60u);
+        t.fix = (__builtin_amdgcn_ballot_w64(needmask) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(needinj) ? 2u : 0u);
+        c.cur += (uint32_t)__popcll(M);
+        c.rs += 64u;
+        return A;
+    };
+
+    // the lane's 16 words, fixed up for first pieces
+    auto prepare = [&](const RowN<NL> &raw, const STask &t, uint32_t d[16]) {
+        if constexpr (!kMis) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                d[4 * q + 0] = raw.q[q].x;
+                d[4 * q + 1] = raw.q[q].y;
+                d[4 * q + 2] = raw.q[q].z;
+                d[4 * q + 3] = raw.q[q].w;
+            }
+        } else {
+            uint32_t a[20];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                a[4 * q + 0] = raw.q[q].x;
+                a[4 * q + 1] = raw.q[q].y;
+                a[4 * q + 2] = raw.q[q].z;
+                a[4 * q + 3] = raw.q[q].w;
+            }
+            const uint32_t sh = (t.info >> 21) & 15u, ws = sh >> 2, sb = sh & 3u;
+            uint32_t b[17];
+#pragma unroll
+            for (int i = 0; i < 17; ++i) b[i] = sel4(ws, a[i], a[i + 1], a[i + 2], a[i + 3]);
+#pragma unroll
+            for (int w = 0; w < 16; ++w) d[w] = __builtin_amdgcn_alignbyte(b[w + 1], b[w], sb);
+        }
+        if (t.fix) {
+            const StreamDesc D = sdesc[t.info & 0x1FFu];
+            const uint32_t P = (0u - D.len) & 63u;
+            const bool first = (t.info & kTfFirst) != 0u;
+            if ((t.fix & 1u) && first) {
+#pragma unroll
+                for (int w = 0; w < 16; ++w) d[w] &= byte_keep_mask(4 * w, (long long)P, 64);
+            }
+            if (t.fix & 2u) {
+                const uint32_t v = __builtin_bswap32(D.partial);
+                if (first && P != 0u) {  // bytes_BE(partial) at piece bytes P..P+3; what lies past
+                    const uint32_t a = P >> 2, q = P & 3u;  // byte 63 goes to the second piece
+                    const uint32_t m0 = v << (8 * q), m1 = q ? (v >> (32 - 8 * q)) : 0u;
+#pragma unroll
+                    for (uint32_t w = 0; w < 16; ++w) d[w] ^= (w == a) ? m0 : ((w == a + 1u) ? m1 : 0u);
+                }
+                if ((t.info & kTfSecond) && P > 60u) d[0] ^= v >> (8 * (64u - P));
+            }
+        }
+    };
+
+    // segment values -> results and the carry of the open segment at lane 63
+    auto finish = [&](const STask &t, uint32_t C, uint32_t &carry) {
+        if (t.M == 0ull) {  // one segment: every lane shifts by 64*(63 - l)
+            const uint32_t x = wave_xor(combine_at(lds, comb_col(lane), C));
+            carry = x;
+            if (lane == 63u && (t.info & kTfLast)) {
+                const uint32_t li = t.info & 0x1FFu;
+                const StreamDesc D = sdesc[li];
+                uint32_t res = __builtin_bswap32(x);
+                if (D.len < 4u) res ^= D.partial << (8 * D.len);
+                out[base + sj[li]] = res;
+            }
+            return;
+        }
+        const uint32_t e = (t.info >> 9) & 63u, ss = (t.info >> 15) & 63u;
+        const uint32_t v = combine_at(lds, comb_col(lane + 63u - e), C);
+        const uint32_t x = seg_scan_xor(v, lane - ss, lane);
+        carry = __builtin_amdgcn_readlane(x, 63);
+        if (e == lane && (t.info & kTfLast)) {
+            const uint32_t li = t.info & 0x1FFu;
+            const StreamDesc D = sdesc[li];
+            uint32_t res = __builtin_bswap32(x);
+            if (D.len < 4u) res ^= D.partial << (8 * D.len);
+            out[base + sj[li]] = res;
+        }
+    };
+
+    const CrcLane kl = make_lane((int)lane);
+    uint32_t *mk0 = marks, *mk1 = marks + 64;
+    RowN<NL> ring[kD][2];
+    STask tk[kD][2];
+#pragma unroll
+    for (int q = 0; q < kD; ++q) {
+        const AddrN<NL> A0 = issue_task(cs[0], mk0, tk[q][0]);
+        const AddrN<NL> A1 = issue_task(cs[1], mk1, tk[q][1]);
+        issue_rowN(A0, ring[q][0]);
+        issue_rowN(A1, ring[q][1]);
+    }
+    uint32_t carry0 = 0u, carry1 = 0u;
+    uint32_t step = 0u;
+    auto process = [&](RowN<NL> (&raw)[2], const STask (&t)[2]) {
+        uint32_t d0[16], d1[16];
+        prepare(raw[0], t[0], d0);
+        prepare(raw[1], t[1], d1);
+        uint32_t c0 = t[0].sreg, c1 = t[1].sreg;
+        if (lane == 0u) {
+            if (!(t[0].info & (kTfFirst | kTfNull))) c0 = carry0;
+            if (!(t[1].info & (kTfFirst | kTfNull))) c1 = carry1;
+        }
+        crc_piece2(lds, kl, c0, d0, c1, d1);
+        finish(t[0], c0, carry0);
+        finish(t[1], c1, carry1);
+    };
+#define LAMPI_STREAM_STEP(S)                                        \
+    if constexpr ((S) < kD) {                                       \
+        wait_rows2<(kD - 1) * 2 * NL>(ring[S][0], ring[S][1]);      \
+        if (step == nsteps) break;                                  \
+        process(ring[S], tk[S]);                                    \
+        ++step;                                                     \
+        {                                                           \
+            const AddrN<NL> A0 = issue_task(cs[0], mk0, tk[S][0]);  \
+            const AddrN<NL> A1 = issue_task(cs[1], mk1, tk[S][1]);  \
+            issue_rowN(A0, ring[S][0]);                             \
+            issue_rowN(A1, ring[S][1]);                             \
+        }                                                           \
+    }
+    for (;;) {
+        LAMPI_STREAM_STEP(0)
+        LAMPI_STREAM_STEP(1)
+        LAMPI_STREAM_STEP(2)
+        LAMPI_STREAM_STEP(3)
+    }
+#undef LAMPI_STREAM_STEP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the rows in flight before exit
+}
+
+template <class Src, int kD = 3>
+__global__ void __launch_bounds__(kBlock) crc_stream_kernel(Src src, size_t n, uint32_t fpg,
+                                                            const uint32_t *__restrict__ img,
+                                                            uint32_t *__restrict__ out) {
+    static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
+    static_assert(kFragsPerWg == kBlock, "one fragment per thread in the set-up");
+    constexpr uint32_t kChains = 2 * kWaves;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[65536 / 4];  // slicing + combine tables
+    __shared__ StreamDesc sdesc[kFragsPerWg + 1];
+    __shared__ uint64_t sstart[kFragsPerWg + 1];  // first piece of list entry i (workgroup-relative)
+    __shared__ uint16_t sj[kFragsPerWg];          // fragment (workgroup-relative) of list entry i
+    __shared__ uint32_t marks[kChains * 64];      // boundary scratch, 64 words per chain
+    __shared__ uint32_t bound[kChains + 1];       // chain c = list entries [bound[c], bound[c+1])
+    __shared__ uint64_t wpieces[kWaves];
+    __shared__ uint32_t wcount[kWaves];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, t = threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * fpg;
+    const uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
+
+    FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
+    if (t < nwg) mine = src.get(base + t);
+    auto nopre = [] {};
+    stage_tables<0, decltype(nopre), 3>(lds, img, nopre);  // no Horner tables; waits for the descriptors too
+    const bool ne = t < nwg && mine.len != 0u;              // list entries: the non-empty fragments
+    if (t < nwg && mine.len == 0u) out[base + t] = mine.partial;  // uicrc(p, 0, s) == s
+    const uint64_t np = ne ? (((uint64_t)mine.len + 63u) >> 6) : 0ull;
+    const bool mis = ne && ((((uintptr_t)mine.addr) + mine.len) & 15u) != 0u;
+    uint64_t ip = np;
+    uint32_t ic = ne ? 1u : 0u;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)ip, s, 64);
+        const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(ip >> 32), s, 64);
+        const uint32_t vc = (uint32_t)__shfl_up((int)ic, s, 64);
+        if (lane >= (uint32_t)s) {
+            ip += ((uint64_t)hi << 32) | lo;
+            ic += vc;
+        }
+    }
+    if (lane == 63u) {
+        wpieces[wave] = ip;
+        wcount[wave] = ic;
+    }
+    __syncthreads();
+    uint64_t op = 0ull, total = 0ull;
+    uint32_t oc = 0u, nne = 0u;
+#pragma unroll
+    for (uint32_t w = 0; w < (uint32_t)kWaves; ++w) {
+        const uint64_t a = wpieces[w];
+        const uint32_t b = wcount[w];
+        if (w < wave) {
+            op += a;
+            oc += b;
+        }
+        total += a;
+        nne += b;
+    }
+    const uint64_t ex = op + ip - np;
+    const uint32_t li = oc + ic - (ne ? 1u : 0u);
+    // chain = min(7, floor((ex + np/2) * 8 / total)): monotonic in list order
+    const uint32_t own = ne ? (uint32_t)min((uint64_t)(kChains - 1), ((2ull * ex + np) * kChains) / (2ull * total)) : 0u;
+    if (ne) {
+        sdesc[li] = StreamDesc{(uint64_t)(uintptr_t)mine.addr, mine.len, mine.partial};
+        sstart[li] = ex;
+        sj[li] = (uint16_t)t;
+        marks[li] = own;
+    }
+    if (t == 0) sstart[nne] = total;
+    __syncthreads();
+    if (ne) {  // entry li opens chains (own(li-1), own(li)]; the last entry closes the rest
+        const int prev = li == 0 ? -1 : (int)marks[li - 1];
+        for (int c = prev + 1; c <= (int)own; ++c) bound[c] = li;
+        if (li + 1 == nne)
+            for (uint32_t c = own + 1; c <= kChains; ++c) bound[c] = nne;
+    }
+    if (t == 0 && nne == 0)
+        for (uint32_t c = 0; c <= kChains; ++c) bound[c] = 0u;
+    __syncthreads();
+    marks[t] = 0u;
+    marks[t + kBlock] = 0u;
+    const bool anymis = __syncthreads_or(mis) != 0;
+    const uint32_t ab[4] = {uniform(bound[2 * wave]), uniform(bound[2 * wave + 1]), uniform(bound[2 * wave + 1]),
+                            uniform(bound[2 * wave + 2])};
+    gbyte *zero = (gbyte *)(img + kImgZero);
+    if (anymis)
+        stream_body<true, kD>(lds, sdesc, sstart, sj, marks + 128 * wave, ab, zero, base, out);
+    else
+        stream_body<false, kD>(lds, sdesc, sstart, sj, marks + 128 * wave, ab, zero, base, out);
+}
+
 // ---- CRC fast path: regular batches -------------------------------------------------------
 // Fragment f = base + f*frag_len, frag_len = R*4096, base 16-byte aligned (P = 0, no masks).
 // A wave checksums kChains of its fragments at once (independent lookup chains interleaved:
@@ -1994,8 +2411,8 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL(crc_frags_kernel<DescSource>, frags_grid(n, fpg), dim3(kBlock), 0, s, DescSource{d}, n, fpg, img,
-                       out);
+    hipLaunchKernelGGL(crc_stream_kernel<DescSource>, frags_grid(n, fpg), dim3(kBlock), 0, s, DescSource{d}, n, fpg,
+                       img, out);
     return hipGetLastError();
 }
 
@@ -2004,7 +2421,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     (void)grid;
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL(crc_frags_kernel<MsgSource>, frags_grid(n, fpg), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(crc_stream_kernel<MsgSource>, frags_grid(n, fpg), dim3(kBlock), 0, s,
                        MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
     return hipGetLastError();
 }

@@ -121,7 +121,9 @@ int main() {
         struct V {
             const char *name;
             std::function<void()> go;
-        } vs[] = {{"product", [&] { launch<0>(d, n, dimg, out); }},
+        } vs[] = {{"stream kernel", [&] { hipLaunchKernelGGL((crc_stream_kernel<DescSource>), frags_grid(n, frags_per_wg(n)),
+                                                          dim3(kBlock), 0, 0, DescSource{d}, n, frags_per_wg(n), dimg, out); }},
+                  {"frame kernel", [&] { launch<0>(d, n, dimg, out); }},
                   {"no lookups", [&] { launch<2>(d, n, dimg, out); }},
                   {"loads + task walk", [&] { launch<1>(d, n, dimg, out); }}};
         for (auto &v : vs) {
