@@ -266,7 +266,7 @@ def run_device(args):
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
-                "kernel": ("crc_frags_kernel (descriptors)" if args.desc and mode == dv.CRC32 else
+                "kernel": ("crc_stream_kernel (descriptors)" if args.desc and mode == dv.CRC32 else
                            "sum_rows_kernel (descriptors)" if args.desc else
                            "crc_regular_kernel" if mode == dv.CRC32 else
                            "crc_regular_kernel (kSum: uicsum on the same schedule)"),
@@ -330,7 +330,7 @@ def run_mixed(args):
         "config": {"workload": f"config C: {lens.size} mixed fragments, {total} B, one descriptor batch "
                                "(lampi_frag_csum_batch)", "fragments": int(lens.size), "bytes": total},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "crc_frags_kernel",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "crc_stream_kernel",
                      "incl_metadata": {"bytes": meta, "achieved": round(meta / kern_avg_s / 1e9, 1),
                                        "frac": round(meta / kern_avg_s / 1e9 / HBM_PEAK_GBS, 4)},
                      "kernel_avg_ms": round(kern_avg_s * 1e3, 4),

@@ -44,6 +44,10 @@
 #include "crc_tables.h"
 #include "frag_csum_kernels.h"
 
+#ifndef LAMPI_EXP
+#define LAMPI_EXP 0
+#endif
+
 namespace lampi {
 
 namespace {
@@ -1267,10 +1271,53 @@ __device__ __forceinline__ uint32_t seg_scan_xor(uint32_t v, uint32_t pos, uint3
     return v;
 }
 
-template <bool kMis, int kD>
+// A chain: rows [c*R/8, (c+1)*R/8) of the workgroup's piece stream (R rows in all), so chains
+// differ by at most one row.  A fragment crossing a chain start is checksummed in parts: the
+// chain holding its first piece leaves the register at its end in sopen, later chains start it
+// from 0 and leave either their open value (sopen) or, where the fragment ends, its value
+// (shead); the parts are joined after the workgroup's rows (stream_join).
+struct StreamChain {
+    uint64_t rs, end;  // pieces [rs, end)
+    uint32_t cur;      // list entry holding piece rs - 1 (head - 1 when the chain starts a fragment)
+    uint32_t b;        // one past the last list entry with a piece in the chain
+    uint32_t head;     // list entry holding piece rs
+    uint32_t mid;      // 1: the chain starts inside fragment `head`
+};
+
+// C (swapped domain) after 64*m zero bytes, m < 2^26: the low six bits of m through lane
+// (63 - (m & 63))'s combine column in LDS, the rows (4096 bytes = 2^12) through the image's
+// shift-by-2^e columns (normal domain, e = 12..31)
+__device__ uint32_t shift_pieces(const uint32_t *lds, const uint32_t *__restrict__ img, uint32_t C, uint64_t m) {
+    const uint32_t l = (uint32_t)(m & 63u);
+    if (l) C = combine_at(lds, comb_col(63u - l), C);
+    uint32_t h = (uint32_t)(m >> 6);
+    if (h) {
+        uint32_t c = __builtin_bswap32(C);
+        while (h) {
+            const uint32_t e = 12u + (uint32_t)__builtin_ctz(h);
+            h &= h - 1u;
+            const uint32_t *col = img + kImgPow2Cols + e * 32u;
+            uint32_t r = 0;
+#pragma unroll
+            for (int b = 0; b < 32; ++b) r ^= ((c >> b) & 1u) ? col[b] : 0u;
+            c = r;
+        }
+        C = __builtin_bswap32(c);
+    }
+    return C;
+}
+
+template <int K>
+struct RowsN4 {
+    RowN<4> r[K];
+};
+
+// kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way
+template <bool kMis, int kD, int kAbl, int kK>
 __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDesc *sdesc, const uint64_t *sstart,
-                                            const uint16_t *sj, uint32_t *marks, const uint32_t (&ab)[4],
-                                            gbyte *zero, size_t base, uint32_t *__restrict__ out) {
+                                            const uint16_t *sj, uint32_t *marks, const StreamChain *sch,
+                                            uint32_t *sopen, uint32_t *shead, gbyte *zero, size_t base,
+                                            uint32_t *__restrict__ out) {
     constexpr int NL = kMis ? 5 : 4;  // loads per row
     const uint32_t lane = threadIdx.x & 63u;
     struct SChain {
@@ -1280,17 +1327,21 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     struct STask {
         uint32_t info, sreg;  // per lane: task word, start register
         uint64_t M;           // boundary mask
-        uint32_t fix;         // bit 0: a first piece needs byte masking, bit 1: partial injected as data
+        uint32_t fix;         // bit 0: a first piece needs byte masking, bit 1: partial injected as data,
+                              // bit 2: null row
+        uint32_t one;         // one-segment rows: list entry | output index << 16
     };
-    SChain cs[2];
+    SChain cs[kK];
+    uint32_t head[kK], mid[kK];
     uint32_t nsteps = 0;
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-        const uint32_t a = ab[2 * c], b = ab[2 * c + 1];
-        cs[c].rs = uniform64(sstart[a]);
-        cs[c].end = uniform64(sstart[b]);
-        cs[c].cur = a - 1u;  // wraps for a == 0: li = cur + (count >= 1)
-        cs[c].b = b;
+    for (int c = 0; c < kK; ++c) {
+        cs[c].rs = uniform64(sch[c].rs);
+        cs[c].end = uniform64(sch[c].end);
+        cs[c].cur = uniform(sch[c].cur);  // wraps for head == 0: li = cur + (count >= 1)
+        cs[c].b = uniform(sch[c].b);
+        head[c] = uniform(sch[c].head);
+        mid[c] = uniform(sch[c].mid);
         nsteps = max(nsteps, (uint32_t)((cs[c].end - cs[c].rs + 63) >> 6));
     }
     if (nsteps == 0) return;
@@ -1299,17 +1350,21 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     auto issue_task = [&](SChain &c, uint32_t *mk, STask &t) -> AddrN<NL> {
         AddrN<NL> A;
         if (c.rs >= c.end) {  // chain done: null row
-            t.info = kTfNull;
+            t.info = kTfNull | (63u << 9);
             t.sreg = 0u;
             t.M = 0ull;
-            t.fix = 0u;
+            t.fix = 4u;
+            t.one = 0u;
 #pragma unroll
             for (int q = 0; q < NL; ++q) A.p[q] = zero;
             return A;
         }
         uint64_t M = 0ull;
         const uint64_t nb = uniform64(sstart[c.cur + 1u]);
-        if (nb < c.rs + 64u) {  // fragment starts in this row: build the boundary mask
+        const uint64_t nb2 = c.cur + 2u <= c.b ? uniform64(sstart[c.cur + 2u]) : ~0ull;
+        if (nb2 >= c.rs + 64u) {  // at most one fragment starts in this row
+            M = nb < c.rs + 64u ? (1ull << (uint32_t)(nb - c.rs)) : 0ull;
+        } else {  // several: build the boundary mask
             const uint32_t i = c.cur + 1u + lane;
             const bool v = i <= c.b;
             const uint64_t p = sstart[v ? i : c.b] - c.rs;
@@ -1317,6 +1372,48 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             const uint32_t m = mk[lane];
             mk[lane] = 0u;
             M = __builtin_amdgcn_ballot_w64(m != 0u);
+        }
+        if ((M & ~1ull) == 0ull) {  // one segment: every lane in list entry cur + M (scalar set-up)
+            const uint32_t lr = c.cur + (uint32_t)M;
+            const uint64_t addr = uniform64(sdesc[lr].addr);
+            const uint32_t len = uniform(sdesc[lr].len), partial = uniform(sdesc[lr].partial);
+            const uint32_t k0 = uniform((uint32_t)(c.rs - sstart[lr]));  // lane 0's piece
+            t.one = (lr & 0xFFFFu) | (uniform(sj[lr]) << 16);
+            const uint32_t np = (uint32_t)(((uint64_t)len + 63u) >> 6);
+            const uint32_t P = (np << 6) - len;
+            const long long o0 = (long long)k0 * 64 - (long long)P;
+            gbyte *pa = (gbyte *)(uintptr_t)addr + o0 + lane * 64u;
+            uint32_t sh = 0u;
+            if constexpr (!kMis) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) A.p[q] = pa + 16 * q;
+                if (o0 + 16 <= 0) {  // lane 0's first piece starts with whole chunks of padding
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (o0 + 16 * q + 16 <= 0 && lane == 0u) A.p[q] = zero;
+                }
+            } else {
+                sh = (uint32_t)((addr + (uint64_t)o0) & 15u);
+                gbyte *pb = pa - sh;
+                const long long ob = o0 + (long long)lane * 64 - (long long)sh;
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    const long long r = ob + 16 * q;
+                    A.p[q] = (r + 16 > 0 && r < (long long)len) ? pb + 16 * q : zero;
+                }
+            }
+            const uint32_t k = k0 + lane;
+            const bool first = k == 0u, last = k + 1u == np, second = k == 1u;
+            t.info = (lr & 0x1FFu) | (63u << 9) | (sh << 21) | (first ? kTfFirst : 0u) | (last ? kTfLast : 0u) |
+                     (second ? kTfSecond : 0u);
+            t.sreg = (first && P == 0u) ? __builtin_bswap32(partial) : 0u;
+            t.M = M;
+            const bool needmask = k0 == 0u && (kMis ? P != 0u : (P & 15u) != 0u);
+            const bool needinj = (k0 == 0u && P != 0u) || (k0 <= 1u && np > 1u && P > 60u);
+            t.fix = (needmask ? 1u : 0u) | (needinj ? 2u : 0u);
+            c.cur += (uint32_t)M;
+            c.rs += 64u;
+            return A;
         }
         const uint32_t li = c.cur + (uint32_t)__popcll(M & le);
         const bool nul = li >= c.b;
@@ -1341,13 +1438,10 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
                 A.p[q] = (!nul && r + 16 > 0 && r < (long long)D.len) ? pb + 16 * q : zero;
             }
         }
-        uint32_t e = 63u, ss = 0u;
-        if (M) {
-            const uint64_t above = lane == 63 ? 0ull : (M >> (lane + 1u));
-            e = above ? lane + (uint32_t)__builtin_ctzll(above) : 63u;
-            const uint64_t below = M & le;
-            ss = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
-        }
+        const uint64_t above = lane == 63 ? 0ull : (M >> (lane + 1u));
+        const uint32_t e = above ? lane + (uint32_t)__builtin_ctzll(above) : 63u;
+        const uint64_t below = M & le;
+        const uint32_t ss = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
         const bool first = !nul && k == 0u, last = !nul && k + 1u == np, second = !nul && k == 1u;
         t.info = (lr & 0x1FFu) | (e << 9) | (ss << 15) | (sh << 21) | (first ? kTfFirst : 0u) |
                  (last ? kTfLast : 0u) | (nul ? kTfNull : 0u) | (second ? kTfSecond : 0u);
@@ -1356,6 +1450,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         const bool needmask = first && (kMis ? P != 0u : (P & 15u) != 0u);
         const bool needinj = (first && P != 0u) || (second && P > 60u);
         t.fix = (__builtin_amdgcn_ballot_w64(needmask) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(needinj) ? 2u : 0u);
+        t.one = 0u;
         c.cur += (uint32_t)__popcll(M);
         c.rs += 64u;
         return A;
@@ -1387,7 +1482,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 #pragma unroll
             for (int w = 0; w < 16; ++w) d[w] = __builtin_amdgcn_alignbyte(b[w + 1], b[w], sb);
         }
-        if (t.fix) {
+        if (t.fix & 3u) {
             const StreamDesc D = sdesc[t.info & 0x1FFu];
             const uint32_t P = (0u - D.len) & 63u;
             const bool first = (t.info & kTfFirst) != 0u;
@@ -1408,71 +1503,113 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         }
     };
 
-    // segment values -> results and the carry of the open segment at lane 63
-    auto finish = [&](const STask &t, uint32_t C, uint32_t &carry) {
-        if (t.M == 0ull) {  // one segment: every lane shifts by 64*(63 - l)
-            const uint32_t x = wave_xor(combine_at(lds, comb_col(lane), C));
-            carry = x;
-            if (lane == 63u && (t.info & kTfLast)) {
-                const uint32_t li = t.info & 0x1FFu;
-                const StreamDesc D = sdesc[li];
-                uint32_t res = __builtin_bswap32(x);
-                if (D.len < 4u) res ^= D.partial << (8 * D.len);
-                out[base + sj[li]] = res;
-            }
+    // a fragment's value: its checksum, or (the head fragment of a chain that starts inside it) the
+    // part for stream_join
+    auto result = [&](int ch, uint32_t li, uint32_t x) {
+        if (mid[ch] && li == head[ch]) {
+            shead[ch] = x;
             return;
         }
-        const uint32_t e = (t.info >> 9) & 63u, ss = (t.info >> 15) & 63u;
-        const uint32_t v = combine_at(lds, comb_col(lane + 63u - e), C);
-        const uint32_t x = seg_scan_xor(v, lane - ss, lane);
-        carry = __builtin_amdgcn_readlane(x, 63);
-        if (e == lane && (t.info & kTfLast)) {
-            const uint32_t li = t.info & 0x1FFu;
-            const StreamDesc D = sdesc[li];
-            uint32_t res = __builtin_bswap32(x);
-            if (D.len < 4u) res ^= D.partial << (8 * D.len);
-            out[base + sj[li]] = res;
+        const StreamDesc D = sdesc[li];
+        uint32_t res = __builtin_bswap32(x);
+        if (D.len < 4u) res ^= D.partial << (8 * D.len);
+        out[base + sj[li]] = res;
+    };
+    // segment values -> results and the carry of the open segment at lane 63.  v: the lane's
+    // value shifted to its segment's end (combine column of lane 63 - (e - l); e = 63 in a
+    // one-segment row).  No early exits: branches here keep the chains from interleaving.
+    auto finish = [&](int ch, const STask &t, uint32_t v, uint32_t &carry) {
+        uint32_t x;
+        if ((t.M & ~1ull) == 0ull) {  // one segment (never a fragment shorter than 4 bytes)
+            x = wave_xor(v);
+            if (lane == 63u && (t.info & kTfLast)) {
+                if (mid[ch] && (t.one & 0xFFFFu) == head[ch])
+                    shead[ch] = x;
+                else
+                    out[base + (t.one >> 16)] = __builtin_bswap32(x);
+            }
+        } else {
+            x = seg_scan_xor(v, lane - ((t.info >> 15) & 63u), lane);
+            if (((t.info >> 9) & 63u) == lane && (t.info & kTfLast)) result(ch, t.info & 0x1FFu, x);
+            x = __builtin_amdgcn_readlane(x, 63);
         }
+        carry = (t.fix & 4u) ? carry : x;  // a null row keeps the chain's final open value
     };
 
     const CrcLane kl = make_lane((int)lane);
-    uint32_t *mk0 = marks, *mk1 = marks + 64;
-    RowN<NL> ring[kD][2];
-    STask tk[kD][2];
+    RowN<NL> ring[kD][kK];
+    STask tk[kD][kK];
 #pragma unroll
     for (int q = 0; q < kD; ++q) {
-        const AddrN<NL> A0 = issue_task(cs[0], mk0, tk[q][0]);
-        const AddrN<NL> A1 = issue_task(cs[1], mk1, tk[q][1]);
-        issue_rowN(A0, ring[q][0]);
-        issue_rowN(A1, ring[q][1]);
+        AddrN<NL> A[kK];
+#pragma unroll
+        for (int c = 0; c < kK; ++c) A[c] = issue_task(cs[c], marks + 64 * c, tk[q][c]);
+#pragma unroll
+        for (int c = 0; c < kK; ++c) issue_rowN(A[c], ring[q][c]);
     }
-    uint32_t carry0 = 0u, carry1 = 0u;
+    uint32_t carry[kK];
+#pragma unroll
+    for (int c = 0; c < kK; ++c) carry[c] = 0u;
     uint32_t step = 0u;
-    auto process = [&](RowN<NL> (&raw)[2], const STask (&t)[2]) {
-        uint32_t d0[16], d1[16];
-        prepare(raw[0], t[0], d0);
-        prepare(raw[1], t[1], d1);
-        uint32_t c0 = t[0].sreg, c1 = t[1].sreg;
-        if (lane == 0u) {
-            if (!(t[0].info & (kTfFirst | kTfNull))) c0 = carry0;
-            if (!(t[1].info & (kTfFirst | kTfNull))) c1 = carry1;
+    auto process = [&](RowN<NL> (&raw)[kK], const STask (&t)[kK]) {
+        if constexpr (kAbl == 1) {  // keep the loaded data and the tasks live, nothing else
+            uint32_t x = t[0].info ^ t[kK - 1].sreg ^ (uint32_t)t[0].M ^ t[kK - 1].fix;
+#pragma unroll
+            for (int q = 0; q < NL; ++q) x ^= raw[0].q[q].x ^ raw[kK - 1].q[q].w;
+            carry[0] ^= x;
+            if (carry[0] == 0x9E3779B9u && lane == 64u) out[0] = carry[kK - 1];
+            return;
         }
-        crc_piece2(lds, kl, c0, d0, c1, d1);
-        finish(t[0], c0, carry0);
-        finish(t[1], c1, carry1);
+        uint32_t d[kK][16], C[kK];
+#pragma unroll
+        for (int c = 0; c < kK; ++c) {
+            prepare(raw[c], t[c], d[c]);
+            C[c] = t[c].sreg;
+            if (lane == 0u && !(t[c].info & (kTfFirst | kTfNull))) C[c] = carry[c];
+        }
+        if constexpr (kAbl == 2) {
+#pragma unroll
+            for (int c = 0; c < kK; ++c)
+#pragma unroll
+                for (int w = 0; w < 16; ++w) C[c] ^= d[c][w];
+        } else if constexpr (kK == 2) {
+            crc_piece2(lds, kl, C[0], d[0], C[1], d[1]);
+        } else {
+            C[0] = crc_piece(lds, kl, C[0], d[0]);
+        }
+        uint32_t v[kK];
+#pragma unroll
+        for (int c = 0; c < kK; ++c) v[c] = combine_at(lds, comb_col(lane + 63u - ((t[c].info >> 9) & 63u)), C[c]);
+#pragma unroll
+        for (int c = 0; c < kK; ++c) finish(c, t[c], v[c], carry[c]);
     };
-#define LAMPI_STREAM_STEP(S)                                        \
-    if constexpr ((S) < kD) {                                       \
-        wait_rows2<(kD - 1) * 2 * NL>(ring[S][0], ring[S][1]);      \
-        if (step == nsteps) break;                                  \
-        process(ring[S], tk[S]);                                    \
-        ++step;                                                     \
-        {                                                           \
-            const AddrN<NL> A0 = issue_task(cs[0], mk0, tk[S][0]);  \
-            const AddrN<NL> A1 = issue_task(cs[1], mk1, tk[S][1]);  \
-            issue_rowN(A0, ring[S][0]);                             \
-            issue_rowN(A1, ring[S][1]);                             \
-        }                                                           \
+    auto wait_slot = [&](RowN<NL> (&r)[kK]) {
+        if constexpr (kK == 2) {
+            wait_rows2<(kD - 1) * 2 * NL>(r[0], r[1]);
+        } else if constexpr (NL == 4) {
+            asm volatile("s_waitcnt vmcnt(%4)"
+                         : "+v"(r[0].q[0]), "+v"(r[0].q[1]), "+v"(r[0].q[2]), "+v"(r[0].q[3])
+                         : "n"((kD - 1) * NL)
+                         : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(%5)"
+                         : "+v"(r[0].q[0]), "+v"(r[0].q[1]), "+v"(r[0].q[2]), "+v"(r[0].q[3]), "+v"(r[0].q[4])
+                         : "n"((kD - 1) * NL)
+                         : "memory");
+        }
+    };
+#define LAMPI_STREAM_STEP(S)                                                                  \
+    if constexpr ((S) < kD) {                                                                 \
+        wait_slot(ring[S]);                                                                   \
+        if (step == nsteps) break;                                                            \
+        process(ring[S], tk[S]);                                                              \
+        ++step;                                                                               \
+        {                                                                                     \
+            AddrN<NL> A[kK];                                                                  \
+            _Pragma("unroll") for (int c = 0; c < kK; ++c) A[c] =                             \
+                issue_task(cs[c], marks + 64 * c, tk[S][c]);                                  \
+            _Pragma("unroll") for (int c = 0; c < kK; ++c) issue_rowN(A[c], ring[S][c]);      \
+        }                                                                                     \
     }
     for (;;) {
         LAMPI_STREAM_STEP(0)
@@ -1482,31 +1619,51 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     }
 #undef LAMPI_STREAM_STEP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the rows in flight before exit
+    if (lane == 0u) {  // the chains' open values (used only where a fragment continues)
+#pragma unroll
+        for (int c = 0; c < kK; ++c) sopen[c] = carry[c];
+    }
 }
 
-template <class Src, int kD = 3>
-__global__ void __launch_bounds__(kBlock) crc_stream_kernel(Src src, size_t n, uint32_t fpg,
-                                                            const uint32_t *__restrict__ img,
-                                                            uint32_t *__restrict__ out) {
+// kAbl (tools/microbench/frags_ablation.hip only): 1 = loads and task walk, no row work;
+// 2 = everything but the table lookups of the pieces.  kK: chains per wave (threads = 512 / kK).
+template <class Src, int kD = 3, int kAbl = 0, int kK = 2>
+__global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n, uint32_t fpg,
+                                                              const uint32_t *__restrict__ img,
+                                                              uint32_t *__restrict__ out) {
     static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
-    static_assert(kFragsPerWg == kBlock, "one fragment per thread in the set-up");
-    constexpr uint32_t kChains = 2 * kWaves;
+    constexpr uint32_t kThreads = 512 / kK, kWv = kThreads / 64;
+    constexpr uint32_t kChains = kWv * kK;  // 8
+    static_assert(kThreads >= kFragsPerWg, "one fragment per thread in the set-up");
     __shared__ __attribute__((aligned(16))) uint32_t lds[65536 / 4];  // slicing + combine tables
     __shared__ StreamDesc sdesc[kFragsPerWg + 1];
     __shared__ uint64_t sstart[kFragsPerWg + 1];  // first piece of list entry i (workgroup-relative)
     __shared__ uint16_t sj[kFragsPerWg];          // fragment (workgroup-relative) of list entry i
     __shared__ uint32_t marks[kChains * 64];      // boundary scratch, 64 words per chain
-    __shared__ uint32_t bound[kChains + 1];       // chain c = list entries [bound[c], bound[c+1])
-    __shared__ uint64_t wpieces[kWaves];
-    __shared__ uint32_t wcount[kWaves];
+    __shared__ StreamChain schain[kChains];
+    __shared__ uint32_t chead[kChains], sopen[kChains], shead[kChains];
+    __shared__ uint64_t wpieces[kWv];
+    __shared__ uint32_t wcount[kWv];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, t = threadIdx.x;
     const size_t base = (size_t)blockIdx.x * fpg;
     const uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
 
     FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
     if (t < nwg) mine = src.get(base + t);
+    if (t < kChains) chead[t] = 0u;
     auto nopre = [] {};
-    stage_tables<0, decltype(nopre), 3>(lds, img, nopre);  // no Horner tables; waits for the descriptors too
+    if constexpr (kThreads == 256) {
+        stage_tables<0, decltype(nopre), 3>(lds, img, nopre);  // no Horner tables; waits for the descriptors too
+    } else {
+        if (t < 256) {  // the table builders are written for 256 threads
+            CombineBasis cb = issue_combine_basis<false>(img);
+            char *b = reinterpret_cast<char *>(lds);
+            build_slices(b);
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(cb.a), "+v"(cb.b) : : "memory");
+            build_combine(b, cb);
+        }
+        __syncthreads();
+    }
     const bool ne = t < nwg && mine.len != 0u;              // list entries: the non-empty fragments
     if (t < nwg && mine.len == 0u) out[base + t] = mine.partial;  // uicrc(p, 0, s) == s
     const uint64_t np = ne ? (((uint64_t)mine.len + 63u) >> 6) : 0ull;
@@ -1531,7 +1688,7 @@ __global__ void __launch_bounds__(kBlock) crc_stream_kernel(Src src, size_t n, u
     uint64_t op = 0ull, total = 0ull;
     uint32_t oc = 0u, nne = 0u;
 #pragma unroll
-    for (uint32_t w = 0; w < (uint32_t)kWaves; ++w) {
+    for (uint32_t w = 0; w < kWv; ++w) {
         const uint64_t a = wpieces[w];
         const uint32_t b = wcount[w];
         if (w < wave) {
@@ -1543,35 +1700,66 @@ __global__ void __launch_bounds__(kBlock) crc_stream_kernel(Src src, size_t n, u
     }
     const uint64_t ex = op + ip - np;
     const uint32_t li = oc + ic - (ne ? 1u : 0u);
-    // chain = min(7, floor((ex + np/2) * 8 / total)): monotonic in list order
-    const uint32_t own = ne ? (uint32_t)min((uint64_t)(kChains - 1), ((2ull * ex + np) * kChains) / (2ull * total)) : 0u;
+    const uint64_t R = (total + 63u) >> 6;  // rows; chain c starts at piece 64 * floor(c * R / 8)
     if (ne) {
         sdesc[li] = StreamDesc{(uint64_t)(uintptr_t)mine.addr, mine.len, mine.partial};
         sstart[li] = ex;
         sj[li] = (uint16_t)t;
-        marks[li] = own;
+#pragma unroll
+        for (uint32_t c = 0; c < kChains; ++c) {
+            const uint64_t pc = 64u * ((c * R) / kChains);
+            if (ex <= pc && pc < ex + np) chead[c] = li;
+        }
     }
     if (t == 0) sstart[nne] = total;
     __syncthreads();
-    if (ne) {  // entry li opens chains (own(li-1), own(li)]; the last entry closes the rest
-        const int prev = li == 0 ? -1 : (int)marks[li - 1];
-        for (int c = prev + 1; c <= (int)own; ++c) bound[c] = li;
-        if (li + 1 == nne)
-            for (uint32_t c = own + 1; c <= kChains; ++c) bound[c] = nne;
+    if (t < kChains) {
+        StreamChain ch;
+        ch.rs = 64u * ((t * R) / kChains);
+        ch.end = t + 1 == kChains ? total : 64u * (((t + 1) * R) / kChains);
+        ch.head = chead[t];
+        ch.mid = sstart[ch.head] < ch.rs ? 1u : 0u;
+        ch.cur = ch.mid ? ch.head : ch.head - 1u;
+        if (t + 1 == kChains) {
+            ch.b = nne;
+        } else {
+            const uint32_t hn = chead[t + 1];
+            ch.b = sstart[hn] < ch.end ? hn + 1u : hn;
+        }
+        if (nne == 0) ch = StreamChain{0ull, 0ull, 0u, 0u, 0u, 0u};
+        schain[t] = ch;
     }
-    if (t == 0 && nne == 0)
-        for (uint32_t c = 0; c <= kChains; ++c) bound[c] = 0u;
-    __syncthreads();
-    marks[t] = 0u;
-    marks[t + kBlock] = 0u;
+    for (uint32_t i = t; i < kChains * 64; i += kThreads) marks[i] = 0u;
     const bool anymis = __syncthreads_or(mis) != 0;
-    const uint32_t ab[4] = {uniform(bound[2 * wave]), uniform(bound[2 * wave + 1]), uniform(bound[2 * wave + 1]),
-                            uniform(bound[2 * wave + 2])};
     gbyte *zero = (gbyte *)(img + kImgZero);
     if (anymis)
-        stream_body<true, kD>(lds, sdesc, sstart, sj, marks + 128 * wave, ab, zero, base, out);
+        stream_body<true, kD, kAbl, kK>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+                                        sopen + kK * wave, shead + kK * wave, zero, base, out);
     else
-        stream_body<false, kD>(lds, sdesc, sstart, sj, marks + 128 * wave, ab, zero, base, out);
+        stream_body<false, kD, kAbl, kK>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+                                         sopen + kK * wave, shead + kK * wave, zero, base, out);
+    if (nne == 0 || kAbl != 0) return;
+    __syncthreads();
+    // stream_join: fragments crossing chain starts.  Thread c owns the fragment crossing chain c's
+    // start when that is the first chain start inside it; the part before is chain c-1's open
+    // value, every later part is shifted in by its length.
+    if (t >= 1 && t < kChains && schain[t].mid) {
+        const uint32_t f = schain[t].head;
+        if (schain[t - 1].rs <= sstart[f]) {
+            const uint64_t ef = sstart[f + 1];
+            uint32_t C = sopen[t - 1];
+            for (uint32_t c = t; c < kChains; ++c) {
+                const uint64_t lo = schain[c].rs, hi = schain[c].end;
+                if (hi == lo) continue;
+                if (ef <= hi) {
+                    C = shift_pieces(lds, img, C, ef - lo) ^ shead[c];
+                    break;
+                }
+                C = shift_pieces(lds, img, C, hi - lo) ^ sopen[c];
+            }
+            out[base + sj[f]] = __builtin_bswap32(C);
+        }
+    }
 }
 
 // ---- CRC fast path: regular batches -------------------------------------------------------
@@ -2402,6 +2590,9 @@ static uint32_t frags_per_wg(size_t n) {
     return fpg;
 }
 
+// crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_ablation.hip)
+constexpr int kStreamD = 3, kStreamK = 1;
+
 static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg - 1) / fpg)); }
 
 static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size_t)kWaves * fpw - 1) / ((size_t)kWaves * fpw))); }
@@ -2411,7 +2602,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL(crc_stream_kernel<DescSource>, frags_grid(n, fpg), dim3(kBlock), 0, s, DescSource{d}, n, fpg,
+    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK>), frags_grid(n, fpg), dim3(512 / kStreamK), 0, s, DescSource{d}, n, fpg,
                        img, out);
     return hipGetLastError();
 }
@@ -2421,7 +2612,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     (void)grid;
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL(crc_stream_kernel<MsgSource>, frags_grid(n, fpg), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK>), frags_grid(n, fpg), dim3(512 / kStreamK), 0, s,
                        MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
     return hipGetLastError();
 }

@@ -131,6 +131,43 @@ def test_descriptor_batch_random(cuda, oracle):
         assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("case", ["three", "aligned40", "mixed600", "huge_first"])
+def test_descriptor_batch_fragments_across_chains(cuda, oracle, case):
+    """The piece-stream kernel cuts a workgroup's pieces into eight chains of equal row counts, so
+    a long fragment is checksummed in parts by several chains and joined at the end (stream_join,
+    shifts by arbitrary piece counts).  Few fragments per workgroup and multi-MiB lengths make
+    fragments span two to eight chains; misaligned ends take the five-load variant."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(hash(case) % 2**32)
+    MiB = 1 << 20
+    if case == "three":
+        lens = np.array([20 * MiB + 3, 1, 5 * MiB + 61], dtype=np.uint64)
+        offs = np.array([5, 21 * MiB + 7, 22 * MiB + 1], dtype=np.uint64)
+    elif case == "aligned40":
+        lens = np.where(np.arange(40) % 2 == 0, 64 * rng.integers(16384, 65536, size=40),
+                        64 * rng.integers(1, 20, size=40)).astype(np.uint64)
+        offs = (np.concatenate([[0], np.cumsum(lens)[:-1]]) + 4096).astype(np.uint64)
+    elif case == "mixed600":
+        lens = np.where(rng.integers(0, 8, size=600) == 0, rng.integers(MiB // 2, 3 * MiB, size=600),
+                        rng.integers(0, 5000, size=600)).astype(np.uint64)
+        offs = rng.integers(0, 40 * MiB, size=600).astype(np.uint64)
+    else:  # one fragment much longer than the rest of its workgroup, then empties and tiny ones
+        lens = np.array([30 * MiB + 64, 0, 3, 0, 64, 128, 4096, 1], dtype=np.uint64)
+        offs = np.array([64, 0, 9, 0, 31 * MiB, 31 * MiB + 64, 31 * MiB + 256, 33 * MiB], dtype=np.uint64)
+    size = int((offs + lens).max()) + 64
+    base = torch.empty(size, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=77)
+    host = base.cpu().numpy()
+    parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
+    descs = dv.make_descs(base, offs, lens, parts)
+    got = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.CRC32))
+    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32), 0)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+
+
 @pytest.mark.parametrize("n", [30000, 300000])
 def test_descriptor_batch_small_fragment_packs(cuda, oracle, n):
     """Fragments of 16..1024 bytes (multiples of 16, 16-byte aligned) go four to a row in lane

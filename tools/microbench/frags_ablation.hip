@@ -61,6 +61,20 @@ static void launch(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint
                        DescSource{d}, n, fpg, img, out);
 }
 
+template <int kAbl, int kD = 2, int kK = 2>
+static void launch_stream(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint32_t *out) {
+    const uint32_t fpg = frags_per_wg(n);
+    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kD, kAbl, kK>), frags_grid(n, fpg), dim3(512 / kK), 0, 0,
+                       DescSource{d}, n, fpg, img, out);
+}
+
+template <int kD, int kK>
+static int stream_vgprs() {
+    hipFuncAttributes a;
+    CK(hipFuncGetAttributes(&a, (const void *)crc_stream_kernel<DescSource, kD, 0, kK>));
+    return a.numRegs;
+}
+
 template <int kD>
 static int vgprs_of() {
     hipFuncAttributes a;
@@ -101,6 +115,8 @@ int main() {
     CK(hipMalloc(&out, (4u << 20) * 4));
     CK(hipMalloc(&ref, (4u << 20) * 4));
 
+    printf("stream VGPRs: K2 kD2 %d, K2 kD3 %d, K1 kD2 %d, K1 kD3 %d, K1 kD4 %d\n", stream_vgprs<2, 2>(),
+           stream_vgprs<3, 2>(), stream_vgprs<2, 1>(), stream_vgprs<3, 1>(), stream_vgprs<4, 1>());
     for (int cfg = 0; cfg < 2; ++cfg) {
         std::vector<lampi_frag_desc> h;
         uint64_t total = 0;
@@ -121,8 +137,15 @@ int main() {
         struct V {
             const char *name;
             std::function<void()> go;
-        } vs[] = {{"stream kernel", [&] { hipLaunchKernelGGL((crc_stream_kernel<DescSource>), frags_grid(n, frags_per_wg(n)),
-                                                          dim3(kBlock), 0, 0, DescSource{d}, n, frags_per_wg(n), dimg, out); }},
+        } vs[] = {{"stream K2 kD2 (product)", [&] { launch_stream<0, 2, 2>(d, n, dimg, out); }},
+                  {"stream K2 kD2 no lookups", [&] { launch_stream<2, 2, 2>(d, n, dimg, out); }},
+                  {"stream K2 kD2 loads+tasks", [&] { launch_stream<1, 2, 2>(d, n, dimg, out); }},
+                  {"stream K2 kD3", [&] { launch_stream<0, 3, 2>(d, n, dimg, out); }},
+                  {"stream K1 kD2", [&] { launch_stream<0, 2, 1>(d, n, dimg, out); }},
+                  {"stream K1 kD3", [&] { launch_stream<0, 3, 1>(d, n, dimg, out); }},
+                  {"stream K1 kD4", [&] { launch_stream<0, 4, 1>(d, n, dimg, out); }},
+                  {"stream K1 kD3 no lookups", [&] { launch_stream<2, 3, 1>(d, n, dimg, out); }},
+                  {"stream K1 kD3 loads+tasks", [&] { launch_stream<1, 3, 1>(d, n, dimg, out); }},
                   {"frame kernel", [&] { launch<0>(d, n, dimg, out); }},
                   {"no lookups", [&] { launch<2>(d, n, dimg, out); }},
                   {"loads + task walk", [&] { launch<1>(d, n, dimg, out); }}};
@@ -133,6 +156,7 @@ int main() {
         // schedule / occupancy sweep: ring depth (VGPRs), fragments per workgroup, workgroups per CU
         // (1 per CU forced with extra LDS); waves per CU = 4 x workgroups per CU (LDS-capped)
         for (int wgcu : {2, 1}) {
+            if (!getenv("SWEEP")) break;
             for (uint32_t fpg : {64u, 128u, 256u}) {
                 const size_t pad = wgcu == 1 ? (16u << 10) : 0;
                 const double m2 = time_ms([&] { launch<0, 2>(d, n, dimg, out, fpg, pad); }, 9);
