@@ -1316,7 +1316,7 @@ struct RowsN4 {
 template <bool kMis, int kD, int kAbl, int kK>
 __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDesc *sdesc, const uint64_t *sstart,
                                             const uint16_t *sj, uint32_t *marks, const StreamChain *sch,
-                                            uint32_t *sopen, uint32_t *shead, gbyte *zero, size_t base,
+                                            uint32_t *sopen, uint32_t *shead, gbyte *zero, uint32_t *sres,
                                             uint32_t *__restrict__ out) {
     constexpr int NL = kMis ? 5 : 4;  // loads per row
     const uint32_t lane = threadIdx.x & 63u;
@@ -1513,7 +1513,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         const StreamDesc D = sdesc[li];
         uint32_t res = __builtin_bswap32(x);
         if (D.len < 4u) res ^= D.partial << (8 * D.len);
-        out[base + sj[li]] = res;
+        sres[sj[li]] = res;
     };
     // segment values -> results and the carry of the open segment at lane 63.  v: the lane's
     // value shifted to its segment's end (combine column of lane 63 - (e - l); e = 63 in a
@@ -1526,7 +1526,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
                 if (mid[ch] && (t.one & 0xFFFFu) == head[ch])
                     shead[ch] = x;
                 else
-                    out[base + (t.one >> 16)] = __builtin_bswap32(x);
+                    sres[t.one >> 16] = __builtin_bswap32(x);
             }
         } else {
             x = seg_scan_xor(v, lane - ((t.info >> 15) & 63u), lane);
@@ -1642,6 +1642,7 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
     __shared__ uint32_t marks[kChains * 64];      // boundary scratch, 64 words per chain
     __shared__ StreamChain schain[kChains];
     __shared__ uint32_t chead[kChains], sopen[kChains], shead[kChains];
+    __shared__ uint32_t sres[kFragsPerWg];        // the workgroup's checksums, stored at the end
     __shared__ uint64_t wpieces[kWv];
     __shared__ uint32_t wcount[kWv];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, t = threadIdx.x;
@@ -1665,7 +1666,7 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
         __syncthreads();
     }
     const bool ne = t < nwg && mine.len != 0u;              // list entries: the non-empty fragments
-    if (t < nwg && mine.len == 0u) out[base + t] = mine.partial;  // uicrc(p, 0, s) == s
+    if (t < nwg && mine.len == 0u) sres[t] = mine.partial;  // uicrc(p, 0, s) == s
     const uint64_t np = ne ? (((uint64_t)mine.len + 63u) >> 6) : 0ull;
     const bool mis = ne && ((((uintptr_t)mine.addr) + mine.len) & 15u) != 0u;
     uint64_t ip = np;
@@ -1734,11 +1735,11 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
     gbyte *zero = (gbyte *)(img + kImgZero);
     if (anymis)
         stream_body<true, kD, kAbl, kK>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
-                                        sopen + kK * wave, shead + kK * wave, zero, base, out);
+                                        sopen + kK * wave, shead + kK * wave, zero, sres, out);
     else
         stream_body<false, kD, kAbl, kK>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
-                                         sopen + kK * wave, shead + kK * wave, zero, base, out);
-    if (nne == 0 || kAbl != 0) return;
+                                         sopen + kK * wave, shead + kK * wave, zero, sres, out);
+    if (kAbl != 0) return;
     __syncthreads();
     // stream_join: fragments crossing chain starts.  Thread c owns the fragment crossing chain c's
     // start when that is the first chain start inside it; the part before is chain c-1's open
@@ -1757,9 +1758,11 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
                 }
                 C = shift_pieces(lds, img, C, hi - lo) ^ sopen[c];
             }
-            out[base + sj[f]] = __builtin_bswap32(C);
+            sres[sj[f]] = __builtin_bswap32(C);
         }
     }
+    __syncthreads();
+    if (t < nwg) out[base + t] = sres[t];
 }
 
 // ---- CRC fast path: regular batches -------------------------------------------------------

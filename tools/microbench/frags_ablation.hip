@@ -62,8 +62,8 @@ static void launch(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint
 }
 
 template <int kAbl, int kD = 2, int kK = 2>
-static void launch_stream(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint32_t *out) {
-    const uint32_t fpg = frags_per_wg(n);
+static void launch_stream(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint32_t *out, uint32_t fpg = 0) {
+    if (fpg == 0) fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kD, kAbl, kK>), frags_grid(n, fpg), dim3(512 / kK), 0, 0,
                        DescSource{d}, n, fpg, img, out);
 }
@@ -146,6 +146,10 @@ int main() {
                   {"stream K1 kD4", [&] { launch_stream<0, 4, 1>(d, n, dimg, out); }},
                   {"stream K1 kD3 no lookups", [&] { launch_stream<2, 3, 1>(d, n, dimg, out); }},
                   {"stream K1 kD3 loads+tasks", [&] { launch_stream<1, 3, 1>(d, n, dimg, out); }},
+                  {"stream K1 kD2 fpg 128", [&] { launch_stream<0, 2, 1>(d, n, dimg, out, 128); }},
+                  {"stream K1 kD2 fpg 64", [&] { launch_stream<0, 2, 1>(d, n, dimg, out, 64); }},
+                  {"stream K1 kD3 fpg 128", [&] { launch_stream<0, 3, 1>(d, n, dimg, out, 128); }},
+                  {"stream K1 kD2 fpg 128 loads+tasks", [&] { launch_stream<1, 2, 1>(d, n, dimg, out, 128); }},
                   {"frame kernel", [&] { launch<0>(d, n, dimg, out); }},
                   {"no lookups", [&] { launch<2>(d, n, dimg, out); }},
                   {"loads + task walk", [&] { launch<1>(d, n, dimg, out); }}};
