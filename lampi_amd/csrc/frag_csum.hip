@@ -677,143 +677,9 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
     }
 }
 
-// ---- CRC, general fragments, pipelined (descriptor batches, ragged messages) --------------
-// The frame of crc_rows_kernel (one wavefront per fragment, right-aligned 4 KiB rows), but the
-// wave's rows stream through a kD-slot register ring of asm-issued loads -- kD-1 rows in
-// flight while one is checksummed, across fragment boundaries -- instead of one compiler
-// prefetch, and the wave's descriptors are read once, one per lane, while the tables are
-// staged.  Every row is exactly five dwordx4 loads: the aligned 16-byte chunks covering the
-// lane's 64-byte window (shifted into place by v_alignbyte for misaligned fragments); a chunk
-// wholly outside the fragment is redirected to the fragment's first chunk and never used, so
-// nothing outside an aligned chunk holding a fragment byte is read and the waits count the
-// ring exactly.
-struct RawRow {
-    u32x4 q[5];
-};
+constexpr uint32_t kFragsPerWg = 256;  // fragments per workgroup of crc_stream_kernel (at most)
 
-struct FragGeom {  // wave-uniform
-    gbyte *addr;
-    uint32_t len, partial, R, P, s16;
-};
-
-template <int N>
-__device__ __forceinline__ void wait_raw(RawRow &r) {
-    asm volatile("s_waitcnt vmcnt(%5)"
-                 : "+v"(r.q[0]), "+v"(r.q[1]), "+v"(r.q[2]), "+v"(r.q[3]), "+v"(r.q[4])
-                 : "n"(N)
-                 : "memory");
-}
-
-// window [o, o + 64) relative to addr; addr + o - s16 is 16-byte aligned.  Chunks wholly outside
-// the fragment load 16 zero bytes (`zero`, in the table image), so with a 16-byte-aligned
-// fragment the row-0 padding needs no masking.
-// The five loads of a ring slot are one asm block fed with addresses computed beforehand: a
-// slot's registers must be defined at a single point -- loads issued on two branches would
-// meet in a phi, and a register copy of data still in flight reads garbage.
-struct RowAddrs {
-    gbyte *p[5];
-};
-
-__device__ __forceinline__ void issue_row5(const RowAddrs &a, RawRow &raw) {
-    asm volatile(
-        "global_load_dwordx4 %0, %5, off\n\t"
-        "global_load_dwordx4 %1, %6, off\n\t"
-        "global_load_dwordx4 %2, %7, off\n\t"
-        "global_load_dwordx4 %3, %8, off\n\t"
-        "global_load_dwordx4 %4, %9, off"
-        : "=&v"(raw.q[0]), "=&v"(raw.q[1]), "=&v"(raw.q[2]), "=&v"(raw.q[3]), "=&v"(raw.q[4])
-        : "v"(a.p[0]), "v"(a.p[1]), "v"(a.p[2]), "v"(a.p[3]), "v"(a.p[4])
-        : "memory");
-}
-
-__device__ __forceinline__ RowAddrs frag_row_addrs(const FragGeom &g, uint32_t r, int lane, gbyte *zero) {
-    // aligned chunk base of the lane's window, relative to addr
-    const long long cb = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P - (long long)g.s16;
-    gbyte *b = g.addr + cb;
-    RowAddrs a;
-    if (g.s16 == 0 && (r > 0 || g.P == 0)) {  // every lane's four chunks inside, the fifth unused
-#pragma unroll
-        for (int k = 0; k < 4; ++k) a.p[k] = b + 16 * k;
-        a.p[4] = zero;
-        return a;
-    }
-    // row 0 of a padded frame or a misaligned fragment: chunk c = cb + 16k is inside iff
-    // -16 < c < len, i.e. (unsigned)(c + 15) < len + 15 while |c| < 2^31
-    const bool small = g.len < 0x80000000u;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const long long c = cb + 16 * k;
-        const bool in = small ? ((uint32_t)c + 15u < g.len + 15u) : (c + 16 > 0 && c < (long long)g.len);
-        a.p[k] = ((k < 4 || g.s16 != 0) && in) ? b + 16 * k : zero;
-    }
-    return a;
-}
-
-// the lane's 16 LE words of the frame row; bytes before the fragment (row 0 padding) read as 0
-// (only a fragment that does not start on a 16-byte boundary has a chunk holding bytes on both
-// sides of its start: that row 0 is masked byte by byte)
-__device__ __forceinline__ void finish_frag_row(const FragGeom &g, uint32_t r, int lane, const RawRow &raw,
-                                                uint32_t d[16]) {
-    uint32_t a[20];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        a[4 * k + 0] = raw.q[k].x;
-        a[4 * k + 1] = raw.q[k].y;
-        a[4 * k + 2] = raw.q[k].z;
-        a[4 * k + 3] = raw.q[k].w;
-    }
-    const uint32_t sb = g.s16 & 3u;
-    if (g.s16 == 0) {
-#pragma unroll
-        for (int w = 0; w < 16; ++w) d[w] = a[w];
-    } else switch (g.s16 >> 2) {  // wave-uniform
-#define LAMPI_SHIFT_CASE(W)                                                                  \
-    case W:                                                                                  \
-        _Pragma("unroll") for (int w = 0; w < 16; ++w) d[w] =                                \
-            __builtin_amdgcn_alignbyte(a[w + (W) + 1], a[w + (W)], sb);                      \
-        break;
-        LAMPI_SHIFT_CASE(0)
-        LAMPI_SHIFT_CASE(1)
-        LAMPI_SHIFT_CASE(2)
-        LAMPI_SHIFT_CASE(3)
-#undef LAMPI_SHIFT_CASE
-    }
-    if (r == 0 && ((uintptr_t)g.addr & 15u) != 0) {
-        const long long o = (long long)lane * kLaneBytes - (long long)g.P;
-#pragma unroll
-        for (int w = 0; w < 16; ++w) d[w] &= byte_keep_mask(o + 4 * w, 0, (long long)g.len);
-    }
-}
-
-// Small fragments go in lane groups ("packs"): a fragment of 16..1024 bytes, a multiple of 16
-// and 16-byte aligned, is checksummed by 16 lanes as one 1 KiB row (right-aligned frame,
-// P = 1024 - len), four fragments per row.  Group lane g's combine shift, 64*(15-g) bytes, is
-// lane 48+g's table (lanes g and g+16 share a bank: 2-way); the group XOR is the 16-lane DPP
-// row reduction.  A 64-byte fragment then costs a quarter row of lookups instead of a row.
-constexpr uint32_t kFragsPerWg = 256;
-constexpr uint32_t kPackBytes = 1024;
-
-__device__ __forceinline__ bool pack_ok(uint32_t len, uint64_t addr) {
-    return len >= 16 && len <= kPackBytes && (len & 15u) == 0 && (addr & 15u) == 0;
-}
-
-// pack row: group lane g of a fragment of `len` bytes at `addr` (len 0: an empty group); the
-// fifth chunk is never used by a 16-byte-aligned frame and reads the zero chunk
-__device__ __forceinline__ RowAddrs pack_row_addrs(gbyte *addr, uint32_t len, uint32_t g, gbyte *zero) {
-    const long long o = (long long)g * kLaneBytes - (long long)(kPackBytes - len);
-    RowAddrs a;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-        const long long c = o + 16 * k;
-        const bool inside = k < 4 && c + 16 > 0 && c < (long long)len;
-        a.p[k] = inside ? addr + c : zero;
-    }
-    return a;
-}
-
-// Two chains per wave, one row of each per step, so the two dependent lookup chains interleave
-// (as the two fragments per step of crc_regular_kernel).  A chain that is finished (or empty)
-// gets null tasks: its ring loads read the zero chunk and nothing is processed.
+// Two independent registers through their 16-word pieces, interleaved (two chains per wave)
 __device__ __forceinline__ void crc_piece2(const uint32_t *lds, const CrcLane &k, uint32_t &C0, const uint32_t d0[16],
                                            uint32_t &C1, const uint32_t d1[16]) {
     uint32_t X0 = C0 ^ d0[0], X1 = C1 ^ d1[0];
@@ -828,337 +694,6 @@ __device__ __forceinline__ void crc_piece2(const uint32_t *lds, const CrcLane &k
     const Look4 t1 = look4(lds, k, X1);
     C0 = xor3(t0.t0, t0.t1, t0.t2) ^ t0.t3;
     C1 = xor3(t1.t0, t1.t1, t1.t2) ^ t1.t3;
-}
-
-// Work split (per workgroup of up to kFragsPerWg consecutive fragments): thread t reads
-// descriptor t into LDS and takes its cost (quarter rows: a pack member 1, a fragment 4 per
-// row, an empty fragment 0 -- answered at once); a block-wide prefix of the costs cuts the
-// fragments into 2 x kWaves contiguous runs of about equal cost (midpoint rule), one per chain:
-// wave w runs chains 2w and 2w+1.  Two LDS lists (pack members in order, whole-row fragments in
-// order) turn a run into a slice of each; a chain walks its pack rows (four members each), then
-// its fragments' rows.  Eight runs over the whole workgroup balance Zipf-sized batches to ~1.15x
-// the ideal chain length, against ~1.33x for four runs per half.
-// kAbl (tools/microbench/frags_ablation.hip only): 1 = loads and task walk, no row work;
-// 2 = everything but the table lookups
-template <class Src, int kD = 3, int kAbl = 0>
-__global__ void __launch_bounds__(kBlock) crc_frags_kernel(Src src, size_t n, uint32_t fpg,
-                                                           const uint32_t *__restrict__ img,
-                                                           uint32_t *__restrict__ out) {
-    static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
-    static_assert(kFragsPerWg == kBlock, "one fragment per thread in the set-up");
-    constexpr uint32_t kChains = 2 * kWaves;
-    struct SDesc {
-        uint64_t addr;
-        uint32_t len, partial;
-    };
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
-    __shared__ SDesc sdesc[kFragsPerWg];
-    __shared__ uint16_t plist[kFragsPerWg], rlist[kFragsPerWg];  // pack members / row fragments, in order
-    __shared__ uint32_t spk[kFragsPerWg + 1], srw[kFragsPerWg + 1];  // exclusive counts of each kind
-    __shared__ uint32_t sown[kFragsPerWg];
-    __shared__ uint32_t bound[kChains + 1];  // run c = fragments [bound[c], bound[c+1])
-    __shared__ uint32_t wsum[kWaves][2];
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint32_t t = threadIdx.x;
-    const size_t base = (size_t)blockIdx.x * fpg;  // fpg <= kFragsPerWg fragments per workgroup
-    const uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
-
-    FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
-    if (t < nwg) mine = src.get(base + t);
-    stage_tables<0>(lds, img, [] {});  // waits for the descriptors too
-    const uint64_t myA = (uint64_t)(uintptr_t)mine.addr;
-    const bool valid = t < nwg;
-    const bool isPack = valid && pack_ok(mine.len, myA);
-    const bool isRow = valid && !isPack && mine.len != 0;
-    if (valid && mine.len == 0) out[base + t] = mine.partial;  // uicrc(p, 0, s) == s
-    const uint32_t myR = (uint32_t)(((uint64_t)mine.len + (kRowBytes - 1)) / kRowBytes);
-    const uint32_t cost = isPack ? 1u : (isRow ? 4u * myR : 0u);
-    const uint32_t kinds = (isPack ? 1u : 0u) | (isRow ? 0x10000u : 0u);
-    sdesc[t] = SDesc{myA, mine.len, mine.partial};
-    // block-wide exclusive prefixes of the cost and of the two kind counts
-    uint32_t ic = cost, ik = kinds;
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-        const uint32_t vc = (uint32_t)__shfl_up((int)ic, s, 64);
-        const uint32_t vk = (uint32_t)__shfl_up((int)ik, s, 64);
-        if (lane >= s) {
-            ic += vc;
-            ik += vk;
-        }
-    }
-    if (lane == 63) {
-        wsum[wave][0] = ic;
-        wsum[wave][1] = ik;
-    }
-    __syncthreads();
-    uint32_t oc = 0, ok = 0, total = 0, totk = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < (uint32_t)kWaves; ++w) {
-        const uint32_t a = wsum[w][0], b = wsum[w][1];
-        if (w < wave) {
-            oc += a;
-            ok += b;
-        }
-        total += a;
-        totk += b;
-    }
-    const uint32_t excl = oc + ic - cost, exk = ok + ik - kinds;
-    // run = min(7, floor((excl + cost/2) * 8 / total)): monotonic in t
-    const uint32_t own = total ? min(kChains - 1, (uint32_t)(((2ull * excl + cost) * kChains) / (2ull * total))) : 0u;
-    sown[t] = own;
-    spk[t] = exk & 0xFFFFu;
-    srw[t] = exk >> 16;
-    if (t == 0) {
-        spk[kFragsPerWg] = totk & 0xFFFFu;
-        srw[kFragsPerWg] = totk >> 16;
-    }
-    if (isPack) plist[exk & 0xFFFFu] = (uint16_t)t;
-    if (isRow) rlist[exk >> 16] = (uint16_t)t;
-    __syncthreads();
-    if (valid) {  // t opens runs (own(t-1), own(t)]; the last fragment closes the rest
-        const int prev = t == 0 ? -1 : (int)sown[t - 1];
-        for (int c = prev + 1; c <= (int)own; ++c) bound[c] = t;
-        if (t + 1 == nwg)
-            for (uint32_t c = own + 1; c <= kChains; ++c) bound[c] = nwg;
-    }
-    if (t == 0 && nwg < kFragsPerWg) {  // counts at nwg (the slots past the batch end hold 0)
-        spk[nwg] = totk & 0xFFFFu;
-        srw[nwg] = totk >> 16;
-    }
-    __syncthreads();
-
-    // A chain's tasks: pack rows (members plist[p .. p+3], clamped to pe), then row r of
-    // fragment rlist[q] for q < re.  The issue side and the process side walk the same sequence
-    // kD steps apart (ChainPos + next()), so nothing per ring slot is stored beyond the data.
-    struct ChainPos {
-        uint32_t p, pe, q, re;
-        uint32_t kind;  // 0: row r of fragment j, 1: a pack row, 2: null (chain done)
-        uint32_t j, r;
-        gbyte *addr;    // kind 0: fragment j
-        uint32_t len, partial;
-    };
-    auto geom = [](const ChainPos &p) -> FragGeom {  // derived on use (scalar ALU), not carried
-        FragGeom g;
-        g.addr = p.addr;
-        g.len = p.len;
-        g.partial = p.partial;
-        g.R = (uint32_t)(((uint64_t)p.len + (kRowBytes - 1)) / kRowBytes);
-        g.P = g.R * kRowBytes - p.len;
-        g.s16 = (uint32_t)(((uintptr_t)p.addr - g.P) & 15u);
-        return g;
-    };
-    auto to_rows = [&](ChainPos &p) {
-        if (p.q < p.re) {
-            p.kind = 0u;
-            p.j = __builtin_amdgcn_readfirstlane((uint32_t)rlist[p.q]);
-            const SDesc sd = sdesc[p.j];
-            p.addr = (gbyte *)(uintptr_t)uniform64(sd.addr);
-            p.len = uniform(sd.len);
-            p.partial = uniform(sd.partial);
-            p.r = 0u;
-        } else {
-            p.kind = 2u;
-        }
-    };
-    auto next = [&](ChainPos &p) {
-        if (p.kind == 2u) return;
-        if (p.kind == 0u) {
-            if ((uint64_t)(p.r + 1) * kRowBytes < p.len) {
-                ++p.r;
-                return;
-            }
-            ++p.q;
-        } else {
-            p.p += 4u;
-            if (p.p < p.pe) return;
-        }
-        to_rows(p);
-    };
-    auto start = [&](uint32_t ch) -> ChainPos {
-        const uint32_t b0 = bound[ch], b1 = bound[ch + 1];
-        ChainPos p{spk[b0], spk[b1], srw[b0], srw[b1], 1u, 0u, 0u, nullptr, 0u, 0u};
-        p.p = uniform(p.p);
-        p.pe = uniform(p.pe);
-        p.q = uniform(p.q);
-        p.re = uniform(p.re);
-        if (p.p >= p.pe) to_rows(p);
-        return p;
-    };
-    ChainPos pi[2] = {start(2 * wave), start(2 * wave + 1)};
-    if (pi[0].kind == 2u && pi[1].kind == 2u) return;
-    ChainPos pp[2] = {pi[0], pi[1]};  // process side: the same sequence, kD steps behind
-
-    // this lane's pack member: plist[p + (lane >> 4)] (none past pe: j = kFragsPerWg, len 0)
-    struct Member {
-        uint32_t j, len, partial;
-        gbyte *addr;
-    };
-    auto member = [&](const ChainPos &t) -> Member {
-        const uint32_t i = t.p + ((uint32_t)lane >> 4);
-        Member m{kFragsPerWg, 0u, 0u, nullptr};
-        if (i < t.pe) {
-            m.j = plist[i];
-            const SDesc sd = sdesc[m.j];
-            m.addr = (gbyte *)(uintptr_t)sd.addr;
-            m.len = sd.len;
-            m.partial = sd.partial;
-        }
-        return m;
-    };
-    gbyte *zero = (gbyte *)(img + kImgZero);
-    auto addrs = [&](const ChainPos &t) -> RowAddrs {
-        RowAddrs a;
-        if (t.kind == 1u) {
-            const Member p = member(t);
-            a = pack_row_addrs(p.addr, p.len, (uint32_t)lane & 15u, zero);
-        } else if (t.kind == 0u) {
-            a = frag_row_addrs(geom(t), t.r, lane, zero);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 5; ++q) a.p[q] = zero;
-        }
-        return a;
-    };
-
-    RawRow ring[kD][2];
-#pragma unroll
-    for (int q = 0; q < kD; ++q) {
-        if (q > 0) {
-            next(pi[0]);
-            next(pi[1]);
-        }
-        const RowAddrs a0 = addrs(pi[0]), a1 = addrs(pi[1]);
-        issue_row5(a0, ring[q][0]);
-        issue_row5(a1, ring[q][1]);
-    }
-
-    const CrcLane k = make_lane(lane);
-    uint32_t C[2] = {0u, 0u};  // registers of the chains' current multi-row fragments
-    // data and starting register of a task's row (pack rows: the group's own frame)
-    auto prepare = [&](const RawRow &raw, const ChainPos &t, uint32_t &c0, uint32_t d[16]) {
-        if (t.kind == 1u) {
-            const Member p = member(t);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                d[4 * q + 0] = raw.q[q].x;
-                d[4 * q + 1] = raw.q[q].y;
-                d[4 * q + 2] = raw.q[q].z;
-                d[4 * q + 3] = raw.q[q].w;
-            }
-            const uint32_t g = (uint32_t)lane & 15u, P = kPackBytes - p.len;
-            if ((P & 63u) == 0) {
-                c0 = (g == (P >> 6)) ? __builtin_bswap32(p.partial) : 0u;
-            } else {
-                c0 = 0;
-                RowGeom rg{1u, P, 0u};
-                crc_inject(d, rg, p.partial, (int)g);
-            }
-            return;
-        }
-        const FragGeom g = geom(t);
-        finish_frag_row(g, t.r, lane, raw, d);
-        if (t.r == 0) {
-            if ((g.P & 63u) == 0) {  // the register enters as lane P/64's starting value
-                c0 = ((uint32_t)lane == (g.P >> 6)) ? __builtin_bswap32(g.partial) : 0u;
-            } else {
-                c0 = 0;
-                RowGeom rg{g.R, g.P, g.s16};
-                crc_inject(d, rg, g.partial, lane);
-            }
-        } else {
-            c0 = horner_shift(lds, c0);
-            if (t.r == 1 && g.P > (uint32_t)kRowBytes - 4 && lane == 0)  // register bytes spill into row 1
-                d[0] ^= __builtin_bswap32(g.partial) >> (8 * (kRowBytes - g.P));
-        }
-    };
-    auto finish = [&](const ChainPos &t, uint32_t c) {
-        if (t.kind == 1u) {
-            const Member p = member(t);
-            const uint32_t g = (uint32_t)lane & 15u;
-            CrcLane kq = k;
-            kq.comb_base = 448u + 4u * g;  // lane 48 + g's combine column: shift by 64*(15-g)
-            const uint32_t x = row16_xor(lane_combine(lds, kq, c));
-            if (g == 0 && p.j < kFragsPerWg) out[base + p.j] = __builtin_bswap32(x);
-        } else if ((uint64_t)(t.r + 1) * kRowBytes >= t.len) {
-            const uint32_t x = wave_xor(lane_combine(lds, k, c));
-            if (lane == 0) {
-                uint32_t res = __builtin_bswap32(x);
-                if (t.len < 4) res ^= t.partial << (8 * t.len);
-                out[base + t.j] = res;
-            }
-        }
-    };
-    auto process = [&](RawRow (&raw)[2]) {
-        if constexpr (kAbl == 1) {  // keep the loaded data live, nothing else
-            uint32_t x = 0;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) x ^= raw[0].q[q].x ^ raw[1].q[q].w;
-            C[0] ^= x;
-            if (C[0] == 0x9E3779B9u && lane == 64) out[0] = C[1];
-            return;
-        }
-        uint32_t d0[16], d1[16];
-        uint32_t c0 = C[0], c1 = C[1];
-        if (pp[0].kind != 2u) {
-            prepare(raw[0], pp[0], c0, d0);
-        } else {
-#pragma unroll
-            for (int w = 0; w < 16; ++w) d0[w] = 0u;
-        }
-        if (pp[1].kind != 2u) {
-            prepare(raw[1], pp[1], c1, d1);
-        } else {
-#pragma unroll
-            for (int w = 0; w < 16; ++w) d1[w] = 0u;
-        }
-        if constexpr (kAbl == 2) {
-#pragma unroll
-            for (int w = 0; w < 16; ++w) {
-                c0 ^= d0[w];
-                c1 ^= d1[w];
-            }
-        } else {
-            crc_piece2(lds, k, c0, d0, c1, d1);  // a null chain computes garbage, never used
-        }
-        if (pp[0].kind == 0u) C[0] = c0;
-        if (pp[1].kind == 0u) C[1] = c1;
-        if (pp[0].kind != 2u) finish(pp[0], c0);
-        if (pp[1].kind != 2u) finish(pp[1], c1);
-    };
-    constexpr int kL = 10;  // loads per step (two rows)
-#define LAMPI_FRAG_STEP(S)                                                            \
-    if constexpr ((S) < kD) {                                                         \
-        asm volatile("s_waitcnt vmcnt(%10)"                                           \
-                     : "+v"(ring[(S) % kD][0].q[0]), "+v"(ring[(S) % kD][0].q[1]),    \
-                       "+v"(ring[(S) % kD][0].q[2]), "+v"(ring[(S) % kD][0].q[3]),    \
-                       "+v"(ring[(S) % kD][0].q[4]), "+v"(ring[(S) % kD][1].q[0]),    \
-                       "+v"(ring[(S) % kD][1].q[1]), "+v"(ring[(S) % kD][1].q[2]),    \
-                       "+v"(ring[(S) % kD][1].q[3]), "+v"(ring[(S) % kD][1].q[4])     \
-                     : "n"((kD - 1) * kL)                                             \
-                     : "memory");                                                     \
-        if (pp[0].kind == 2u && pp[1].kind == 2u) break;                              \
-        process(ring[(S) % kD]);                                                      \
-        next(pp[0]);                                                                  \
-        next(pp[1]);                                                                  \
-        next(pi[0]);                                                                  \
-        next(pi[1]);                                                                  \
-        {                                                                             \
-            const RowAddrs a0 = addrs(pi[0]), a1 = addrs(pi[1]);                      \
-            issue_row5(a0, ring[(S) % kD][0]);                                        \
-            issue_row5(a1, ring[(S) % kD][1]);                                        \
-        }                                                                             \
-    }
-    for (;;) {
-        LAMPI_FRAG_STEP(0)
-        LAMPI_FRAG_STEP(1)
-        LAMPI_FRAG_STEP(2)
-        LAMPI_FRAG_STEP(3)
-        LAMPI_FRAG_STEP(4)
-        LAMPI_FRAG_STEP(5)
-    }
-#undef LAMPI_FRAG_STEP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the rows in flight before exit
 }
 
 // ---- CRC, general fragments as piece streams (descriptor batches, ragged messages) ---------
@@ -2594,7 +2129,7 @@ static uint32_t frags_per_wg(size_t n) {
 }
 
 // crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_ablation.hip)
-constexpr int kStreamD = 3, kStreamK = 1;
+constexpr int kStreamD = 2, kStreamK = 1;
 
 static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg - 1) / fpg)); }
 

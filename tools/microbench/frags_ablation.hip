@@ -1,8 +1,9 @@
-// frags_ablation.hip -- crc_frags_kernel (the general-fragment product kernel) on config C
+// frags_ablation.hip -- crc_stream_kernel (the general-fragment product kernel) on config C
 // (659,114 Zipf-sized fragments, 4 GiB) and on 4M x 4 KiB descriptors (config B through
-// descriptors), with ablated variants: loads + task walk only, and no table lookups; the
-// regular kernel on the uniform batch for comparison.  Checksums of the product variant are
-// compared with the regular kernel's on the uniform batch.
+// descriptors): ablated variants (loads + task walk only; no table lookups), ring depth, chains
+// per wave, fragments per workgroup and the occupancy sweep; the regular kernel on the uniform
+// batch for comparison.  Checksums of the product variant are compared with the regular
+// kernel's on the uniform batch.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 frags_ablation.hip -o frags_ablation
 #include "../../lampi_amd/csrc/crc_tables.cc"
 #include "../../lampi_amd/csrc/frag_csum.hip"
@@ -53,18 +54,11 @@ static std::vector<uint32_t> zipf_lengths(uint64_t min_total) {  // SURVEY.md 8(
     return out;
 }
 
-template <int kAbl, int kD = 3>
-static void launch(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint32_t *out, uint32_t fpg = 0,
-                   size_t pad_lds = 0) {
-    if (fpg == 0) fpg = frags_per_wg(n);
-    hipLaunchKernelGGL((crc_frags_kernel<DescSource, kD, kAbl>), frags_grid(n, fpg), dim3(kBlock), pad_lds, 0,
-                       DescSource{d}, n, fpg, img, out);
-}
-
 template <int kAbl, int kD = 2, int kK = 2>
-static void launch_stream(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint32_t *out, uint32_t fpg = 0) {
+static void launch_stream(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint32_t *out, uint32_t fpg = 0,
+                          size_t pad_lds = 0) {
     if (fpg == 0) fpg = frags_per_wg(n);
-    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kD, kAbl, kK>), frags_grid(n, fpg), dim3(512 / kK), 0, 0,
+    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kD, kAbl, kK>), frags_grid(n, fpg), dim3(512 / kK), pad_lds, 0,
                        DescSource{d}, n, fpg, img, out);
 }
 
@@ -72,13 +66,6 @@ template <int kD, int kK>
 static int stream_vgprs() {
     hipFuncAttributes a;
     CK(hipFuncGetAttributes(&a, (const void *)crc_stream_kernel<DescSource, kD, 0, kK>));
-    return a.numRegs;
-}
-
-template <int kD>
-static int vgprs_of() {
-    hipFuncAttributes a;
-    CK(hipFuncGetAttributes(&a, (const void *)crc_frags_kernel<DescSource, kD, 0>));
     return a.numRegs;
 }
 
@@ -137,44 +124,39 @@ int main() {
         struct V {
             const char *name;
             std::function<void()> go;
-        } vs[] = {{"stream K2 kD2 (product)", [&] { launch_stream<0, 2, 2>(d, n, dimg, out); }},
-                  {"stream K2 kD2 no lookups", [&] { launch_stream<2, 2, 2>(d, n, dimg, out); }},
-                  {"stream K2 kD2 loads+tasks", [&] { launch_stream<1, 2, 2>(d, n, dimg, out); }},
-                  {"stream K2 kD3", [&] { launch_stream<0, 3, 2>(d, n, dimg, out); }},
-                  {"stream K1 kD2", [&] { launch_stream<0, 2, 1>(d, n, dimg, out); }},
-                  {"stream K1 kD3", [&] { launch_stream<0, 3, 1>(d, n, dimg, out); }},
-                  {"stream K1 kD4", [&] { launch_stream<0, 4, 1>(d, n, dimg, out); }},
-                  {"stream K1 kD3 no lookups", [&] { launch_stream<2, 3, 1>(d, n, dimg, out); }},
-                  {"stream K1 kD3 loads+tasks", [&] { launch_stream<1, 3, 1>(d, n, dimg, out); }},
-                  {"stream K1 kD2 fpg 128", [&] { launch_stream<0, 2, 1>(d, n, dimg, out, 128); }},
-                  {"stream K1 kD2 fpg 64", [&] { launch_stream<0, 2, 1>(d, n, dimg, out, 64); }},
-                  {"stream K1 kD3 fpg 128", [&] { launch_stream<0, 3, 1>(d, n, dimg, out, 128); }},
-                  {"stream K1 kD2 fpg 128 loads+tasks", [&] { launch_stream<1, 2, 1>(d, n, dimg, out, 128); }},
-                  {"frame kernel", [&] { launch<0>(d, n, dimg, out); }},
-                  {"no lookups", [&] { launch<2>(d, n, dimg, out); }},
-                  {"loads + task walk", [&] { launch<1>(d, n, dimg, out); }}};
+        } vs[] = {{"product (K1 kD2)", [&] { launch_stream<0, 2, 1>(d, n, dimg, out); }},
+                  {"no lookups", [&] { launch_stream<2, 3, 1>(d, n, dimg, out); }},
+                  {"loads + tasks", [&] { launch_stream<1, 3, 1>(d, n, dimg, out); }},
+                  {"K1 kD3", [&] { launch_stream<0, 3, 1>(d, n, dimg, out); }},
+                  {"K1 kD4", [&] { launch_stream<0, 4, 1>(d, n, dimg, out); }},
+                  {"K2 kD2", [&] { launch_stream<0, 2, 2>(d, n, dimg, out); }},
+                  {"K2 kD3", [&] { launch_stream<0, 3, 2>(d, n, dimg, out); }},
+                  {"K1 kD3 fpg 64", [&] { launch_stream<0, 3, 1>(d, n, dimg, out, 64); }},
+                  {"K1 kD3 fpg 128", [&] { launch_stream<0, 3, 1>(d, n, dimg, out, 128); }}};
         for (auto &v : vs) {
             const double ms = time_ms(v.go, 15);
-            printf("%-26s %-20s %8.3f ms  %6.1f%% of 8 TB/s\n", cname, v.name, ms, total / (ms * 1e-3) / 8e12 * 100);
+            printf("%-24s %-18s %8.3f ms  %6.1f%% of 8 TB/s\n", cname, v.name, ms, total / (ms * 1e-3) / 8e12 * 100);
         }
-        // schedule / occupancy sweep: ring depth (VGPRs), fragments per workgroup, workgroups per CU
-        // (1 per CU forced with extra LDS); waves per CU = 4 x workgroups per CU (LDS-capped)
-        for (int wgcu : {2, 1}) {
-            if (!getenv("SWEEP")) break;
-            for (uint32_t fpg : {64u, 128u, 256u}) {
-                const size_t pad = wgcu == 1 ? (16u << 10) : 0;
-                const double m2 = time_ms([&] { launch<0, 2>(d, n, dimg, out, fpg, pad); }, 9);
-                const double m3 = time_ms([&] { launch<0, 3>(d, n, dimg, out, fpg, pad); }, 9);
-                const double m4 = time_ms([&] { launch<0, 4>(d, n, dimg, out, fpg, pad); }, 9);
-                printf("%-26s sweep: %d waves/CU, fpg %3u: kD=2 (%d VGPRs) %5.1f%%  kD=3 (%d) %5.1f%%  kD=4 (%d) %5.1f%%\n",
-                       cname, 4 * wgcu, fpg, vgprs_of<2>(), total / (m2 * 1e-3) / 8e12 * 100, vgprs_of<3>(),
-                       total / (m3 * 1e-3) / 8e12 * 100, vgprs_of<4>(), total / (m4 * 1e-3) / 8e12 * 100);
-            }
+        // occupancy sweep: waves per CU = waves per workgroup x workgroups per CU;
+        // LDS (~76 KiB per workgroup) allows two workgroups per CU, extra dynamic LDS forces one.
+        // 32 waves per CU would need <= 40 KiB per workgroup: the 64 KiB of tables rule it out.
+        struct O {
+            int waves;
+            const char *how;
+            std::function<void()> go;
+        } occ[] = {{4, "K2 (4 waves/WG), 1 WG/CU", [&] { launch_stream<0, 3, 2>(d, n, dimg, out, 0, 16u << 10); }},
+                   {8, "K2 (4 waves/WG), 2 WG/CU", [&] { launch_stream<0, 3, 2>(d, n, dimg, out); }},
+                   {8, "K1 (8 waves/WG), 1 WG/CU", [&] { launch_stream<0, 3, 1>(d, n, dimg, out, 0, 16u << 10); }},
+                   {16, "K1 (8 waves/WG), 2 WG/CU", [&] { launch_stream<0, 3, 1>(d, n, dimg, out); }}};
+        for (auto &o : occ) {
+            const double ms = time_ms(o.go, 9);
+            printf("%-24s occupancy %2d waves/CU (%s): %6.1f%% of 8 TB/s\n", cname, o.waves, o.how,
+                   total / (ms * 1e-3) / 8e12 * 100);
         }
         if (cfg == 1) {
             const double ms = time_ms([&] { launch_crc_regular(buf, n, 4096, 0xFFFFFFFFu, ref, dimg, 512, 0); }, 15);
-            printf("%-26s %-20s %8.3f ms  %6.1f%% of 8 TB/s\n", cname, "regular kernel", ms, total / (ms * 1e-3) / 8e12 * 100);
-            launch<0>(d, n, dimg, out);
+            printf("%-24s %-18s %8.3f ms  %6.1f%% of 8 TB/s\n", cname, "regular kernel", ms, total / (ms * 1e-3) / 8e12 * 100);
+            launch_stream<0, 3, 1>(d, n, dimg, out);
             CK(hipDeviceSynchronize());
             std::vector<uint32_t> a(n), b(n);
             CK(hipMemcpy(a.data(), out, n * 4, hipMemcpyDeviceToHost));
