@@ -322,6 +322,7 @@ def run_mixed(args):
     got = shard.digest(dv.as_u32(out), np.arange(lens.size, dtype=np.uint64))
     achieved = total / kern_avg_s / 1e9
     meta = total + 20 * lens.size  # + the 16-byte descriptor read and the 4-byte result write
+    traffic = read_traffic("crc_configC")
     print(json.dumps({
         "metric": METRIC, "value": round(total / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
@@ -330,7 +331,10 @@ def run_mixed(args):
         "config": {"workload": f"config C: {lens.size} mixed fragments, {total} B, one descriptor batch "
                                "(lampi_frag_csum_batch)", "fragments": int(lens.size), "bytes": total},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "crc_stream_kernel",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
+                     "traffic_source": None if traffic is None else traffic.get("source"),
+                     "kernel": "crc_stream_kernel",
                      "incl_metadata": {"bytes": meta, "achieved": round(meta / kern_avg_s / 1e9, 1),
                                        "frac": round(meta / kern_avg_s / 1e9 / HBM_PEAK_GBS, 4)},
                      "kernel_avg_ms": round(kern_avg_s * 1e3, 4),

@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
-#   smoke | tests | tests_bcopy | bench | bench16k | benchsum | benchC | benchD | bcopy | prof | pmc | e2e | microbench
+#   smoke | tests | tests_bcopy | bench | bench16k | benchsum | benchC | benchD | bcopy | prof | profC | pmc | pmcC | e2e | microbench
 # A test failure (exit 1) lets later steps run; a fault, abort, segfault, timeout or
 # kill (exit >= 124, 134, 139, ...) ends the session immediately.
 set -u
@@ -38,6 +38,10 @@ for step in "$@"; do
             -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline &&
          run pmc_ea 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv \
             -d gpurun_out/pmc_ea -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    profC) run profC 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profC -o run \
+            -- python3 bench.py --config C --steps 20 ;;
+    pmcC) run pmcC_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcC_fetch -o run \
+            -- python3 bench.py --config C --steps 5 --warmup 1 ;;
     pmcsq) for cfg in B C D; do
              extra="--no-cpu-baseline"; [ $cfg = C ] && extra="--config C"; [ $cfg = D ] && extra="--desc --no-cpu-baseline"
              run pmc_sq$cfg 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
