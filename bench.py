@@ -304,14 +304,15 @@ def run_mixed(args):
     descs = dv.make_descs(buf, offs, lens)
     out = torch.empty(lens.size, dtype=torch.int32, device="cuda")
     stream = torch.cuda.current_stream()
+    mode = dv.CRC32 if args.mode == "crc" else dv.SUM32
     for _ in range(args.warmup):
-        dv.frag_csum_batch(descs, mode=dv.CRC32, out=out)
+        dv.frag_csum_batch(descs, mode=mode, out=out)
     torch.cuda.synchronize()
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
     evs[0].record(stream)
     for i in range(args.steps):
-        dv.frag_csum_batch(descs, mode=dv.CRC32, out=out)
+        dv.frag_csum_batch(descs, mode=mode, out=out)
         evs[i + 1].record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -319,10 +320,16 @@ def run_mixed(args):
     kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
     with open(os.path.join(ROOT, "tests", "golden", "fixtures.json")) as f:
         gold = json.load(f)["digests"]["C"]
-    got = shard.digest(dv.as_u32(out), np.arange(lens.size, dtype=np.uint64))
+    vals = dv.as_u32(out)
+    got = shard.digest(vals, np.arange(lens.size, dtype=np.uint64))
+    if mode == dv.CRC32:
+        want = (gold["crc_xor"], gold["crc_wsum"])
+    else:  # SUM: total of the sums and the weighted sum
+        got = (int(np.sum(vals, dtype=np.uint64) & 0xFFFFFFFF), got[1])
+        want = (gold["sum_total"], gold["sum_wsum"])
     achieved = total / kern_avg_s / 1e9
     meta = total + 20 * lens.size  # + the 16-byte descriptor read and the 4-byte result write
-    traffic = read_traffic("crc_configC")
+    traffic = read_traffic("crc_configC") if mode == dv.CRC32 else None
     print(json.dumps({
         "metric": METRIC, "value": round(total / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4),
@@ -334,15 +341,16 @@ def run_mixed(args):
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
                      "traffic_source": None if traffic is None else traffic.get("source"),
-                     "kernel": "crc_stream_kernel",
+                     "kernel": "crc_stream_kernel" if mode == dv.CRC32 else "sum_rows_kernel",
                      "incl_metadata": {"bytes": meta, "achieved": round(meta / kern_avg_s / 1e9, 1),
                                        "frac": round(meta / kern_avg_s / 1e9 / HBM_PEAK_GBS, 4)},
                      "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                      "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2],
                                                                           max(kern_ms))],
                      "algorithmic_bytes_per_launch": total},
-        "parity": {"check": "full digest vs tests/golden/fixtures.json (config C)", "xor": f"{got[0]:08x}",
-                   "wsum": f"{got[1]:08x}", "ok": got == (gold["crc_xor"], gold["crc_wsum"])},
+        "parity": {"check": f"full digest vs tests/golden/fixtures.json (config C, {args.mode})",
+                   ("xor" if mode == dv.CRC32 else "sum"): f"{got[0]:08x}", "wsum": f"{got[1]:08x}",
+                   "ok": got == want},
         "cpu_baseline": None}))
 
 

@@ -786,23 +786,25 @@ __device__ __forceinline__ uint32_t combine_at(const uint32_t *lds, uint32_t b, 
 
 __device__ __forceinline__ uint32_t comb_col(uint32_t l) { return (l >> 5) * 256u + 128u + (l & 31u) * 4u; }
 
-// inclusive XOR scan inside segments: lane l gets the XOR of lanes [ss, l] (pos = l - ss).
-// Row-local steps by row_shr (sources outside the row read 0), then row_bcast:15 / :31 carry
-// across rows for lanes whose segment started in an earlier row.
-__device__ __forceinline__ uint32_t seg_scan_xor(uint32_t v, uint32_t pos, uint32_t lane) {
+// inclusive scan inside segments (XOR for CRC values, + for sums): lane l gets the combination of
+// lanes [ss, l] (pos = l - ss).  Row-local steps by row_shr (sources outside the row read 0),
+// then row_bcast:15 / :31 carry across rows for lanes whose segment started in an earlier row.
+template <bool kAdd>
+__device__ __forceinline__ uint32_t seg_scan(uint32_t v, uint32_t pos, uint32_t lane) {
+    auto op = [](uint32_t a, uint32_t b) { return kAdd ? a + b : a ^ b; };
     uint32_t t;
     t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v ^= pos >= 1u ? t : 0u;
+    v = op(v, pos >= 1u ? t : 0u);
     t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v ^= pos >= 2u ? t : 0u;
+    v = op(v, pos >= 2u ? t : 0u);
     t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v ^= pos >= 4u ? t : 0u;
+    v = op(v, pos >= 4u ? t : 0u);
     t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v ^= pos >= 8u ? t : 0u;
+    v = op(v, pos >= 8u ? t : 0u);
     t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    v ^= pos > (lane & 15u) ? t : 0u;
+    v = op(v, pos > (lane & 15u) ? t : 0u);
     t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-    v ^= pos > (lane & 31u) ? t : 0u;
+    v = op(v, pos > (lane & 31u) ? t : 0u);
     return v;
 }
 
@@ -848,7 +850,7 @@ struct RowsN4 {
 };
 
 // kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way
-template <bool kMis, int kD, int kAbl, int kK>
+template <bool kMis, int kD, int kAbl, int kK, bool kSum>
 __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDesc *sdesc, const uint64_t *sstart,
                                             const uint16_t *sj, uint32_t *marks, const StreamChain *sch,
                                             uint32_t *sopen, uint32_t *shead, gbyte *zero, uint32_t *sres,
@@ -915,11 +917,16 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             const uint32_t k0 = uniform((uint32_t)(c.rs - sstart[lr]));  // lane 0's piece
             t.one = (lr & 0xFFFFu) | (uniform(sj[lr]) << 16);
             const uint32_t np = (uint32_t)(((uint64_t)len + 63u) >> 6);
-            const uint32_t P = (np << 6) - len;
+            // CRC: pieces right-aligned (P leading zeros); SUM: left-aligned on the word grid
+            const uint32_t P = kSum ? 0u : (np << 6) - len;
             const long long o0 = (long long)k0 * 64 - (long long)P;
             gbyte *pa = (gbyte *)(uintptr_t)addr + o0 + lane * 64u;
             uint32_t sh = 0u;
-            if constexpr (!kMis) {
+            if constexpr (!kMis && kSum) {  // chunks past the fragment end read zeros
+                const long long o = o0 + (long long)lane * 64;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) A.p[q] = (o + 16 * q < (long long)len) ? pa + 16 * q : zero;
+            } else if constexpr (!kMis) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) A.p[q] = pa + 16 * q;
                 if (o0 + 16 <= 0) {  // lane 0's first piece starts with whole chunks of padding
@@ -941,11 +948,15 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             const bool first = k == 0u, last = k + 1u == np, second = k == 1u;
             t.info = (lr & 0x1FFu) | (63u << 9) | (sh << 21) | (first ? kTfFirst : 0u) | (last ? kTfLast : 0u) |
                      (second ? kTfSecond : 0u);
-            t.sreg = (first && P == 0u) ? __builtin_bswap32(partial) : 0u;
+            t.sreg = (!kSum && first && P == 0u) ? __builtin_bswap32(partial) : 0u;
             t.M = M;
-            const bool needmask = k0 == 0u && (kMis ? P != 0u : (P & 15u) != 0u);
-            const bool needinj = (k0 == 0u && P != 0u) || (k0 <= 1u && np > 1u && P > 60u);
-            t.fix = (needmask ? 1u : 0u) | (needinj ? 2u : 0u);
+            if constexpr (kSum) {  // the last piece, if in this row and partial, is masked
+                t.fix = (k0 + 64u >= np && (len & 63u) != 0u) ? 1u : 0u;
+            } else {
+                const bool needmask = k0 == 0u && (kMis ? P != 0u : (P & 15u) != 0u);
+                const bool needinj = (k0 == 0u && P != 0u) || (k0 <= 1u && np > 1u && P > 60u);
+                t.fix = (needmask ? 1u : 0u) | (needinj ? 2u : 0u);
+            }
             c.cur += (uint32_t)M;
             c.rs += 64u;
             return A;
@@ -956,11 +967,14 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         const StreamDesc D = sdesc[lr];
         const uint32_t k = (uint32_t)(c.rs + lane - sstart[lr]);
         const uint32_t np = (uint32_t)(((uint64_t)D.len + 63u) >> 6);
-        const uint32_t P = (np << 6) - D.len;  // mod 2^32: always < 64
+        const uint32_t P = kSum ? 0u : (np << 6) - D.len;  // mod 2^32: always < 64
         const long long o = (long long)k * 64 - (long long)P;
         gbyte *pa = (gbyte *)(uintptr_t)D.addr + o;
         uint32_t sh = 0u;
-        if constexpr (!kMis) {
+        if constexpr (!kMis && kSum) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) A.p[q] = (!nul && o + 16 * q < (long long)D.len) ? pa + 16 * q : zero;
+        } else if constexpr (!kMis) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) A.p[q] = (!nul && o + 16 * q + 16 > 0) ? pa + 16 * q : zero;
         } else {
@@ -980,11 +994,15 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         const bool first = !nul && k == 0u, last = !nul && k + 1u == np, second = !nul && k == 1u;
         t.info = (lr & 0x1FFu) | (e << 9) | (ss << 15) | (sh << 21) | (first ? kTfFirst : 0u) |
                  (last ? kTfLast : 0u) | (nul ? kTfNull : 0u) | (second ? kTfSecond : 0u);
-        t.sreg = (first && P == 0u) ? __builtin_bswap32(D.partial) : 0u;
+        t.sreg = (!kSum && first && P == 0u) ? __builtin_bswap32(D.partial) : 0u;
         t.M = M;
-        const bool needmask = first && (kMis ? P != 0u : (P & 15u) != 0u);
-        const bool needinj = (first && P != 0u) || (second && P > 60u);
-        t.fix = (__builtin_amdgcn_ballot_w64(needmask) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(needinj) ? 2u : 0u);
+        if constexpr (kSum) {
+            t.fix = __builtin_amdgcn_ballot_w64(last && (D.len & 63u) != 0u) ? 1u : 0u;
+        } else {
+            const bool needmask = first && (kMis ? P != 0u : (P & 15u) != 0u);
+            const bool needinj = (first && P != 0u) || (second && P > 60u);
+            t.fix = (__builtin_amdgcn_ballot_w64(needmask) ? 1u : 0u) | (__builtin_amdgcn_ballot_w64(needinj) ? 2u : 0u);
+        }
         t.one = 0u;
         c.cur += (uint32_t)__popcll(M);
         c.rs += 64u;
@@ -1017,7 +1035,13 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 #pragma unroll
             for (int w = 0; w < 16; ++w) d[w] = __builtin_amdgcn_alignbyte(b[w + 1], b[w], sb);
         }
-        if (t.fix & 3u) {
+        if (kSum && (t.fix & 1u)) {  // zero the bytes of a partial last piece past the fragment end
+            const uint32_t rem = sdesc[t.info & 0x1FFu].len & 63u;
+            if ((t.info & kTfLast) && rem != 0u) {
+#pragma unroll
+                for (int w = 0; w < 16; ++w) d[w] &= byte_keep_mask(4 * w, 0, (long long)rem);
+            }
+        } else if (!kSum && (t.fix & 3u)) {
             const StreamDesc D = sdesc[t.info & 0x1FFu];
             const uint32_t P = (0u - D.len) & 63u;
             const bool first = (t.info & kTfFirst) != 0u;
@@ -1045,10 +1069,14 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             shead[ch] = x;
             return;
         }
-        const StreamDesc D = sdesc[li];
-        uint32_t res = __builtin_bswap32(x);
-        if (D.len < 4u) res ^= D.partial << (8 * D.len);
-        sres[sj[li]] = res;
+        if constexpr (kSum) {
+            sres[sj[li]] = x;
+        } else {
+            const StreamDesc D = sdesc[li];
+            uint32_t res = __builtin_bswap32(x);
+            if (D.len < 4u) res ^= D.partial << (8 * D.len);
+            sres[sj[li]] = res;
+        }
     };
     // segment values -> results and the carry of the open segment at lane 63.  v: the lane's
     // value shifted to its segment's end (combine column of lane 63 - (e - l); e = 63 in a
@@ -1056,15 +1084,15 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     auto finish = [&](int ch, const STask &t, uint32_t v, uint32_t &carry) {
         uint32_t x;
         if ((t.M & ~1ull) == 0ull) {  // one segment (never a fragment shorter than 4 bytes)
-            x = wave_xor(v);
+            x = kSum ? wave_add(v) : wave_xor(v);
             if (lane == 63u && (t.info & kTfLast)) {
                 if (mid[ch] && (t.one & 0xFFFFu) == head[ch])
                     shead[ch] = x;
                 else
-                    sres[t.one >> 16] = __builtin_bswap32(x);
+                    sres[t.one >> 16] = kSum ? x : __builtin_bswap32(x);
             }
         } else {
-            x = seg_scan_xor(v, lane - ((t.info >> 15) & 63u), lane);
+            x = seg_scan<kSum>(v, lane - ((t.info >> 15) & 63u), lane);
             if (((t.info >> 9) & 63u) == lane && (t.info & kTfLast)) result(ch, t.info & 0x1FFu, x);
             x = __builtin_amdgcn_readlane(x, 63);
         }
@@ -1102,7 +1130,12 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             C[c] = t[c].sreg;
             if (lane == 0u && !(t[c].info & (kTfFirst | kTfNull))) C[c] = carry[c];
         }
-        if constexpr (kAbl == 2) {
+        if constexpr (kSum) {
+#pragma unroll
+            for (int c = 0; c < kK; ++c)
+#pragma unroll
+                for (int w = 0; w < 16; w += 2) C[c] = C[c] + d[c][w] + d[c][w + 1];
+        } else if constexpr (kAbl == 2) {
 #pragma unroll
             for (int c = 0; c < kK; ++c)
 #pragma unroll
@@ -1114,7 +1147,8 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         }
         uint32_t v[kK];
 #pragma unroll
-        for (int c = 0; c < kK; ++c) v[c] = combine_at(lds, comb_col(lane + 63u - ((t[c].info >> 9) & 63u)), C[c]);
+        for (int c = 0; c < kK; ++c)
+            v[c] = kSum ? C[c] : combine_at(lds, comb_col(lane + 63u - ((t[c].info >> 9) & 63u)), C[c]);
 #pragma unroll
         for (int c = 0; c < kK; ++c) finish(c, t[c], v[c], carry[c]);
     };
@@ -1162,7 +1196,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 
 // kAbl (tools/microbench/frags_ablation.hip only): 1 = loads and task walk, no row work;
 // 2 = everything but the table lookups of the pieces.  kK: chains per wave (threads = 512 / kK).
-template <class Src, int kD = 3, int kAbl = 0, int kK = 2>
+template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false>
 __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n, uint32_t fpg,
                                                               const uint32_t *__restrict__ img,
                                                               uint32_t *__restrict__ out) {
@@ -1170,7 +1204,7 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
     constexpr uint32_t kThreads = 512 / kK, kWv = kThreads / 64;
     constexpr uint32_t kChains = kWv * kK;  // 8
     static_assert(kThreads >= kFragsPerWg, "one fragment per thread in the set-up");
-    __shared__ __attribute__((aligned(16))) uint32_t lds[65536 / 4];  // slicing + combine tables
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kSum ? 4 : 65536 / 4];  // slicing + combine tables
     __shared__ StreamDesc sdesc[kFragsPerWg + 1];
     __shared__ uint64_t sstart[kFragsPerWg + 1];  // first piece of list entry i (workgroup-relative)
     __shared__ uint16_t sj[kFragsPerWg];          // fragment (workgroup-relative) of list entry i
@@ -1188,7 +1222,9 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
     if (t < nwg) mine = src.get(base + t);
     if (t < kChains) chead[t] = 0u;
     auto nopre = [] {};
-    if constexpr (kThreads == 256) {
+    if constexpr (kSum) {
+        __syncthreads();
+    } else if constexpr (kThreads == 256) {
         stage_tables<0, decltype(nopre), 3>(lds, img, nopre);  // no Horner tables; waits for the descriptors too
     } else {
         if (t < 256) {  // the table builders are written for 256 threads
@@ -1201,9 +1237,10 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
         __syncthreads();
     }
     const bool ne = t < nwg && mine.len != 0u;              // list entries: the non-empty fragments
-    if (t < nwg && mine.len == 0u) sres[t] = mine.partial;  // uicrc(p, 0, s) == s
+    if (t < nwg && mine.len == 0u) sres[t] = kSum ? 0u : mine.partial;  // uicrc(p, 0, s) == s, uicsum(p, 0) == 0
     const uint64_t np = ne ? (((uint64_t)mine.len + 63u) >> 6) : 0ull;
-    const bool mis = ne && ((((uintptr_t)mine.addr) + mine.len) & 15u) != 0u;
+    // CRC pieces end at the fragment end, SUM pieces start at the fragment start
+    const bool mis = ne && ((((uintptr_t)mine.addr) + (kSum ? 0u : mine.len)) & 15u) != 0u;
     uint64_t ip = np;
     uint32_t ic = ne ? 1u : 0u;
 #pragma unroll
@@ -1269,10 +1306,10 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
     const bool anymis = __syncthreads_or(mis) != 0;
     gbyte *zero = (gbyte *)(img + kImgZero);
     if (anymis)
-        stream_body<true, kD, kAbl, kK>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+        stream_body<true, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                         sopen + kK * wave, shead + kK * wave, zero, sres, out);
     else
-        stream_body<false, kD, kAbl, kK>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+        stream_body<false, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                          sopen + kK * wave, shead + kK * wave, zero, sres, out);
     if (kAbl != 0) return;
     __syncthreads();
@@ -1288,12 +1325,12 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
                 const uint64_t lo = schain[c].rs, hi = schain[c].end;
                 if (hi == lo) continue;
                 if (ef <= hi) {
-                    C = shift_pieces(lds, img, C, ef - lo) ^ shead[c];
+                    C = kSum ? C + shead[c] : shift_pieces(lds, img, C, ef - lo) ^ shead[c];
                     break;
                 }
-                C = shift_pieces(lds, img, C, hi - lo) ^ sopen[c];
+                C = kSum ? C + sopen[c] : shift_pieces(lds, img, C, hi - lo) ^ sopen[c];
             }
-            sres[sj[f]] = __builtin_bswap32(C);
+            sres[sj[f]] = kSum ? C : __builtin_bswap32(C);
         }
     }
     __syncthreads();
@@ -2240,21 +2277,34 @@ hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t 
     return hipGetLastError();
 }
 
-hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, int grid, hipStream_t s) {
+hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
+                           hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
+    if (img) {  // piece streams (img: the zero chunk)
+        const uint32_t fpg = frags_per_wg(n);
+        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, true>), frags_grid(n, fpg),
+                           dim3(512 / kStreamK), 0, s, DescSource{d}, n, fpg, img, out);
+        return hipGetLastError();
+    }
     const uint32_t fpw = pick_fpw(n, 1);
     hipLaunchKernelGGL(sum_rows_kernel<DescSource>, grid_for(n, fpw), dim3(kBlock), 0, s, DescSource{d}, n, fpw, out);
     return hipGetLastError();
 }
 
-hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out, int grid,
-                          hipStream_t s) {
+hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out,
+                          const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
     if (msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 && ((uintptr_t)base & 15u) == 0 &&
         n <= 0xFFFFFFFFull) {
         return launch_regular<true>(base, n, frag_len, 0u, out, nullptr, s);
+    }
+    if (img) {
+        const uint32_t fpg = frags_per_wg(n);
+        hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, true>), frags_grid(n, fpg),
+                           dim3(512 / kStreamK), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
+        return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
     hipLaunchKernelGGL(sum_rows_kernel<MsgSource>, grid_for(n, fpw), dim3(kBlock), 0, s,

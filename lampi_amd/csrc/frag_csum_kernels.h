@@ -44,9 +44,12 @@ hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t
 hipError_t launch_sum64_desc(const lampi_frag_desc *d, size_t n, uint64_t *out, bool phased, hipStream_t s);
 hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t *src, uint64_t len, uint64_t plong,
                                uint64_t plen, uint64_t *out3, hipStream_t s);
-hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, int grid, hipStream_t s);
-hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out, int grid,
-                          hipStream_t s);
+// SUM per descriptor / per fragment of a message: piece streams when img (the table image, for its
+// zero chunk) is given, one wavefront per fragment (sum_rows_kernel) otherwise.
+hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
+                           hipStream_t s);
+hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out,
+                          const uint32_t *img, int grid, hipStream_t s);
 hipError_t launch_crc_combine(const uint32_t *vals, uint32_t n, const uint32_t *tabs, uint32_t npow,
                               uint32_t *out, hipStream_t s);
 hipError_t launch_sum_finish(const uint32_t *partials, uint32_t npart, const uint8_t *src, uint64_t len,

@@ -194,7 +194,7 @@ uint32_t device_sum(HostCtx &c, uint64_t len, unsigned int *pint, unsigned int *
     if (n) {
         LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc.data(), n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
                                    c.stream));
-        LAMPI_CHECK(launch_sum_desc(c.ddesc, n, c.dvals, grid, c.stream));
+        LAMPI_CHECK(launch_sum_desc(c.ddesc, n, c.dvals, nullptr, grid, c.stream));
     }
     uint32_t *out3 = c.dvals + n;
     LAMPI_CHECK(launch_sum_finish(c.dvals, n, c.dbuf, len, *pint, *plen, out3, c.stream));
@@ -340,10 +340,10 @@ int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
     hipStream_t s = (hipStream_t)stream;
-    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_desc(d_descs, n, d_out, crc_grid(dev), s));
     const uint32_t *img = nullptr;
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
+    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_desc(d_descs, n, d_out, img, crc_grid(dev), s));
     return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s));
 }
 
@@ -392,10 +392,10 @@ int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t 
     hipStream_t s = (hipStream_t)stream;
     const uint8_t *base = (const uint8_t *)d_msg;
     const int grid = crc_grid(dev);
-    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_msg(base, msg_len, frag_len, n, d_out, grid, s));
     const uint32_t *img = nullptr;
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
+    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_msg(base, msg_len, frag_len, n, d_out, img, grid, s));
     const bool regular = msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 &&
                          ((uintptr_t)base & 15u) == 0;
     if (regular) return to_int(launch_crc_regular(base, n, frag_len, partial, d_out, img, grid, s));

@@ -131,8 +131,9 @@ def test_descriptor_batch_random(cuda, oracle):
         assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 @pytest.mark.parametrize("case", ["three", "aligned40", "mixed600", "huge_first"])
-def test_descriptor_batch_fragments_across_chains(cuda, oracle, case):
+def test_descriptor_batch_fragments_across_chains(cuda, oracle, case, mode):
     """The piece-stream kernel cuts a workgroup's pieces into eight chains of equal row counts, so
     a long fragment is checksummed in parts by several chains and joined at the end (stream_join,
     shifts by arbitrary piece counts).  Few fragments per workgroup and multi-MiB lengths make
@@ -162,18 +163,19 @@ def test_descriptor_batch_fragments_across_chains(cuda, oracle, case):
     host = base.cpu().numpy()
     parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
     descs = dv.make_descs(base, offs, lens, parts)
-    got = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.CRC32))
-    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32), 0)
+    got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
+    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
 
 
 @pytest.mark.parametrize("n", [30000, 300000])
-def test_descriptor_batch_small_fragment_packs(cuda, oracle, n):
-    """Fragments of 16..1024 bytes (multiples of 16, 16-byte aligned) go four to a row in lane
-    groups; mixed with unaligned, odd-length, empty and multi-row fragments in one batch, every
-    register random, so packs, partial packs and whole-row fragments interleave in every wave.
-    30,000 runs with 8 fragments per workgroup, 300,000 with the full 128 (frags_per_wg)."""
+def test_descriptor_batch_small_fragments(cuda, oracle, n):
+    """Fragments of 16..1024 bytes (multiples of 16, 16-byte aligned) mixed with unaligned,
+    odd-length, empty and multi-row fragments in one batch, every register random: rows hold many
+    fragment boundaries (the boundary-mask path and the segmented scan), with misaligned ones in
+    the same workgroups.  30,000 runs with 8 fragments per workgroup, 300,000 with the full 256
+    (frags_per_wg); both checksum modes."""
     import torch
 
     dv = _dv()
@@ -190,10 +192,11 @@ def test_descriptor_batch_small_fragment_packs(cuda, oracle, n):
     offs[kind == 6] |= np.uint64(1)                                          # misaligned small ones
     parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
     descs = dv.make_descs(base, offs, lens, parts)
-    got = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.CRC32))
-    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32), 0)
-    bad = np.nonzero(got != want)[0]
-    assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+    for mode in (dv.CRC32, dv.SUM32):
+        got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
+        want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == dv.CRC32 else None, mode)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(mode, int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
 
 
 def test_kat_check_values(cuda):
