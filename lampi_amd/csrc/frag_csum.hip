@@ -1195,14 +1195,14 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 }
 
 // kAbl (tools/microbench/frags_ablation.hip only): 1 = loads and task walk, no row work;
-// 2 = everything but the table lookups of the pieces.  kK: chains per wave (threads = 512 / kK).
-template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false>
-__global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n, uint32_t fpg,
-                                                              const uint32_t *__restrict__ img,
-                                                              uint32_t *__restrict__ out) {
+// 2 = everything but the table lookups of the pieces.  kK: chains per wave, kWv: waves per
+// workgroup (kWv * kK chains); kWaveCap > 0 asks the compiler for that many waves per SIMD.
+template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0>
+__global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kWaveCap > 0 ? kWaveCap : 1)))
+crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
     static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
-    constexpr uint32_t kThreads = 512 / kK, kWv = kThreads / 64;
-    constexpr uint32_t kChains = kWv * kK;  // 8
+    constexpr uint32_t kThreads = 64 * kWv;
+    constexpr uint32_t kChains = kWv * kK;
     static_assert(kThreads >= kFragsPerWg, "one fragment per thread in the set-up");
     __shared__ __attribute__((aligned(16))) uint32_t lds[kSum ? 4 : 65536 / 4];  // slicing + combine tables
     __shared__ StreamDesc sdesc[kFragsPerWg + 1];
@@ -1305,8 +1305,8 @@ __global__ void __launch_bounds__(512 / kK) crc_stream_kernel(Src src, size_t n,
     for (uint32_t i = t; i < kChains * 64; i += kThreads) marks[i] = 0u;
     const bool anymis = __syncthreads_or(mis) != 0;
     gbyte *zero = (gbyte *)(img + kImgZero);
-    if (anymis)
-        stream_body<true, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+    if (anymis)  // five loads per row: a one-slot ring keeps its registers within the aligned variant's
+        stream_body<true, 1, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                         sopen + kK * wave, shead + kK * wave, zero, sres, out);
     else
         stream_body<false, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
@@ -2156,17 +2156,19 @@ static uint32_t pick_fpw(size_t n, uint32_t R) {
 
 constexpr int kRegularChains = 2;
 
-// fragments per workgroup of crc_frags_kernel: 128, halved for small batches so that they still
-// spread over the chip (a 16 MiB chunk of 65,456-byte fragments is 256 fragments: 64
-// workgroups of four, one fragment per wave)
+// fragments per workgroup of crc_stream_kernel: 96 (measured: tools/microbench/frags_ablation.hip,
+// 12-wave workgroups -- 96 beat 64/128/192/256 on config C and on 4 KiB descriptors: shorter
+// workgroups shrink the end-of-kernel tail, and 96 uniform 4 KiB fragments are 8 rows per chain),
+// halved for small batches so that they still spread over the chip (a 16 MiB chunk of
+// 65,456-byte fragments is only 256 fragments)
 static uint32_t frags_per_wg(size_t n) {
-    uint32_t fpg = kFragsPerWg;
-    while (fpg > 4 && n / fpg < 2048) fpg >>= 1;
+    uint32_t fpg = 96;
+    while (fpg > 3 && n / fpg < 2048) fpg >>= 1;
     return fpg;
 }
 
 // crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_ablation.hip)
-constexpr int kStreamD = 2, kStreamK = 1;
+constexpr int kStreamD = 2, kStreamK = 1, kStreamWv = 12, kStreamCap = 6;
 
 static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg - 1) / fpg)); }
 
@@ -2177,7 +2179,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK>), frags_grid(n, fpg), dim3(512 / kStreamK), 0, s, DescSource{d}, n, fpg,
+    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg,
                        img, out);
     return hipGetLastError();
 }
@@ -2187,7 +2189,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     (void)grid;
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK>), frags_grid(n, fpg), dim3(512 / kStreamK), 0, s,
+    hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
                        MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
     return hipGetLastError();
 }
@@ -2283,8 +2285,8 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     if (n == 0) return hipSuccess;
     if (img) {  // piece streams (img: the zero chunk)
         const uint32_t fpg = frags_per_wg(n);
-        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, true>), frags_grid(n, fpg),
-                           dim3(512 / kStreamK), 0, s, DescSource{d}, n, fpg, img, out);
+        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, true, kStreamWv, kStreamCap>),
+                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
@@ -2302,8 +2304,8 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     }
     if (img) {
         const uint32_t fpg = frags_per_wg(n);
-        hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, true>), frags_grid(n, fpg),
-                           dim3(512 / kStreamK), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
+        hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, true, kStreamWv, kStreamCap>),
+                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);

@@ -30,7 +30,8 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     bench16k) run bench16k 600 python bench.py --frags 1048576 --frag-bytes 16384 --no-cpu-baseline ;;
     benchsum) run benchsum 600 python bench.py --mode sum --no-cpu-baseline ;;
-    benchC) run benchC 600 python bench.py --config C --steps 10 ;;
+    benchC) run benchC 600 python bench.py --config C --steps 50 ;;
+    benchCsum) run benchCsum 600 python bench.py --config C --mode sum --steps 50 ;;
     benchD) run benchD 600 python bench.py --desc --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
             -- python3 bench.py --steps 20 --no-cpu-baseline ;;
