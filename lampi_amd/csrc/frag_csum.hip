@@ -330,7 +330,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Issues the combine basis, lets `pre` issue kPre more asm loads (the first rows of the
 // workgroup), builds the constant tables, waits for the basis only (vmcnt(kPre)), builds the
 // combine tables and ends with an LDS-only barrier.
-template <int kPre, class Pre, int kParts = 7, bool kCoal = false>
+template <int kPre, class Pre, int kParts = 7, bool kCoal = false, bool kSync = true>
 __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__restrict__ img, Pre pre) {
     CombineBasis cb = issue_combine_basis<kCoal>(img);
     pre();
@@ -339,7 +339,7 @@ __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__re
     if (kParts & 4) build_horner<kCoal>(b);
     asm volatile("s_waitcnt vmcnt(%2)" : "+v"(cb.a), "+v"(cb.b) : "n"(kPre) : "memory");
     if (kParts & 2) build_combine(b, cb);
-    lds_barrier();
+    if (kSync) lds_barrier();
 }
 
 // ---- loads --------------------------------------------------------------------------
@@ -1454,21 +1454,23 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // reads kV consecutive fragments one after the other instead of one.
 // kSum: the same schedule computes uicsum instead (no tables; the LDS stays allocated so the
 // kernel keeps the two-workgroups-per-CU occupancy the schedule was measured at).
+// kWv: waves per workgroup (the table builders use the first 256 threads); kCap > 0 asks the
+// compiler for that many waves per SIMD.
 template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
-          bool kSum = false>
-__global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
-                                                             uint32_t fpw, size_t frag_len, uint32_t partial,
-                                                             const uint32_t *__restrict__ img,
-                                                             uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
-                                                             size_t dst_stride) {
+          bool kSum = false, int kWv = kWaves, int kCap = 0>
+__global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kCap > 0 ? kCap : 1)))
+crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, size_t frag_len, uint32_t partial,
+                   const uint32_t *__restrict__ img, uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
+                   size_t dst_stride) {
     constexpr int K = kChains;
+    static_assert(kWv >= kWaves, "the table builders need 256 threads");
     constexpr int kS = kCoal ? kRowBytes / 4 : 16;  // chunk stride of a lane
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
     const uint32_t R = (uint32_t)(frag_len / kRowBytes);
-    const uint32_t f0 = wg_first(fpw);
-    // fragments of this wave: f0 + kWaves*j, j < nfr; processed in groups of K
-    const uint32_t nfr = f0 < n ? min(fpw, (n - f0 + kWaves - 1) / kWaves) : 0u;
+    const uint32_t f0 = uniform(blockIdx.x * kWv * fpw + (threadIdx.x >> 6));
+    // fragments of this wave: f0 + kWv*j, j < nfr; processed in groups of K
+    const uint32_t nfr = f0 < n ? min(fpw, (n - f0 + kWv - 1) / kWv) : 0u;
     const uint32_t ngrp = (nfr + K - 1) / K;
     const uint32_t lane_off = (uint32_t)lane * (kCoal ? kChunkBytes : kLaneBytes);
     const uint32_t vinit = __builtin_bswap32(partial);
@@ -1482,7 +1484,7 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
     // fragment of slot s in group i; missing fragments (past nfr) re-read slot 0 (no output)
     auto frag = [&](uint32_t i, uint32_t s) -> uint32_t {
         const uint32_t j = K * i + s;
-        return f0 + kWaves * (j < nfr ? j : K * i);
+        return f0 + kWv * (j < nfr ? j : K * i);
     };
     auto row_ptr = [&](uint32_t f, uint32_t r) -> gbyte * {
         return (gbyte *)(base + ((uint64_t)(nfr ? f : 0u) * frag_len + (uint64_t)r * kRowBytes + lane_off));
@@ -1506,9 +1508,15 @@ __global__ void __launch_bounds__(kBlock) crc_regular_kernel(const uint8_t *__re
     if constexpr (kSum) {
         issue_all();
         asm volatile("" ::"v"(lds) : "memory");  // the LDS array escapes: it stays allocated
-    } else if (kAblate != 2) {
+    } else if (kAblate != 2 && kWv == kWaves) {
         // every ring slot is in flight while the workgroup builds its tables
         stage_tables<4 * K * D, decltype(issue_all), 7, kCoal>(lds, img, issue_all);
+    } else if (kAblate != 2) {
+        if (threadIdx.x < 64 * kWaves)
+            stage_tables<4 * K * D, decltype(issue_all), 7, kCoal, false>(lds, img, issue_all);
+        else
+            issue_all();
+        lds_barrier();
     } else {
         stage_tables<0>(lds, img, [] {});
     }

@@ -50,6 +50,54 @@ def test_library_targets_gfx950():
         assert other not in data
 
 
+def _kernel_metadata():
+    """(name, private_segment_fixed_size, vgpr_count) of every kernel in the library's gfx950 code
+    object (offload bundle entry -> llvm-readelf --notes)."""
+    import re
+    import struct
+    import tempfile
+
+    import lampi_amd
+
+    data = open(lampi_amd._lib.LIB_PATH, "rb").read()
+    i = data.find(b"__CLANG_OFFLOAD_BUNDLE__")
+    assert i >= 0, "no offload bundle in the library"
+    n = struct.unpack_from("<Q", data, i + 24)[0]
+    p, co = i + 32, None
+    for _ in range(n):
+        off, size, ts = struct.unpack_from("<QQQ", data, p)
+        p += 24
+        triple = data[p:p + ts]
+        p += ts
+        if b"gfx950" in triple:
+            co = data[i + off:i + off + size]
+    assert co, "no gfx950 entry in the offload bundle"
+    with tempfile.NamedTemporaryFile(suffix=".co") as f:
+        f.write(co)
+        f.flush()
+        out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", f.name], capture_output=True,
+                             text=True, check=True).stdout
+    kernels = []
+    for e in re.split(r"\n  - \.agpr_count", out[out.find(".kernels:"):])[1:]:
+        kernels.append((re.search(r"\n    \.name:\s+(\S+)", e).group(1),
+                        int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", e).group(1)),
+                        int(re.search(r"\.vgpr_count:\s+(\d+)", e).group(1))))
+    return kernels
+
+
+def test_kernels_use_no_scratch():
+    """No kernel spills to scratch.  The row kernels issue their loads by inline asm and wait for
+    them with explicit vmcnt: a spill of a register that an asm load is still writing reads
+    garbage (a 64-VGPR experiment of the regular kernel that spilled faulted on the GPU).  The
+    stream kernel must also stay within 80 VGPRs (six waves per SIMD: the occupancy it was
+    measured at)."""
+    ks = _kernel_metadata()
+    assert len(ks) >= 20
+    assert [k for k in ks if k[1] != 0] == []
+    stream = [k for k in ks if "crc_stream_kernel" in k[0]]
+    assert stream and all(k[2] <= 80 for k in stream), stream
+
+
 def test_version_string_needs_no_gpu():
     import lampi_amd
 
