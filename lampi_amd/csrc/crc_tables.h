@@ -47,6 +47,9 @@ constexpr size_t kImgPow2Cols = kImgHorner16Cols + 32;
 //                            fragment from here
 constexpr size_t kImgZero = kImgPow2Cols + 1024;
 constexpr size_t kImgWords = kImgZero + 16;
+// The device allocation of the image is followed by kImgTrashBytes of writable scratch: lanes of
+// the fused copy with nothing to store write their 16 bytes there (per-lane slots, never read).
+constexpr size_t kImgTrashBytes = 1024;
 constexpr int kChunkBytes = 16;                          // coalesced layout: 16-byte chunks
 constexpr int kChunkStep = kRowBytes / 4 - kChunkBytes;  // 1008 zero bytes between a lane's chunks
 

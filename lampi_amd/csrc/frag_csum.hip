@@ -38,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdint>
 
 #include "crc_const.h"
@@ -755,6 +756,10 @@ __device__ __forceinline__ void issue_rowN(const AddrN<5> &a, RowN<5> &r) {
         : "memory");
 }
 
+__device__ __forceinline__ void issue_rowN(const AddrN<1> &a, RowN<1> &r) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(r.q[0]) : "v"(a.p[0]) : "memory");
+}
+
 // wait until at most N younger loads are outstanding; the two chains' registers of the slot are
 // threaded through so no use is scheduled above the wait
 template <int N>
@@ -772,6 +777,32 @@ __device__ __forceinline__ void wait_rows2(RowN<5> &a, RowN<5> &b) {
                    "+v"(b.q[1]), "+v"(b.q[2]), "+v"(b.q[3]), "+v"(b.q[4])
                  : "n"(N)
                  : "memory");
+}
+
+// Waits whose count depends on a run-time (wave-uniform) condition must be ONE asm statement: two
+// waits on two branches make the compiler merge the ring registers through a phi, and it then
+// copies registers whose loads are still in flight before the wait (garbage; seen in the ISA).
+// sel (SGPR): 0 -> vmcnt(A), 1 -> vmcnt(B), else vmcnt(C).
+#define LAMPI_WAIT_SEL_ASM                 \
+    "s_cmp_eq_u32 %[sel], 0\n\t"          \
+    "s_cbranch_scc1 1f\n\t"               \
+    "s_cmp_eq_u32 %[sel], 1\n\t"          \
+    "s_cbranch_scc1 2f\n\t"               \
+    "s_waitcnt vmcnt(%[c])\n\t"           \
+    "s_branch 3f\n"                        \
+    "1:\n\t"                              \
+    "s_waitcnt vmcnt(%[a])\n\t"           \
+    "s_branch 3f\n"                        \
+    "2:\n\t"                              \
+    "s_waitcnt vmcnt(%[b])\n"              \
+    "3:"
+
+template <int A, int B, int C>
+__device__ __forceinline__ void wait_sel(uint32_t sel, u32x4 &r) {
+    asm volatile(LAMPI_WAIT_SEL_ASM
+                 : "+v"(r)
+                 : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
+                 : "scc", "memory");
 }
 
 // shift by 64*(63 - l') zero bytes with lane l''s combine column (b = comb_col(l'))
@@ -850,12 +881,27 @@ struct RowsN4 {
 };
 
 // kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way
-template <bool kMis, int kD, int kAbl, int kK, bool kSum>
+// kPB: piece bytes (64; 16 for the fused copy, whose rows are then 1 KiB and every load and store
+// instruction of a wave covers 1 KiB).  kCopy (SUM, 16-byte pieces, 16-byte-aligned src and dst):
+// each lane stores its piece to dst + 16k with one asm store per row (lanes with nothing to store
+// write a per-lane trash slot, so the ring's waits count loads and stores exactly); a piece that
+// ends past copylen is stored byte by byte in addition (compiler stores: they only make the waits
+// stricter).
+struct StreamCopy {
+    uint64_t dst;
+    uint32_t copylen, pad;
+};
+
+template <bool kMis, int kD, int kAbl, int kK, bool kSum, int kPB = 64, bool kCopy = false>
 __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDesc *sdesc, const uint64_t *sstart,
                                             const uint16_t *sj, uint32_t *marks, const StreamChain *sch,
                                             uint32_t *sopen, uint32_t *shead, gbyte *zero, uint32_t *sres,
-                                            uint32_t *__restrict__ out) {
-    constexpr int NL = kMis ? 5 : 4;  // loads per row
+                                            uint32_t *__restrict__ out, const StreamCopy *scopy = nullptr,
+                                            uint8_t *trash = nullptr) {
+    static_assert(kPB == 64 || (kPB == 16 && kSum && !kMis && kK == 1), "16-byte pieces: aligned SUM only");
+    static_assert(!kCopy || kPB == 16, "the fused copy runs on 16-byte pieces");
+    constexpr int NL = kMis ? kPB / 16 + 1 : kPB / 16;  // loads per row
+    constexpr int kW = kPB / 4;                          // words per piece
     const uint32_t lane = threadIdx.x & 63u;
     struct SChain {
         uint64_t rs, end;  // piece index of the next row's first piece, of the chain's end
@@ -867,6 +913,8 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         uint32_t fix;         // bit 0: a first piece needs byte masking, bit 1: partial injected as data,
                               // bit 2: null row
         uint32_t one;         // one-segment rows: list entry | output index << 16
+        gwbyte *dst;          // kCopy: where the lane's piece goes (the trash slot when nothing)
+        uint32_t ncp;         // kCopy: bytes of the piece to copy (0..16)
     };
     SChain cs[kK];
     uint32_t head[kK], mid[kK];
@@ -892,6 +940,10 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             t.M = 0ull;
             t.fix = 4u;
             t.one = 0u;
+            if constexpr (kCopy) {
+                t.dst = (gwbyte *)(trash + 16u * lane);
+                t.ncp = 0u;
+            }
 #pragma unroll
             for (int q = 0; q < NL; ++q) A.p[q] = zero;
             return A;
@@ -916,16 +968,23 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             const uint32_t len = uniform(sdesc[lr].len), partial = uniform(sdesc[lr].partial);
             const uint32_t k0 = uniform((uint32_t)(c.rs - sstart[lr]));  // lane 0's piece
             t.one = (lr & 0xFFFFu) | (uniform(sj[lr]) << 16);
-            const uint32_t np = (uint32_t)(((uint64_t)len + 63u) >> 6);
+            const uint32_t np = (uint32_t)(((uint64_t)len + (kPB - 1)) / kPB);
             // CRC: pieces right-aligned (P leading zeros); SUM: left-aligned on the word grid
             const uint32_t P = kSum ? 0u : (np << 6) - len;
-            const long long o0 = (long long)k0 * 64 - (long long)P;
-            gbyte *pa = (gbyte *)(uintptr_t)addr + o0 + lane * 64u;
+            const long long o0 = (long long)k0 * kPB - (long long)P;
+            gbyte *pa = (gbyte *)(uintptr_t)addr + o0 + lane * (uint32_t)kPB;
             uint32_t sh = 0u;
+            if constexpr (kCopy) {
+                const StreamCopy cp = scopy[lr];
+                const uint64_t ob = (uint64_t)k0 * kPB + lane * (uint32_t)kPB;
+                const uint32_t cl = uniform(cp.copylen);
+                t.ncp = ob < cl ? (uint32_t)min<uint64_t>(cl - ob, 16u) : 0u;
+                t.dst = (gwbyte *)(uintptr_t)(uniform64(cp.dst) + ob);
+            }
             if constexpr (!kMis && kSum) {  // chunks past the fragment end read zeros
-                const long long o = o0 + (long long)lane * 64;
+                const long long o = o0 + (long long)lane * kPB;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) A.p[q] = (o + 16 * q < (long long)len) ? pa + 16 * q : zero;
+                for (int q = 0; q < kPB / 16; ++q) A.p[q] = (o + 16 * q < (long long)len) ? pa + 16 * q : zero;
             } else if constexpr (!kMis) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) A.p[q] = pa + 16 * q;
@@ -951,7 +1010,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             t.sreg = (!kSum && first && P == 0u) ? __builtin_bswap32(partial) : 0u;
             t.M = M;
             if constexpr (kSum) {  // the last piece, if in this row and partial, is masked
-                t.fix = (k0 + 64u >= np && (len & 63u) != 0u) ? 1u : 0u;
+                t.fix = (k0 + 64u >= np && (len % kPB) != 0u) ? 1u : 0u;
             } else {
                 const bool needmask = k0 == 0u && (kMis ? P != 0u : (P & 15u) != 0u);
                 const bool needinj = (k0 == 0u && P != 0u) || (k0 <= 1u && np > 1u && P > 60u);
@@ -966,14 +1025,20 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         const uint32_t lr = nul ? c.b : li;
         const StreamDesc D = sdesc[lr];
         const uint32_t k = (uint32_t)(c.rs + lane - sstart[lr]);
-        const uint32_t np = (uint32_t)(((uint64_t)D.len + 63u) >> 6);
+        const uint32_t np = (uint32_t)(((uint64_t)D.len + (kPB - 1)) / kPB);
         const uint32_t P = kSum ? 0u : (np << 6) - D.len;  // mod 2^32: always < 64
-        const long long o = (long long)k * 64 - (long long)P;
+        const long long o = (long long)k * kPB - (long long)P;
         gbyte *pa = (gbyte *)(uintptr_t)D.addr + o;
         uint32_t sh = 0u;
+        if constexpr (kCopy) {
+            const StreamCopy cp = scopy[lr];
+            const uint64_t ob = (uint64_t)k * kPB;
+            t.ncp = (!nul && ob < cp.copylen) ? (uint32_t)min<uint64_t>(cp.copylen - ob, 16u) : 0u;
+            t.dst = nul ? (gwbyte *)(trash + 16u * lane) : (gwbyte *)(uintptr_t)(cp.dst + ob);
+        }
         if constexpr (!kMis && kSum) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) A.p[q] = (!nul && o + 16 * q < (long long)D.len) ? pa + 16 * q : zero;
+            for (int q = 0; q < kPB / 16; ++q) A.p[q] = (!nul && o + 16 * q < (long long)D.len) ? pa + 16 * q : zero;
         } else if constexpr (!kMis) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) A.p[q] = (!nul && o + 16 * q + 16 > 0) ? pa + 16 * q : zero;
@@ -997,7 +1062,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         t.sreg = (!kSum && first && P == 0u) ? __builtin_bswap32(D.partial) : 0u;
         t.M = M;
         if constexpr (kSum) {
-            t.fix = __builtin_amdgcn_ballot_w64(last && (D.len & 63u) != 0u) ? 1u : 0u;
+            t.fix = __builtin_amdgcn_ballot_w64(last && (D.len % kPB) != 0u) ? 1u : 0u;
         } else {
             const bool needmask = first && (kMis ? P != 0u : (P & 15u) != 0u);
             const bool needinj = (first && P != 0u) || (second && P > 60u);
@@ -1009,11 +1074,11 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         return A;
     };
 
-    // the lane's 16 words, fixed up for first pieces
-    auto prepare = [&](const RowN<NL> &raw, const STask &t, uint32_t d[16]) {
+    // the lane's kW words, fixed up for first pieces
+    auto prepare = [&](const RowN<NL> &raw, const STask &t, uint32_t d[kW]) {
         if constexpr (!kMis) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < kPB / 16; ++q) {
                 d[4 * q + 0] = raw.q[q].x;
                 d[4 * q + 1] = raw.q[q].y;
                 d[4 * q + 2] = raw.q[q].z;
@@ -1036,10 +1101,10 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             for (int w = 0; w < 16; ++w) d[w] = __builtin_amdgcn_alignbyte(b[w + 1], b[w], sb);
         }
         if (kSum && (t.fix & 1u)) {  // zero the bytes of a partial last piece past the fragment end
-            const uint32_t rem = sdesc[t.info & 0x1FFu].len & 63u;
+            const uint32_t rem = sdesc[t.info & 0x1FFu].len % kPB;
             if ((t.info & kTfLast) && rem != 0u) {
 #pragma unroll
-                for (int w = 0; w < 16; ++w) d[w] &= byte_keep_mask(4 * w, 0, (long long)rem);
+                for (int w = 0; w < kW; ++w) d[w] &= byte_keep_mask(4 * w, 0, (long long)rem);
             }
         } else if (!kSum && (t.fix & 3u)) {
             const StreamDesc D = sdesc[t.info & 0x1FFu];
@@ -1123,7 +1188,17 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             if (carry[0] == 0x9E3779B9u && lane == 64u) out[0] = carry[kK - 1];
             return;
         }
-        uint32_t d[kK][16], C[kK];
+        if constexpr (kCopy) {  // the piece to dst (the trash slot unless all 16 bytes are copied)
+            gwbyte *sa = t[0].ncp == 16u ? t[0].dst : (gwbyte *)(trash + 16u * lane);
+            asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(sa), "v"(raw[0].q[0]) : "memory");
+            if (t[0].ncp != 0u && t[0].ncp < 16u) {  // a piece ending past copylen: its first ncp bytes
+                const uint32_t w[4] = {raw[0].q[0].x, raw[0].q[0].y, raw[0].q[0].z, raw[0].q[0].w};
+#pragma unroll
+                for (uint32_t b = 0; b < 15; ++b)  // constant indices: a dynamic w[] index would go to scratch
+                    if (b < t[0].ncp) t[0].dst[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3u)));
+            }
+        }
+        uint32_t d[kK][kW], C[kK];
 #pragma unroll
         for (int c = 0; c < kK; ++c) {
             prepare(raw[c], t[c], d[c]);
@@ -1134,7 +1209,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 #pragma unroll
             for (int c = 0; c < kK; ++c)
 #pragma unroll
-                for (int w = 0; w < 16; w += 2) C[c] = C[c] + d[c][w] + d[c][w + 1];
+                for (int w = 0; w < kW; w += 2) C[c] = C[c] + d[c][w] + d[c][w + 1];
         } else if constexpr (kAbl == 2) {
 #pragma unroll
             for (int c = 0; c < kK; ++c)
@@ -1152,14 +1227,23 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 #pragma unroll
         for (int c = 0; c < kK; ++c) finish(c, t[c], v[c], carry[c]);
     };
-    auto wait_slot = [&](RowN<NL> (&r)[kK]) {
-        if constexpr (kK == 2) {
+    bool first_pass = true;
+    auto wait_slot = [&](RowN<NL> (&r)[kK], auto S) {
+        constexpr int kS = decltype(S)::value;
+        if constexpr (kCopy) {
+            // vmcnt counts loads and stores in issue order: younger than slot S's loads are
+            // (kD - 1) loads and, after the first pass, kD - 1 stores (one per step; S on the first)
+            static_assert(NL == 1, "one load per row");
+            wait_sel<(kD - 1) * NL + kS, (kD - 1) * (NL + 1), (kD - 1) * (NL + 1)>(first_pass ? 0u : 1u, r[0].q[0]);
+        } else if constexpr (kK == 2) {
             wait_rows2<(kD - 1) * 2 * NL>(r[0], r[1]);
         } else if constexpr (NL == 4) {
             asm volatile("s_waitcnt vmcnt(%4)"
                          : "+v"(r[0].q[0]), "+v"(r[0].q[1]), "+v"(r[0].q[2]), "+v"(r[0].q[3])
                          : "n"((kD - 1) * NL)
                          : "memory");
+        } else if constexpr (NL == 1) {
+            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r[0].q[0]) : "n"((kD - 1) * NL) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(%5)"
                          : "+v"(r[0].q[0]), "+v"(r[0].q[1]), "+v"(r[0].q[2]), "+v"(r[0].q[3]), "+v"(r[0].q[4])
@@ -1169,7 +1253,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     };
 #define LAMPI_STREAM_STEP(S)                                                                  \
     if constexpr ((S) < kD) {                                                                 \
-        wait_slot(ring[S]);                                                                   \
+        wait_slot(ring[S], std::integral_constant<int, (S)>{});                               \
         if (step == nsteps) break;                                                            \
         process(ring[S], tk[S]);                                                              \
         ++step;                                                                               \
@@ -1185,6 +1269,11 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         LAMPI_STREAM_STEP(1)
         LAMPI_STREAM_STEP(2)
         LAMPI_STREAM_STEP(3)
+        LAMPI_STREAM_STEP(4)
+        LAMPI_STREAM_STEP(5)
+        LAMPI_STREAM_STEP(6)
+        LAMPI_STREAM_STEP(7)
+        first_pass = false;
     }
 #undef LAMPI_STREAM_STEP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the rows in flight before exit
@@ -1197,10 +1286,15 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 // kAbl (tools/microbench/frags_ablation.hip only): 1 = loads and task walk, no row work;
 // 2 = everything but the table lookups of the pieces.  kK: chains per wave, kWv: waves per
 // workgroup (kWv * kK chains); kWaveCap > 0 asks the compiler for that many waves per SIMD.
-template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0>
+// kPB / kCopy: see stream_body (the fused copy: SUM, 16-byte pieces; a workgroup with a fragment
+// whose src or dst is not 16-byte aligned does nothing -- sum_rows_kernel<CopySource, ..., true>
+// takes those).  trash: 1 KiB of device memory the copy's masked lanes store to.
+template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0,
+          int kPB = 64, bool kCopy = false>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kWaveCap > 0 ? kWaveCap : 1)))
-crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
-    static_assert(!Src::kCopy, "copy sources use crc_rows_kernel");
+crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out,
+                  uint8_t *trash) {
+    static_assert(Src::kCopy == kCopy, "copy sources run the fused-copy variant");
     constexpr uint32_t kThreads = 64 * kWv;
     constexpr uint32_t kChains = kWv * kK;
     static_assert(kThreads >= kFragsPerWg, "one fragment per thread in the set-up");
@@ -1212,6 +1306,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     __shared__ StreamChain schain[kChains];
     __shared__ uint32_t chead[kChains], sopen[kChains], shead[kChains];
     __shared__ uint32_t sres[kFragsPerWg];        // the workgroup's checksums, stored at the end
+    __shared__ StreamCopy scopy[kCopy ? kFragsPerWg + 1 : 1];
     __shared__ uint64_t wpieces[kWv];
     __shared__ uint32_t wcount[kWv];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, t = threadIdx.x;
@@ -1220,6 +1315,10 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
 
     FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
     if (t < nwg) mine = src.get(base + t);
+    if constexpr (kCopy) {  // fast path only: 16-byte-aligned src and dst throughout the workgroup
+        const bool slow = t < nwg && mine.len != 0u && ((((uintptr_t)mine.addr) | (uintptr_t)mine.dst) & 15u) != 0u;
+        if (__syncthreads_or(slow)) return;
+    }
     if (t < kChains) chead[t] = 0u;
     auto nopre = [] {};
     if constexpr (kSum) {
@@ -1238,9 +1337,9 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     }
     const bool ne = t < nwg && mine.len != 0u;              // list entries: the non-empty fragments
     if (t < nwg && mine.len == 0u) sres[t] = kSum ? 0u : mine.partial;  // uicrc(p, 0, s) == s, uicsum(p, 0) == 0
-    const uint64_t np = ne ? (((uint64_t)mine.len + 63u) >> 6) : 0ull;
+    const uint64_t np = ne ? (((uint64_t)mine.len + (kPB - 1)) / kPB) : 0ull;
     // CRC pieces end at the fragment end, SUM pieces start at the fragment start
-    const bool mis = ne && ((((uintptr_t)mine.addr) + (kSum ? 0u : mine.len)) & 15u) != 0u;
+    const bool mis = !kCopy && ne && ((((uintptr_t)mine.addr) + (kSum ? 0u : mine.len)) & 15u) != 0u;
     uint64_t ip = np;
     uint32_t ic = ne ? 1u : 0u;
 #pragma unroll
@@ -1273,11 +1372,12 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     }
     const uint64_t ex = op + ip - np;
     const uint32_t li = oc + ic - (ne ? 1u : 0u);
-    const uint64_t R = (total + 63u) >> 6;  // rows; chain c starts at piece 64 * floor(c * R / 8)
+    const uint64_t R = (total + 63u) >> 6;  // rows; chain c starts at piece 64 * floor(c * R / kChains)
     if (ne) {
         sdesc[li] = StreamDesc{(uint64_t)(uintptr_t)mine.addr, mine.len, mine.partial};
         sstart[li] = ex;
         sj[li] = (uint16_t)t;
+        if constexpr (kCopy) scopy[li] = StreamCopy{(uint64_t)(uintptr_t)mine.dst, mine.copylen, 0u};
 #pragma unroll
         for (uint32_t c = 0; c < kChains; ++c) {
             const uint64_t pc = 64u * ((c * R) / kChains);
@@ -1305,12 +1405,18 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     for (uint32_t i = t; i < kChains * 64; i += kThreads) marks[i] = 0u;
     const bool anymis = __syncthreads_or(mis) != 0;
     gbyte *zero = (gbyte *)(img + kImgZero);
-    if (anymis)  // five loads per row: a one-slot ring keeps its registers within the aligned variant's
-        stream_body<true, 1, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
-                                        sopen + kK * wave, shead + kK * wave, zero, sres, out);
-    else
-        stream_body<false, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
-                                         sopen + kK * wave, shead + kK * wave, zero, sres, out);
+    if constexpr (kPB == 64) {
+        if (anymis)  // five loads per row: a one-slot ring keeps its registers within the aligned variant's
+            stream_body<true, 1, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+                                                 sopen + kK * wave, shead + kK * wave, zero, sres, out);
+        else
+            stream_body<false, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+                                                   sopen + kK * wave, shead + kK * wave, zero, sres, out);
+    } else {
+        stream_body<false, kD, kAbl, kK, kSum, kPB, kCopy>(lds, sdesc, sstart, sj, marks + 64 * kK * wave,
+                                                           schain + kK * wave, sopen + kK * wave, shead + kK * wave,
+                                                           zero, sres, out, scopy, trash);
+    }
     if (kAbl != 0) return;
     __syncthreads();
     // stream_join: fragments crossing chain starts.  Thread c owns the fragment crossing chain c's
@@ -1375,6 +1481,33 @@ __device__ __forceinline__ void wait_rows(RowsK<K> &b) {
                        "+v"(b.x[3].q[0]), "+v"(b.x[3].q[1]), "+v"(b.x[3].q[2]), "+v"(b.x[3].q[3])
                      : "n"(N)
                      : "memory");
+    }
+}
+
+// wait_rows with the count chosen at run time (sel, SGPR: 0 -> A, 1 -> B, else C) in one asm
+// statement (see LAMPI_WAIT_SEL_ASM)
+template <int A, int B, int C, int K>
+__device__ __forceinline__ void wait_rows_sel(uint32_t sel, RowsK<K> &b) {
+    if constexpr (K == 1) {
+        asm volatile(LAMPI_WAIT_SEL_ASM
+                     : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3])
+                     : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
+                     : "scc", "memory");
+    } else if constexpr (K == 2) {
+        asm volatile(LAMPI_WAIT_SEL_ASM
+                     : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
+                       "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3])
+                     : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
+                     : "scc", "memory");
+    } else {
+        static_assert(K == 4, "kChains is 1, 2 or 4");
+        asm volatile(LAMPI_WAIT_SEL_ASM
+                     : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
+                       "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3]),
+                       "+v"(b.x[2].q[0]), "+v"(b.x[2].q[1]), "+v"(b.x[2].q[2]), "+v"(b.x[2].q[3]),
+                       "+v"(b.x[3].q[0]), "+v"(b.x[3].q[1]), "+v"(b.x[3].q[2]), "+v"(b.x[3].q[3])
+                     : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
+                     : "scc", "memory");
     }
 }
 
@@ -1621,13 +1754,9 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     const bool short_tail = kCopy && (nfr % K) != 0;
 #define LAMPI_RING_STEP(S)                                                  \
     if constexpr ((S) < D) {                                                \
-        if constexpr (kCopy) {                                              \
-            if (short_tail && t[(S) % D].i + 1 >= ngrp)                     \
-                wait_rows<0, K>(ring[(S) % D]);                             \
-            else if (first)                                                 \
-                wait_rows<(D - 1 + (S)) * kL, K>(ring[(S) % D]);            \
-            else                                                            \
-                wait_rows<2 * (D - 1) * kL, K>(ring[(S) % D]);              \
+        if constexpr (kCopy) { /* one asm statement: see wait_rows_sel */  \
+            const uint32_t sel_ = uniform((short_tail && t[(S) % D].i + 1 >= ngrp) ? 0u : (first ? 1u : 2u)); \
+            wait_rows_sel<0, (D - 1 + (S)) * kL, 2 * (D - 1) * kL, K>(sel_, ring[(S) % D]); \
         } else {                                                            \
             wait_rows<(D - 1) * kL, K>(ring[(S) % D]);                      \
         }                                                                   \
@@ -1652,9 +1781,20 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 // ---- SUM -------------------------------------------------------------------------------
 // Acc = uint32_t: uicsum (32-bit words); Acc = uint64_t: csum (64-bit words, ref
 // MemFunctions.cc:142-516, 913-1071).  Phase (kPhase sources) is taken mod the word size.
-template <class Src, class Acc = uint32_t>
+// kSkipFast (copy sources): the workgroup does nothing when every fragment of its 4*fpw has
+// 16-byte-aligned src and dst -- crc_stream_kernel's fused copy took those (same partition).
+template <class Src, class Acc = uint32_t, bool kSkipFast = false>
 __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uint32_t fpw, Acc *__restrict__ out) {
     const int lane = threadIdx.x & 63;
+    if constexpr (kSkipFast) {
+        const size_t g = (size_t)blockIdx.x * kWaves * fpw + threadIdx.x;
+        bool slow = false;
+        if (threadIdx.x < kWaves * fpw && g < n) {
+            const FragInfo fi = src.get(g);
+            slow = fi.len != 0u && ((((uintptr_t)fi.addr) | (uintptr_t)fi.dst) & 15u) != 0u;
+        }
+        if (!__syncthreads_or(slow)) return;
+    }
     const size_t f0 = wg_first(fpw);
     const size_t fend = f0 + (size_t)kWaves * fpw;
     for (size_t f = f0; f < n && f < fend; f += kWaves) {
@@ -2177,6 +2317,7 @@ static uint32_t frags_per_wg(size_t n) {
 
 // crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_ablation.hip)
 constexpr int kStreamD = 2, kStreamK = 1, kStreamWv = 12, kStreamCap = 6;
+constexpr int kCopyD = 4;  // fused copy: 1 KiB rows, three in flight per wave (6 slots spilled at 80 VGPRs)
 
 static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg - 1) / fpg)); }
 
@@ -2188,7 +2329,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg,
-                       img, out);
+                       img, out, nullptr);
     return hipGetLastError();
 }
 
@@ -2198,7 +2339,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
-                       MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
+                       MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out, nullptr);
     return hipGetLastError();
 }
 
@@ -2256,16 +2397,27 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
     return hipGetLastError();
 }
 
+// SUM: crc_stream_kernel's fused copy (16-byte pieces, coalesced loads and stores) for workgroups
+// whose fragments all have 16-byte-aligned src and dst, then sum_rows_kernel for the others (same
+// partition: 4*fpw = fpg fragments per workgroup).  img must be an allocation of the table image
+// followed by kImgTrashBytes of device memory (device_tables()).
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                              hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const uint32_t fpw = pick_fpw(n, 1);
-    if (mode == LAMPI_CSUM_CRC32)
+    if (!img) return hipErrorInvalidValue;  // the tables (CRC) / zero chunk and trash slots (SUM)
+    if (mode == LAMPI_CSUM_CRC32) {
+        const uint32_t fpw = pick_fpw(n, 1);
         hipLaunchKernelGGL(crc_rows_kernel<CopySource>, grid_for(n, fpw), dim3(kBlock), 0, s, CopySource{d}, n, fpw,
                            img, out);
-    else
-        hipLaunchKernelGGL(sum_rows_kernel<CopySource>, grid_for(n, fpw), dim3(kBlock), 0, s, CopySource{d}, n, fpw,
-                           out);
+        return hipGetLastError();
+    }
+    uint32_t fpg = 96;  // a multiple of 4 (kWaves): sum_rows_kernel's workgroups cover the same fragments
+    while (fpg > 4 && n / fpg < 2048) fpg = fpg > 12 ? fpg / 2 : 4;
+    uint8_t *trash = (uint8_t *)(uintptr_t)(img + kImgWords);
+    hipLaunchKernelGGL((crc_stream_kernel<CopySource, kCopyD, 0, 1, true, kStreamWv, kStreamCap, 16, true>),
+                       frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, CopySource{d}, n, fpg, img, out, trash);
+    hipLaunchKernelGGL((sum_rows_kernel<CopySource, uint32_t, true>), frags_grid(n, fpg), dim3(kBlock), 0, s,
+                       CopySource{d}, n, fpg / kWaves, out);
     return hipGetLastError();
 }
 
@@ -2294,7 +2446,7 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     if (img) {  // piece streams (img: the zero chunk)
         const uint32_t fpg = frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, true, kStreamWv, kStreamCap>),
-                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out);
+                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
@@ -2313,7 +2465,7 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (img) {
         const uint32_t fpg = frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, true, kStreamWv, kStreamCap>),
-                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
+                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out, nullptr);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);

@@ -50,7 +50,7 @@ hipError_t device_tables(int dev, const uint32_t **out) {
     std::call_once(t.once, [&] {
         const std::vector<uint32_t> &h = host_image();
         uint32_t *p = nullptr;
-        t.err = hipMalloc(&p, h.size() * sizeof(uint32_t));
+        t.err = hipMalloc(&p, h.size() * sizeof(uint32_t) + kImgTrashBytes);  // + the copy's trash slots
         if (t.err == hipSuccess) t.err = hipMemcpy(p, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
         if (t.err == hipSuccess) t.img = p;
     });
@@ -371,11 +371,9 @@ int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d
     int dev = 0;
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
-    const uint32_t *img = nullptr;
-    if (mode == LAMPI_CSUM_CRC32) {
-        e = device_tables(dev, &img);
-        if (e != hipSuccess) return to_int(e);
-    }
+    const uint32_t *img = nullptr;  // both modes: SUM's fused copy reads its zero chunk and trash slots
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
     return to_int(launch_bcopy_desc(d_descs, n, d_out, mode, img, (hipStream_t)stream));
 }
 
