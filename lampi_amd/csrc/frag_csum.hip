@@ -906,6 +906,10 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     struct SChain {
         uint64_t rs, end;  // piece index of the next row's first piece, of the chain's end
         uint32_t cur, b;   // list position of the fragment holding piece rs - 1; chain end
+        // list entry `cur` as the last one-segment row read it (hit: hot == 1): its descriptor,
+        // first piece and the next entry's first piece, so a row inside it reads no LDS
+        uint32_t hot, hlen, hpartial, hj;
+        uint64_t haddr, hs, hnb;
     };
     struct STask {
         uint32_t info, sreg;  // per lane: task word, start register
@@ -925,6 +929,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         cs[c].end = uniform64(sch[c].end);
         cs[c].cur = uniform(sch[c].cur);  // wraps for head == 0: li = cur + (count >= 1)
         cs[c].b = uniform(sch[c].b);
+        cs[c].hot = 0u;
         head[c] = uniform(sch[c].head);
         mid[c] = uniform(sch[c].mid);
         nsteps = max(nsteps, (uint32_t)((cs[c].end - cs[c].rs + 63) >> 6));
@@ -949,8 +954,9 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             return A;
         }
         uint64_t M = 0ull;
-        const uint64_t nb = uniform64(sstart[c.cur + 1u]);
-        const uint64_t nb2 = c.cur + 2u <= c.b ? uniform64(sstart[c.cur + 2u]) : ~0ull;
+        const bool hit = c.hot && c.hnb >= c.rs + 64u;  // the row lies inside cached entry cur
+        const uint64_t nb = hit ? c.hnb : uniform64(sstart[c.cur + 1u]);
+        const uint64_t nb2 = hit ? ~0ull : (c.cur + 2u <= c.b ? uniform64(sstart[c.cur + 2u]) : ~0ull);
         if (nb2 >= c.rs + 64u) {  // at most one fragment starts in this row
             M = nb < c.rs + 64u ? (1ull << (uint32_t)(nb - c.rs)) : 0ull;
         } else {  // several: build the boundary mask
@@ -964,10 +970,19 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         }
         if ((M & ~1ull) == 0ull) {  // one segment: every lane in list entry cur + M (scalar set-up)
             const uint32_t lr = c.cur + (uint32_t)M;
-            const uint64_t addr = uniform64(sdesc[lr].addr);
-            const uint32_t len = uniform(sdesc[lr].len), partial = uniform(sdesc[lr].partial);
-            const uint32_t k0 = uniform((uint32_t)(c.rs - sstart[lr]));  // lane 0's piece
-            t.one = (lr & 0xFFFFu) | (uniform(sj[lr]) << 16);
+            if (!hit) {  // cache entry lr: it is `cur` after this row (M is 0 or 1)
+                c.haddr = uniform64(sdesc[lr].addr);
+                c.hlen = uniform(sdesc[lr].len);
+                c.hpartial = uniform(sdesc[lr].partial);
+                c.hs = uniform64(sstart[lr]);
+                c.hj = uniform(sj[lr]);
+                c.hnb = M ? nb2 : nb;  // first piece of entry lr + 1
+                c.hot = 1u;
+            }
+            const uint64_t addr = c.haddr;
+            const uint32_t len = c.hlen, partial = c.hpartial;
+            const uint32_t k0 = (uint32_t)(c.rs - c.hs);  // lane 0's piece
+            t.one = (lr & 0xFFFFu) | (c.hj << 16);
             const uint32_t np = (uint32_t)(((uint64_t)len + (kPB - 1)) / kPB);
             // CRC: pieces right-aligned (P leading zeros); SUM: left-aligned on the word grid
             const uint32_t P = kSum ? 0u : (np << 6) - len;
@@ -1071,6 +1086,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         t.one = 0u;
         c.cur += (uint32_t)__popcll(M);
         c.rs += 64u;
+        c.hot = 0u;
         return A;
     };
 
