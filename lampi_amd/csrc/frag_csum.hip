@@ -375,18 +375,35 @@ __device__ __forceinline__ void load64(gbyte *frag, long long o, long long lo, l
             d[4 * k + 3] = v.w;
         }
     } else {
-        // not 16-byte aligned: 17 aligned dwords, funnel-shifted by s16 % 4 bytes.  An
-        // aligned dword holding a byte of the fragment never crosses a page.
-        uint32_t a[17];
-        const uint32_t sh = s16 & 3u;
-        const long long c0 = o - (long long)sh;
+        // not 16-byte aligned ((frag + o) % 16 == s16, the same for every lane): the five aligned
+        // 16-byte chunks covering [o, o + 64), funnel-shifted (word offset s16 / 4 is wave-uniform:
+        // a switch; byte shift s16 % 4 by v_alignbyte).  A chunk holding a byte of [lo, hi) never
+        // crosses a page.  (Seventeen dword loads per lane ran the misaligned fused copy at 32%.)
+        const long long cb = o - (long long)s16;
+        uint32_t a[20];
 #pragma unroll
-        for (int k = 0; k < 17; ++k) {
-            const long long c = c0 + 4 * k;
-            a[k] = (c + 4 > lo && c < hi) ? *(guint *)(frag + c) : 0u;
+        for (int k = 0; k < 5; ++k) {
+            const long long c = cb + 16 * k;
+            u32x4 v = {0u, 0u, 0u, 0u};
+            if (c + 16 > lo && c < hi) v = *(gu32x4 *)(frag + c);
+            a[4 * k + 0] = v.x;
+            a[4 * k + 1] = v.y;
+            a[4 * k + 2] = v.z;
+            a[4 * k + 3] = v.w;
         }
-#pragma unroll
-        for (int w = 0; w < 16; ++w) d[w] = __builtin_amdgcn_alignbyte(a[w + 1], a[w], sh);
+        const uint32_t sb = s16 & 3u;
+        switch (s16 >> 2) {  // wave-uniform
+#define LAMPI_LOAD64_CASE(W)                                                                 \
+    case W:                                                                                  \
+        _Pragma("unroll") for (int w = 0; w < 16; ++w) d[w] =                                \
+            __builtin_amdgcn_alignbyte(a[w + (W) + 1], a[w + (W)], sb);                      \
+        break;
+            LAMPI_LOAD64_CASE(0)
+            LAMPI_LOAD64_CASE(1)
+            LAMPI_LOAD64_CASE(2)
+            LAMPI_LOAD64_CASE(3)
+#undef LAMPI_LOAD64_CASE
+        }
     }
     if (mask) {
 #pragma unroll
@@ -759,6 +776,14 @@ __device__ __forceinline__ void issue_rowN(const AddrN<5> &a, RowN<5> &r) {
 __device__ __forceinline__ void issue_rowN(const AddrN<1> &a, RowN<1> &r) {
     asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(r.q[0]) : "v"(a.p[0]) : "memory");
 }
+__device__ __forceinline__ void issue_rowN(const AddrN<2> &a, RowN<2> &r) {
+    asm volatile(
+        "global_load_dwordx4 %0, %2, off\n\t"
+        "global_load_dwordx4 %1, %3, off"
+        : "=&v"(r.q[0]), "=&v"(r.q[1])
+        : "v"(a.p[0]), "v"(a.p[1])
+        : "memory");
+}
 
 // wait until at most N younger loads are outstanding; the two chains' registers of the slot are
 // threaded through so no use is scheduled above the wait
@@ -801,6 +826,13 @@ template <int A, int B, int C>
 __device__ __forceinline__ void wait_sel(uint32_t sel, u32x4 &r) {
     asm volatile(LAMPI_WAIT_SEL_ASM
                  : "+v"(r)
+                 : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
+                 : "scc", "memory");
+}
+template <int A, int B, int C>
+__device__ __forceinline__ void wait_sel(uint32_t sel, u32x4 &r0, u32x4 &r1) {
+    asm volatile(LAMPI_WAIT_SEL_ASM
+                 : "+v"(r0), "+v"(r1)
                  : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
                  : "scc", "memory");
 }
@@ -882,7 +914,8 @@ struct RowsN4 {
 
 // kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way
 // kPB: piece bytes (64; 16 for the fused copy, whose rows are then 1 KiB and every load and store
-// instruction of a wave covers 1 KiB).  kCopy (SUM, 16-byte pieces, 16-byte-aligned src and dst):
+// instruction of a wave covers 1 KiB).  kCopy (SUM, 16-byte pieces, 16-byte-aligned dst; a source
+// that is not 16-byte aligned takes the two-load funnel variant):
 // each lane stores its piece to dst + 16k with one asm store per row (lanes with nothing to store
 // write a per-lane trash slot, so the ring's waits count loads and stores exactly); a piece that
 // ends past copylen is stored byte by byte in addition (compiler stores: they only make the waits
@@ -898,7 +931,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
                                             uint32_t *sopen, uint32_t *shead, gbyte *zero, uint32_t *sres,
                                             uint32_t *__restrict__ out, const StreamCopy *scopy = nullptr,
                                             uint8_t *trash = nullptr) {
-    static_assert(kPB == 64 || (kPB == 16 && kSum && !kMis && kK == 1), "16-byte pieces: aligned SUM only");
+    static_assert(kPB == 64 || (kPB == 16 && kSum && kK == 1), "16-byte pieces: SUM, one chain per wave");
     static_assert(!kCopy || kPB == 16, "the fused copy runs on 16-byte pieces");
     constexpr int NL = kMis ? kPB / 16 + 1 : kPB / 16;  // loads per row
     constexpr int kW = kPB / 4;                          // words per piece
@@ -1011,9 +1044,9 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             } else {
                 sh = (uint32_t)((addr + (uint64_t)o0) & 15u);
                 gbyte *pb = pa - sh;
-                const long long ob = o0 + (long long)lane * 64 - (long long)sh;
+                const long long ob = o0 + (long long)lane * kPB - (long long)sh;
 #pragma unroll
-                for (int q = 0; q < 5; ++q) {
+                for (int q = 0; q < NL; ++q) {
                     const long long r = ob + 16 * q;
                     A.p[q] = (r + 16 > 0 && r < (long long)len) ? pb + 16 * q : zero;
                 }
@@ -1062,7 +1095,7 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             gbyte *pb = pa - sh;
             const long long ob = o - (long long)sh;
 #pragma unroll
-            for (int q = 0; q < 5; ++q) {
+            for (int q = 0; q < NL; ++q) {
                 const long long r = ob + 16 * q;
                 A.p[q] = (!nul && r + 16 > 0 && r < (long long)D.len) ? pb + 16 * q : zero;
             }
@@ -1100,21 +1133,21 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
                 d[4 * q + 2] = raw.q[q].z;
                 d[4 * q + 3] = raw.q[q].w;
             }
-        } else {
-            uint32_t a[20];
+        } else {  // the aligned chunks covering the piece, funnel-shifted by the lane's misalignment
+            uint32_t a[4 * NL];
 #pragma unroll
-            for (int q = 0; q < 5; ++q) {
+            for (int q = 0; q < NL; ++q) {
                 a[4 * q + 0] = raw.q[q].x;
                 a[4 * q + 1] = raw.q[q].y;
                 a[4 * q + 2] = raw.q[q].z;
                 a[4 * q + 3] = raw.q[q].w;
             }
             const uint32_t sh = (t.info >> 21) & 15u, ws = sh >> 2, sb = sh & 3u;
-            uint32_t b[17];
+            uint32_t b[kW + 1];
 #pragma unroll
-            for (int i = 0; i < 17; ++i) b[i] = sel4(ws, a[i], a[i + 1], a[i + 2], a[i + 3]);
+            for (int i = 0; i <= kW; ++i) b[i] = sel4(ws, a[i], a[i + 1], a[i + 2], a[i + 3]);
 #pragma unroll
-            for (int w = 0; w < 16; ++w) d[w] = __builtin_amdgcn_alignbyte(b[w + 1], b[w], sb);
+            for (int w = 0; w < kW; ++w) d[w] = __builtin_amdgcn_alignbyte(b[w + 1], b[w], sb);
         }
         if (kSum && (t.fix & 1u)) {  // zero the bytes of a partial last piece past the fragment end
             const uint32_t rem = sdesc[t.info & 0x1FFu].len % kPB;
@@ -1204,20 +1237,23 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             if (carry[0] == 0x9E3779B9u && lane == 64u) out[0] = carry[kK - 1];
             return;
         }
+        uint32_t d[kK][kW], C[kK];
+#pragma unroll
+        for (int c = 0; c < kK; ++c) prepare(raw[c], t[c], d[c]);
         if constexpr (kCopy) {  // the piece to dst (the trash slot unless all 16 bytes are copied)
+            // (prepare masked only bytes past the fragment end, which are never copied)
             gwbyte *sa = t[0].ncp == 16u ? t[0].dst : (gwbyte *)(trash + 16u * lane);
-            asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(sa), "v"(raw[0].q[0]) : "memory");
+            const u32x4 v = u32x4{d[0][0], d[0][1], d[0][2], d[0][3]};
+            asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(sa), "v"(v) : "memory");
             if (t[0].ncp != 0u && t[0].ncp < 16u) {  // a piece ending past copylen: its first ncp bytes
-                const uint32_t w[4] = {raw[0].q[0].x, raw[0].q[0].y, raw[0].q[0].z, raw[0].q[0].w};
+                const uint32_t w[4] = {d[0][0], d[0][1], d[0][2], d[0][3]};
 #pragma unroll
                 for (uint32_t b = 0; b < 15; ++b)  // constant indices: a dynamic w[] index would go to scratch
                     if (b < t[0].ncp) t[0].dst[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3u)));
             }
         }
-        uint32_t d[kK][kW], C[kK];
 #pragma unroll
         for (int c = 0; c < kK; ++c) {
-            prepare(raw[c], t[c], d[c]);
             C[c] = t[c].sreg;
             if (lane == 0u && !(t[c].info & (kTfFirst | kTfNull))) C[c] = carry[c];
         }
@@ -1249,8 +1285,11 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         if constexpr (kCopy) {
             // vmcnt counts loads and stores in issue order: younger than slot S's loads are
             // (kD - 1) loads and, after the first pass, kD - 1 stores (one per step; S on the first)
-            static_assert(NL == 1, "one load per row");
-            wait_sel<(kD - 1) * NL + kS, (kD - 1) * (NL + 1), (kD - 1) * (NL + 1)>(first_pass ? 0u : 1u, r[0].q[0]);
+            constexpr int A = (kD - 1) * NL + kS, B = (kD - 1) * (NL + 1);
+            if constexpr (NL == 1)
+                wait_sel<A, B, B>(first_pass ? 0u : 1u, r[0].q[0]);
+            else
+                wait_sel<A, B, B>(first_pass ? 0u : 1u, r[0].q[0], r[0].q[1]);
         } else if constexpr (kK == 2) {
             wait_rows2<(kD - 1) * 2 * NL>(r[0], r[1]);
         } else if constexpr (NL == 4) {
@@ -1303,8 +1342,8 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 // 2 = everything but the table lookups of the pieces.  kK: chains per wave, kWv: waves per
 // workgroup (kWv * kK chains); kWaveCap > 0 asks the compiler for that many waves per SIMD.
 // kPB / kCopy: see stream_body (the fused copy: SUM, 16-byte pieces; a workgroup with a fragment
-// whose src or dst is not 16-byte aligned does nothing -- sum_rows_kernel<CopySource, ..., true>
-// takes those).  trash: 1 KiB of device memory the copy's masked lanes store to.
+// whose dst is not 16-byte aligned does nothing -- sum_rows_kernel<CopySource, ..., true> takes
+// those).  trash: 1 KiB of device memory the copy's masked lanes store to.
 template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0,
           int kPB = 64, bool kCopy = false>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kWaveCap > 0 ? kWaveCap : 1)))
@@ -1331,8 +1370,8 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
 
     FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
     if (t < nwg) mine = src.get(base + t);
-    if constexpr (kCopy) {  // fast path only: 16-byte-aligned src and dst throughout the workgroup
-        const bool slow = t < nwg && mine.len != 0u && ((((uintptr_t)mine.addr) | (uintptr_t)mine.dst) & 15u) != 0u;
+    if constexpr (kCopy) {  // fast path only: 16-byte-aligned destinations throughout the workgroup
+        const bool slow = t < nwg && mine.len != 0u && (((uintptr_t)mine.dst) & 15u) != 0u;
         if (__syncthreads_or(slow)) return;
     }
     if (t < kChains) chead[t] = 0u;
@@ -1355,7 +1394,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     if (t < nwg && mine.len == 0u) sres[t] = kSum ? 0u : mine.partial;  // uicrc(p, 0, s) == s, uicsum(p, 0) == 0
     const uint64_t np = ne ? (((uint64_t)mine.len + (kPB - 1)) / kPB) : 0ull;
     // CRC pieces end at the fragment end, SUM pieces start at the fragment start
-    const bool mis = !kCopy && ne && ((((uintptr_t)mine.addr) + (kSum ? 0u : mine.len)) & 15u) != 0u;
+    const bool mis = ne && ((((uintptr_t)mine.addr) + (kSum ? 0u : mine.len)) & 15u) != 0u;
     uint64_t ip = np;
     uint32_t ic = ne ? 1u : 0u;
 #pragma unroll
@@ -1428,6 +1467,11 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
         else
             stream_body<false, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                                    sopen + kK * wave, shead + kK * wave, zero, sres, out);
+    } else if (anymis) {  // sources not 16-byte aligned: two loads per piece, funnel-shifted (a
+        // two-slot ring keeps the registers within the budget: four slots spilled)
+        stream_body<true, 2, kAbl, kK, kSum, kPB, kCopy>(lds, sdesc, sstart, sj, marks + 64 * kK * wave,
+                                                          schain + kK * wave, sopen + kK * wave, shead + kK * wave,
+                                                          zero, sres, out, scopy, trash);
     } else {
         stream_body<false, kD, kAbl, kK, kSum, kPB, kCopy>(lds, sdesc, sstart, sj, marks + 64 * kK * wave,
                                                            schain + kK * wave, sopen + kK * wave, shead + kK * wave,
@@ -1797,8 +1841,8 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 // ---- SUM -------------------------------------------------------------------------------
 // Acc = uint32_t: uicsum (32-bit words); Acc = uint64_t: csum (64-bit words, ref
 // MemFunctions.cc:142-516, 913-1071).  Phase (kPhase sources) is taken mod the word size.
-// kSkipFast (copy sources): the workgroup does nothing when every fragment of its 4*fpw has
-// 16-byte-aligned src and dst -- crc_stream_kernel's fused copy took those (same partition).
+// kSkipFast (copy sources): the workgroup does nothing when every fragment of its 4*fpw has a
+// 16-byte-aligned dst -- crc_stream_kernel's fused copy took those (same partition).
 template <class Src, class Acc = uint32_t, bool kSkipFast = false>
 __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uint32_t fpw, Acc *__restrict__ out) {
     const int lane = threadIdx.x & 63;
@@ -1807,7 +1851,7 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
         bool slow = false;
         if (threadIdx.x < kWaves * fpw && g < n) {
             const FragInfo fi = src.get(g);
-            slow = fi.len != 0u && ((((uintptr_t)fi.addr) | (uintptr_t)fi.dst) & 15u) != 0u;
+            slow = fi.len != 0u && (((uintptr_t)fi.dst) & 15u) != 0u;
         }
         if (!__syncthreads_or(slow)) return;
     }
@@ -2414,7 +2458,7 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 }
 
 // SUM: crc_stream_kernel's fused copy (16-byte pieces, coalesced loads and stores) for workgroups
-// whose fragments all have 16-byte-aligned src and dst, then sum_rows_kernel for the others (same
+// whose fragments all have 16-byte-aligned destinations, then sum_rows_kernel for the others (same
 // partition: 4*fpw = fpg fragments per workgroup).  img must be an allocation of the table image
 // followed by kImgTrashBytes of device memory (device_tables()).
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,

@@ -119,14 +119,16 @@ def test_bcopy_batch_random(cuda, oracle):
         _assert_same(got, want, dgot, dwant, lambda i: (int(cl[i]), int(sl[i]), int(sa[i]), int(da[i])))
 
 
-@pytest.mark.parametrize("n", [40, 3000, 30000])
-def test_bcopy_batch_sum_aligned_streams(cuda, oracle, n):
-    """SUM with 16-byte-aligned sources and destinations: the fused-copy piece streams (16-byte
-    pieces, coalesced stores, trash slots for masked lanes, byte stores for a piece ending past
-    copylen).  Random lengths incl. 0 and odd ones, copylen =/</> csumlen; every 16th fragment
-    misaligned in the larger batches so that fast and fallback workgroups (sum_rows_kernel)
-    interleave in one batch; small batches make fragments span chains."""
-    rng = np.random.default_rng(n)
+@pytest.mark.parametrize("n,layout", [(40, "aligned"), (40, "src8"), (3000, "mixed"), (30000, "mixed"),
+                                      (30000, "src8")])
+def test_bcopy_batch_sum_streams(cuda, oracle, n, layout):
+    """SUM through the fused-copy piece streams (16-byte pieces, coalesced stores, trash slots for
+    masked lanes, byte stores for a piece ending past copylen).  Random lengths incl. 0 and odd
+    ones, copylen =/</> csumlen.  "src8": every source at +8 (payload after a 72-byte GM header:
+    the two-load funnel variant); "mixed": some sources misaligned (funnel workgroups) and some
+    destinations misaligned (their workgroups fall back to sum_rows_kernel), interleaved in one
+    batch.  Small batches make fragments span chains."""
+    rng = np.random.default_rng(n + len(layout))
     big = rng.random(n) < (0.5 if n == 40 else 0.05)
     cl = np.where(big, rng.integers(0, 300000, size=n), rng.integers(0, 5000, size=n))
     kind = rng.integers(0, 3, size=n)
@@ -135,8 +137,11 @@ def test_bcopy_batch_sum_aligned_streams(cuda, oracle, n):
     csumlen = np.where(kind == 2, short, cl)
     sa = np.zeros(n, np.int64)
     da = np.zeros(n, np.int64)
-    if n > 40:
+    if layout == "src8":
+        sa[:] = 8
+    elif layout == "mixed":
         sa[::16] = rng.integers(1, 16, size=sa[::16].size)
+        da[5::23] = rng.integers(1, 16, size=da[5::23].size)
     parts = np.zeros(n, np.uint64)
     got, want, dgot, dwant = _run(cuda, oracle, copylen, csumlen, sa, da, parts, 1)
     _assert_same(got, want, dgot, dwant, lambda i: (int(copylen[i]), int(csumlen[i]), int(sa[i]), int(da[i])))
