@@ -169,6 +169,36 @@ def test_descriptor_batch_fragments_across_chains(cuda, oracle, case, mode):
     assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
 
 
+def test_descriptor_batch_maximum_length(cuda):
+    """A single fragment of 2^32 - 1 bytes (the largest `length`), with neighbours: its checksum
+    must equal the chained checksum of two parts (CRC: the first part's register is the second's
+    starting register, crc(s, A||B) = crc(crc(s, A), B); SUM: the sums add when |A| % 4 == 0) --
+    a size-independent property at the size where piece indices exceed 2^26 per workgroup and the
+    parts of one fragment are joined across all twelve chains (shifts by millions of pieces)."""
+    import torch
+
+    dv = _dv()
+    L = 2**32 - 1
+    base = torch.empty(L + 4096, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=123)
+    a = 1_500_000_004  # first part (a multiple of 4)
+    for mode in (dv.CRC32, dv.SUM32):
+        whole = dv.make_descs(base, np.array([17, 0, 5], np.uint64), np.array([L, 0, 999], np.uint64),
+                              np.array([0xFFFFFFFF, 7, 0x1234], np.uint64))
+        w = dv.as_u32(dv.frag_csum_batch(whole, mode=mode))
+        first = dv.make_descs(base, np.array([17], np.uint64), np.array([a], np.uint64),
+                              np.array([0xFFFFFFFF], np.uint64))
+        x = int(dv.as_u32(dv.frag_csum_batch(first, mode=mode))[0])
+        second = dv.make_descs(base, np.array([17 + a], np.uint64), np.array([L - a], np.uint64),
+                               np.array([x if mode == dv.CRC32 else 0], np.uint64))
+        y = int(dv.as_u32(dv.frag_csum_batch(second, mode=mode))[0])
+        want = y if mode == dv.CRC32 else (x + y) & 0xFFFFFFFF
+        assert int(w[0]) == want, (mode, hex(int(w[0])), hex(want))
+        assert int(w[1]) == (7 if mode == dv.CRC32 else 0)  # empty: the register / 0
+    del base
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("n", [30000, 300000])
 def test_descriptor_batch_small_fragments(cuda, oracle, n):
     """Fragments of 16..1024 bytes (multiples of 16, 16-byte aligned) mixed with unaligned,
