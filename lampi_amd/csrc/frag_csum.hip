@@ -451,6 +451,38 @@ __device__ __forceinline__ void store64(uint8_t *dst, long long o, const uint32_
     if (tail) store_word(dst, a + 64, __builtin_amdgcn_alignbyte(0u, d[15], sh), lo, hi);
 }
 
+// A whole 4 KiB row (lane l holds bytes [64l, 64l+64)) to a 16-byte-aligned dst with
+// 1 KiB-coalesced stores: each half row goes through the wave's kStage-byte LDS area (lanes of
+// the half write their 64 bytes, every lane reads back the 16-byte chunks at 16l and 1024+16l).
+// Lane-contiguous 64-byte stores run at 51% of the HBM roofline against 71% for coalesced ones
+// (profiles/r01_copy_patterns.txt).  LDS operations of one wave complete in order, so the area
+// is reused without a barrier; the asm fences only keep the compiler from reordering them.
+template <uint32_t kStage>
+__device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *dst, const uint32_t d[16], int lane) {
+    static_assert(kStage == 1024 || kStage == 2048, "half- or quarter-row staging");
+    constexpr int kParts = kRowBytes / kStage;  // lanes 64/kParts per part
+    constexpr int kLanes = 64 / kParts;
+    constexpr int kRd = kStage / 1024;          // 1 KiB reads (and stores) per part
+    u32x4 *st = (u32x4 *)stage;
+#pragma unroll
+    for (int h = 0; h < kParts; ++h) {
+        if (lane / kLanes == h) {
+            const int b = (lane % kLanes) * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) st[b + q] = u32x4{d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]};
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        u32x4 v[kRd];
+#pragma unroll
+        for (int i = 0; i < kRd; ++i) v[i] = st[64 * i + lane];
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < kRd; ++i) *(gwu32x4 *)(dst + h * kStage + 1024 * i + 16 * lane) = v[i];
+    }
+}
+
 // d[15] of lane - 1 (lane 0 gets `carry`, the last lane's word of the previous row)
 __device__ __forceinline__ uint32_t prev_lane_top(uint32_t d15, uint32_t carry, int lane) {
     const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - 1) * 4, (int)d15);
@@ -598,21 +630,31 @@ __device__ __forceinline__ void crc_inject(uint32_t d[16], const RowGeom &g, uin
 }
 
 // ---- CRC, general fragments (descriptor batches, ragged messages) -----------------------
-template <class Src>
-__global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uint32_t fpw,
-                                                          const uint32_t *__restrict__ img,
-                                                          uint32_t *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
-    stage_tables<0>(lds, img, [] {});
+// kWv: waves per workgroup.  The fused copy (CopySource) runs 8-wave workgroups with a 1 KiB
+// staging area per wave behind the tables (74 KiB: still two workgroups, now 16 waves per CU --
+// each wave keeps one row in flight, so the wave count sets the bytes in flight).
+template <class Src, int kWv = kWaves>
+__global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, uint32_t fpw,
+                                                            const uint32_t *__restrict__ img,
+                                                            uint32_t *__restrict__ out) {
+    static_assert(kWv >= kWaves, "the table builders need 256 threads");
+    constexpr uint32_t kStage = Src::kCopy ? kRowBytes * kWaves / kWv / 2 : 0;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLdsBytes + kWv * kStage) / 4];
+    if constexpr (kWv == kWaves) {
+        stage_tables<0>(lds, img, [] {});
+    } else {
+        if (threadIdx.x < 64 * kWaves) stage_tables<0, void (*)(), 7, false, false>(lds, img, [] {});
+        lds_barrier();
+    }
 
     const int lane = threadIdx.x & 63;
     const CrcLane k = make_lane(lane);
-    const size_t f0 = wg_first(fpw);
-    const size_t fend = f0 + (size_t)kWaves * fpw;  // exclusive, stride kWaves
+    const size_t f0 = uniform(blockIdx.x * kWv * fpw + (threadIdx.x >> 6));
+    const size_t fend = f0 + (size_t)kWv * fpw;  // exclusive, stride kWv
 
-    // next non-empty fragment at or after x (stride kWaves); empty ones are answered directly
+    // next non-empty fragment at or after x (stride kWv); empty ones are answered directly
     auto next_nonempty = [&](size_t x, FragInfo &fi) -> size_t {
-        for (; x < n && x < fend; x += kWaves) {
+        for (; x < n && x < fend; x += kWv) {
             fi = src.get(x);
             fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
             fi.len = uniform(fi.len);
@@ -644,7 +686,7 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
         size_t nf = f;
         uint32_t nr = r + 1;
         if (nr >= g.R) {
-            nf = next_nonempty(f + kWaves, nfi);
+            nf = next_nonempty(f + kWv, nfi);
             nr = 0;
             if (nf < n) ng = crc_geom(nfi);
         }
@@ -656,9 +698,16 @@ __global__ void __launch_bounds__(kBlock) crc_rows_kernel(Src src, size_t n, uin
             if (cur.copylen) {
                 const long long o = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P;
                 const uint32_t dm = (uint32_t)((uintptr_t)cur.dst - g.P) & 15u;
-                if (r == 0) carry = 0;
-                const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
-                store64(cur.dst, o, d, 0, (long long)cur.copylen, dm & 3u, dm == 0, prev, lane == 63 && r + 1 == g.R);
+                const long long row0 = (long long)r * kRowBytes - (long long)g.P;
+                if (dm == 0 && row0 >= 0 && row0 + kRowBytes <= (long long)cur.copylen) {
+                    store_row_coalesced<kStage>(lds + (kLdsBytes + (threadIdx.x >> 6) * kStage) / 4,
+                                                cur.dst + row0, d, lane);
+                } else {
+                    if (r == 0) carry = 0;
+                    const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
+                    store64(cur.dst, o, d, 0, (long long)cur.copylen, dm & 3u, dm == 0, prev,
+                            lane == 63 && r + 1 == g.R);
+                }
                 carry = __builtin_amdgcn_readlane(d[15], 63);
             }
         }
@@ -2466,9 +2515,11 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC) / zero chunk and trash slots (SUM)
     if (mode == LAMPI_CSUM_CRC32) {
-        const uint32_t fpw = pick_fpw(n, 1);
-        hipLaunchKernelGGL(crc_rows_kernel<CopySource>, grid_for(n, fpw), dim3(kBlock), 0, s, CopySource{d}, n, fpw,
-                           img, out);
+        constexpr int kWv = 2 * kWaves;
+        const uint32_t fpw = std::max(1u, pick_fpw(n, 1) / 2);
+        const dim3 grid((unsigned)((n + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw)));
+        hipLaunchKernelGGL((crc_rows_kernel<CopySource, kWv>), grid, dim3(64 * kWv), 0, s, CopySource{d}, n, fpw, img,
+                           out);
         return hipGetLastError();
     }
     uint32_t fpg = 96;  // a multiple of 4 (kWaves): sum_rows_kernel's workgroups cover the same fragments
