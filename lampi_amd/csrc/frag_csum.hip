@@ -2413,6 +2413,18 @@ static uint32_t pick_fpw(size_t n, uint32_t R) {
 
 constexpr int kRegularChains = 2;
 
+// crc_rows_kernel with a fused copy: 8-wave workgroups (16 waves/CU, one row in flight each),
+// half the fragments per wave of the 4-wave schedule so a workgroup covers the same span
+template <class Src>
+static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uint32_t *img, uint32_t *out,
+                                 hipStream_t s) {
+    static_assert(Src::kCopy, "the staging area is for the fused copy");
+    constexpr int kWv = 2 * kWaves;
+    const uint32_t fpw = std::max(1u, pick_fpw(n, R) / 2);
+    const dim3 grid((unsigned)((n + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw)));
+    hipLaunchKernelGGL((crc_rows_kernel<Src, kWv>), grid, dim3(64 * kWv), 0, s, src, n, fpw, img, out);
+}
+
 // fragments per workgroup of crc_stream_kernel: 96 (measured: tools/microbench/frags_ablation.hip,
 // 12-wave workgroups -- 96 beat 64/128/192/256 on config C and on 4 KiB descriptors: shorter
 // workgroups shrink the end-of-kernel tail, and 96 uniform 4 KiB fragments are 8 rows per chain),
@@ -2515,11 +2527,7 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC) / zero chunk and trash slots (SUM)
     if (mode == LAMPI_CSUM_CRC32) {
-        constexpr int kWv = 2 * kWaves;
-        const uint32_t fpw = std::max(1u, pick_fpw(n, 1) / 2);
-        const dim3 grid((unsigned)((n + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw)));
-        hipLaunchKernelGGL((crc_rows_kernel<CopySource, kWv>), grid, dim3(64 * kWv), 0, s, CopySource{d}, n, fpw, img,
-                           out);
+        launch_crc_rows_copy(CopySource{d}, n, 1, img, out, s);
         return hipGetLastError();
     }
     uint32_t fpg = 96;  // a multiple of 4 (kWaves): sum_rows_kernel's workgroups cover the same fragments
@@ -2593,9 +2601,8 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                          n <= 0xFFFFFFFFull;
     if (mode == LAMPI_CSUM_CRC32) {
         if (regular) return launch_crc_regular_copy(base, n, frag_len, partial, dst, dst_stride, out, img, s);
-        const uint32_t fpw = pick_fpw(n, (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes));
-        hipLaunchKernelGGL(crc_rows_kernel<MsgCopySource>, grid_for(n, fpw), dim3(kBlock), 0, s,
-                           MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n, fpw, img, out);
+        launch_crc_rows_copy(MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n,
+                             (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes), img, out, s);
         return hipGetLastError();
     }
     if (regular) {
@@ -2658,8 +2665,7 @@ hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t
             hipLaunchKernelGGL(sum_rows_kernel<PieceSource>, grid_for(npieces, fpw), dim3(kBlock), 0, s, src, npieces,
                                fpw, vals);
         else
-            hipLaunchKernelGGL(crc_rows_kernel<PieceSource>, grid_for(npieces, fpw), dim3(kBlock), 0, s, src, npieces,
-                               fpw, img, vals);
+            launch_crc_rows_copy(src, npieces, 1, img, vals, s);
         hipLaunchKernelGGL(chain_small_kernel, dim3((unsigned)((npieces + 255) / 256)), dim3(256), 0, s, d,
                            (uint32_t)npieces, phase, kSmall, mode, img, vals);
     }
