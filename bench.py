@@ -501,6 +501,11 @@ def run_bcopy(args):
     descs8 = dv.make_copy_descs(src, offs[:-1] + np.uint64(8), dst, offs[:-1], np.full(n - 1, L), np.full(n - 1, L))
     _, kern_desc8 = timed(lambda: dv.frag_bcopy_batch(descs8, n=n - 1, mode=mode, out=out))
     copy8_ok = bool(torch.equal(src[8:8 + (n - 1) * L], dst[:(n - 1) * L]))
+    # the GM send shape: payloads gathered into ring slots right after the 72-byte header --
+    # destinations 8 bytes past a 16-byte boundary, sources aligned
+    descs_d8 = dv.make_copy_descs(src, offs[:-1], dst, offs[:-1] + np.uint64(8), np.full(n - 1, L), np.full(n - 1, L))
+    _, kern_dst8 = timed(lambda: dv.frag_bcopy_batch(descs_d8, n=n - 1, mode=mode, out=out))
+    copyd8_ok = bool(torch.equal(src[:(n - 1) * L], dst[8:8 + (n - 1) * L]))
     _, kern_copy = timed(lambda: dst.copy_(src))
     moved = 2.0 * n * L
     achieved = moved / kern / 1e9
@@ -525,6 +530,10 @@ def run_bcopy(args):
                                           "to aligned dst; copy checked", "kernel_avg_ms": round(kern_desc8 * 1e3, 4),
                                   "frac": round(2.0 * (n - 1) * L / kern_desc8 / 1e9 / HBM_PEAK_GBS, 4),
                                   "copy_ok": copy8_ok},
+        "descriptor_batch_dst8": {"what": "n-1 fragments from aligned src to dst + 8 (gather into GM slots after a "
+                                          "72-byte header); copy checked", "kernel_avg_ms": round(kern_dst8 * 1e3, 4),
+                                  "frac": round(2.0 * (n - 1) * L / kern_dst8 / 1e9 / HBM_PEAK_GBS, 4),
+                                  "copy_ok": copyd8_ok},
         "copy_reference": {"what": "torch dst.copy_(src), same bytes, no checksum",
                            "kernel_avg_ms": round(kern_copy * 1e3, 4),
                            "achieved_GBs": round(moved / kern_copy / 1e9, 1)},

@@ -483,6 +483,48 @@ __device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *ds
     }
 }
 
+// As store_row_coalesced for a destination at dm = dst % 16 in {4, 8, 12}: each part is staged
+// dm bytes into the area, so the 16-byte chunks read back are aligned in the destination.  The
+// first chunk of a part starts with the last dm bytes of the part before (copied to the front of
+// the area first); the row's first chunk is stored from word dm/4 on and its last dm bytes (left
+// behind the last part) by dm/4 word stores: the row writes exactly its 4096 bytes.
+template <uint32_t kStage>
+__device__ __forceinline__ void store_row_coalesced_w(uint32_t *stage, uint8_t *dst, const uint32_t d[16], int lane,
+                                                      uint32_t dm) {
+    static_assert(kStage == 1024, "quarter-row staging");
+    constexpr int kParts = kRowBytes / kStage;
+    constexpr int kLanes = 64 / kParts;
+    constexpr int kTop = kStage / 4;  // word index of the bytes left behind a part
+    const int sw = (int)(dm >> 2);
+    uint8_t *base = dst - dm;  // 16-byte aligned
+#pragma unroll
+    for (int h = 0; h < kParts; ++h) {
+        if (h > 0 && lane < sw) stage[lane] = stage[kTop + lane];
+        if (lane / kLanes == h) {
+            const int b = sw + (lane % kLanes) * 16;
+#pragma unroll
+            for (int w = 0; w < 16; ++w) stage[b + w] = d[w];
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        const u32x4 v = ((const u32x4 *)stage)[lane];
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        uint8_t *c = base + h * kStage + 16 * lane;
+        if (h > 0 || lane > 0) {
+            *(gwu32x4 *)c = v;
+        } else {
+            if (sw <= 1) *(gwuint *)(c + 4) = v.y;
+            if (sw <= 2) *(gwuint *)(c + 8) = v.z;
+            *(gwuint *)(c + 12) = v.w;
+        }
+    }
+    asm volatile("" ::: "memory");
+    if (lane < sw) *(gwuint *)(base + kRowBytes + 4 * lane) = stage[kTop + lane];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // d[15] of lane - 1 (lane 0 gets `carry`, the last lane's word of the previous row)
 __device__ __forceinline__ uint32_t prev_lane_top(uint32_t d15, uint32_t carry, int lane) {
     const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - 1) * 4, (int)d15);
@@ -638,8 +680,9 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                                                             const uint32_t *__restrict__ img,
                                                             uint32_t *__restrict__ out) {
     static_assert(kWv >= kWaves, "the table builders need 256 threads");
-    constexpr uint32_t kStage = Src::kCopy ? (kWv == kWaves ? kRowBytes / 2 : 1024u) : 0;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLdsBytes + kWv * kStage) / 4];
+    constexpr uint32_t kStage = Src::kCopy ? 1024u : 0u;     // a quarter row per part
+    constexpr uint32_t kArea = Src::kCopy ? kStage + 16u : 0u;  // + the carried bytes (dst % 16 = 4, 8, 12)
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLdsBytes + kWv * kArea) / 4];
     if constexpr (kWv == kWaves) {
         stage_tables<0>(lds, img, [] {});
     } else {
@@ -699,9 +742,12 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                 const long long o = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P;
                 const uint32_t dm = (uint32_t)((uintptr_t)cur.dst - g.P) & 15u;
                 const long long row0 = (long long)r * kRowBytes - (long long)g.P;
-                if (dm == 0 && row0 >= 0 && row0 + kRowBytes <= (long long)cur.copylen) {
-                    store_row_coalesced<kStage>(lds + (kLdsBytes + (threadIdx.x >> 6) * kStage) / 4,
-                                                cur.dst + row0, d, lane);
+                const bool whole = row0 >= 0 && row0 + kRowBytes <= (long long)cur.copylen;
+                uint32_t *area = lds + (kLdsBytes + (threadIdx.x >> 6) * kArea) / 4;
+                if (whole && dm == 0) {
+                    store_row_coalesced<kStage>(area, cur.dst + row0, d, lane);
+                } else if (whole && (dm & 3u) == 0) {
+                    store_row_coalesced_w<kStage>(area, cur.dst + row0, d, lane, dm);
                 } else {
                     if (r == 0) carry = 0;
                     const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;

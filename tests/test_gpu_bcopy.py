@@ -147,6 +147,27 @@ def test_bcopy_batch_sum_streams(cuda, oracle, n, layout):
     _assert_same(got, want, dgot, dwant, lambda i: (int(copylen[i]), int(csumlen[i]), int(sa[i]), int(da[i])))
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("dst_align", [4, 8, 12])
+def test_bcopy_batch_word_misaligned_dst(cuda, oracle, mode, dst_align):
+    """Destinations 4, 8 or 12 bytes past a 16-byte boundary (the send side gathers payloads into
+    GM ring slots right after the 72-byte header): in CRC mode whole rows go through the staged
+    coalesced stores with the carried bytes, edge rows through word stores.  Multi-row fragments,
+    ragged lengths, copylen =/</> csumlen, sources aligned or not; untouched bytes stay."""
+    rng = np.random.default_rng(900 + dst_align + mode)
+    n = 600
+    cl = np.where(rng.random(n) < 0.3, rng.integers(0, 70000, size=n), 4096 * rng.integers(1, 9, size=n))
+    kind = rng.integers(0, 3, size=n)
+    short = (cl * rng.random(n)).astype(np.int64)
+    copylen = np.where(kind == 1, short, cl)
+    csumlen = np.where(kind == 2, short, cl)
+    sa = np.where(rng.random(n) < 0.5, 0, rng.integers(0, 16, size=n))
+    da = np.full(n, dst_align)
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    got, want, dgot, dwant = _run(cuda, oracle, copylen, csumlen, sa, da, parts, mode)
+    _assert_same(got, want, dgot, dwant, lambda i: (int(copylen[i]), int(csumlen[i]), int(sa[i]), int(da[i])))
+
+
 def test_bcopy_batch_uniform_4k(cuda, oracle):
     """256K x 4 KiB gather into a staging array (the send-side shape): checksums vs the oracle,
     the copy compared on the device."""
