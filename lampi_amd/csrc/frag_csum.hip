@@ -1009,7 +1009,7 @@ struct RowsN4 {
 
 // kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way
 // kPB: piece bytes (64; 16 for the fused copy, whose rows are then 1 KiB and every load and store
-// instruction of a wave covers 1 KiB).  kCopy (SUM, 16-byte pieces, 16-byte-aligned dst; a source
+// instruction of a wave covers 1 KiB).  kCopy (SUM, 16-byte pieces, 4-byte-aligned dst; a source
 // that is not 16-byte aligned takes the two-load funnel variant):
 // each lane stores its piece to dst + 16k with one asm store per row (lanes with nothing to store
 // write a per-lane trash slot, so the ring's waits count loads and stores exactly); a piece that
@@ -1465,8 +1465,10 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
 
     FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
     if (t < nwg) mine = src.get(base + t);
-    if constexpr (kCopy) {  // fast path only: 16-byte-aligned destinations throughout the workgroup
-        const bool slow = t < nwg && mine.len != 0u && (((uintptr_t)mine.dst) & 15u) != 0u;
+    if constexpr (kCopy) {  // fast path only: 4-byte-aligned destinations throughout the workgroup
+        // (a piece's dwordx4 store is then dword-aligned: dst + 16k at dst % 16 = 4, 8, 12 --
+        // the GM send side's slots after a 72-byte header -- runs at the aligned rate)
+        const bool slow = t < nwg && mine.len != 0u && (((uintptr_t)mine.dst) & 3u) != 0u;
         if (__syncthreads_or(slow)) return;
     }
     if (t < kChains) chead[t] = 0u;
@@ -1937,7 +1939,7 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 // Acc = uint32_t: uicsum (32-bit words); Acc = uint64_t: csum (64-bit words, ref
 // MemFunctions.cc:142-516, 913-1071).  Phase (kPhase sources) is taken mod the word size.
 // kSkipFast (copy sources): the workgroup does nothing when every fragment of its 4*fpw has a
-// 16-byte-aligned dst -- crc_stream_kernel's fused copy took those (same partition).
+// 4-byte-aligned dst -- crc_stream_kernel's fused copy took those (same partition).
 template <class Src, class Acc = uint32_t, bool kSkipFast = false>
 __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uint32_t fpw, Acc *__restrict__ out) {
     const int lane = threadIdx.x & 63;
@@ -1946,7 +1948,7 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
         bool slow = false;
         if (threadIdx.x < kWaves * fpw && g < n) {
             const FragInfo fi = src.get(g);
-            slow = fi.len != 0u && (((uintptr_t)fi.dst) & 15u) != 0u;
+            slow = fi.len != 0u && (((uintptr_t)fi.dst) & 3u) != 0u;
         }
         if (!__syncthreads_or(slow)) return;
     }
@@ -2565,7 +2567,7 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 }
 
 // SUM: crc_stream_kernel's fused copy (16-byte pieces, coalesced loads and stores) for workgroups
-// whose fragments all have 16-byte-aligned destinations, then sum_rows_kernel for the others (same
+// whose fragments all have 4-byte-aligned destinations, then sum_rows_kernel for the others (same
 // partition: 4*fpw = fpg fragments per workgroup).  img must be an allocation of the table image
 // followed by kImgTrashBytes of device memory (device_tables()).
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
