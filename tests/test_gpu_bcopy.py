@@ -126,8 +126,8 @@ def test_bcopy_batch_sum_streams(cuda, oracle, n, layout):
     masked lanes, byte stores for a piece ending past copylen).  Random lengths incl. 0 and odd
     ones, copylen =/</> csumlen.  "src8": every source at +8 (payload after a 72-byte GM header:
     the two-load funnel variant); "mixed": some sources misaligned (funnel workgroups) and some
-    destinations misaligned (their workgroups fall back to sum_rows_kernel), interleaved in one
-    batch.  Small batches make fragments span chains."""
+    destinations misaligned (byte-misaligned ones send their workgroups to sum_rows_kernel,
+    4/8/12 stay on the streams), interleaved in one batch.  Small batches make fragments span chains."""
     rng = np.random.default_rng(n + len(layout))
     big = rng.random(n) < (0.5 if n == 40 else 0.05)
     cl = np.where(big, rng.integers(0, 300000, size=n), rng.integers(0, 5000, size=n))
