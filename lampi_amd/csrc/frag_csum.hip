@@ -451,12 +451,14 @@ __device__ __forceinline__ void store64(uint8_t *dst, long long o, const uint32_
     if (tail) store_word(dst, a + 64, __builtin_amdgcn_alignbyte(0u, d[15], sh), lo, hi);
 }
 
-// A whole 4 KiB row (lane l holds bytes [64l, 64l+64)) to a 16-byte-aligned dst with
-// 1 KiB-coalesced stores: each half row goes through the wave's kStage-byte LDS area (lanes of
-// the half write their 64 bytes, every lane reads back the 16-byte chunks at 16l and 1024+16l).
+// A whole 4 KiB row (lane l holds bytes [64l, 64l+64)) to a 4-byte-aligned dst with
+// 1 KiB-coalesced stores: each quarter row goes through the wave's kStage-byte LDS area (its 16
+// lanes write their 64 bytes, every lane reads back the 16-byte chunk at 16l and stores it).
 // Lane-contiguous 64-byte stores run at 51% of the HBM roofline against 71% for coalesced ones
-// (profiles/r01_copy_patterns.txt).  LDS operations of one wave complete in order, so the area
-// is reused without a barrier; the asm fences only keep the compiler from reordering them.
+// (profiles/r01_copy_patterns.txt); dword-aligned dwordx4 stores (dst % 16 = 4, 8, 12) run at
+// the aligned rate (dst + 8: 68%, against 61% for staging destination-aligned chunks with
+// carried bytes and 21% for word stores).  LDS operations of one wave complete in order, so the
+// area is reused without a barrier; the asm fences only keep the compiler from reordering them.
 template <uint32_t kStage>
 __device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *dst, const uint32_t d[16], int lane) {
     static_assert(kStage == 1024 || kStage == 2048, "half- or quarter-row staging");
@@ -481,48 +483,6 @@ __device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *ds
 #pragma unroll
         for (int i = 0; i < kRd; ++i) *(gwu32x4 *)(dst + h * kStage + 1024 * i + 16 * lane) = v[i];
     }
-}
-
-// As store_row_coalesced for a destination at dm = dst % 16 in {4, 8, 12}: each part is staged
-// dm bytes into the area, so the 16-byte chunks read back are aligned in the destination.  The
-// first chunk of a part starts with the last dm bytes of the part before (copied to the front of
-// the area first); the row's first chunk is stored from word dm/4 on and its last dm bytes (left
-// behind the last part) by dm/4 word stores: the row writes exactly its 4096 bytes.
-template <uint32_t kStage>
-__device__ __forceinline__ void store_row_coalesced_w(uint32_t *stage, uint8_t *dst, const uint32_t d[16], int lane,
-                                                      uint32_t dm) {
-    static_assert(kStage == 1024, "quarter-row staging");
-    constexpr int kParts = kRowBytes / kStage;
-    constexpr int kLanes = 64 / kParts;
-    constexpr int kTop = kStage / 4;  // word index of the bytes left behind a part
-    const int sw = (int)(dm >> 2);
-    uint8_t *base = dst - dm;  // 16-byte aligned
-#pragma unroll
-    for (int h = 0; h < kParts; ++h) {
-        if (h > 0 && lane < sw) stage[lane] = stage[kTop + lane];
-        if (lane / kLanes == h) {
-            const int b = sw + (lane % kLanes) * 16;
-#pragma unroll
-            for (int w = 0; w < 16; ++w) stage[b + w] = d[w];
-        }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        const u32x4 v = ((const u32x4 *)stage)[lane];
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        uint8_t *c = base + h * kStage + 16 * lane;
-        if (h > 0 || lane > 0) {
-            *(gwu32x4 *)c = v;
-        } else {
-            if (sw <= 1) *(gwuint *)(c + 4) = v.y;
-            if (sw <= 2) *(gwuint *)(c + 8) = v.z;
-            *(gwuint *)(c + 12) = v.w;
-        }
-    }
-    asm volatile("" ::: "memory");
-    if (lane < sw) *(gwuint *)(base + kRowBytes + 4 * lane) = stage[kTop + lane];
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
 }
 
 // d[15] of lane - 1 (lane 0 gets `carry`, the last lane's word of the previous row)
@@ -681,7 +641,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                                                             uint32_t *__restrict__ out) {
     static_assert(kWv >= kWaves, "the table builders need 256 threads");
     constexpr uint32_t kStage = Src::kCopy ? 1024u : 0u;     // a quarter row per part
-    constexpr uint32_t kArea = Src::kCopy ? kStage + 16u : 0u;  // + the carried bytes (dst % 16 = 4, 8, 12)
+    constexpr uint32_t kArea = kStage;
     __shared__ __attribute__((aligned(16))) uint32_t lds[(kLdsBytes + kWv * kArea) / 4];
     if constexpr (kWv == kWaves) {
         stage_tables<0>(lds, img, [] {});
@@ -744,10 +704,8 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                 const long long row0 = (long long)r * kRowBytes - (long long)g.P;
                 const bool whole = row0 >= 0 && row0 + kRowBytes <= (long long)cur.copylen;
                 uint32_t *area = lds + (kLdsBytes + (threadIdx.x >> 6) * kArea) / 4;
-                if (whole && dm == 0) {
+                if (whole && (dm & 3u) == 0) {
                     store_row_coalesced<kStage>(area, cur.dst + row0, d, lane);
-                } else if (whole && (dm & 3u) == 0) {
-                    store_row_coalesced_w<kStage>(area, cur.dst + row0, d, lane, dm);
                 } else {
                     if (r == 0) carry = 0;
                     const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
