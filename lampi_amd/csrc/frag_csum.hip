@@ -2616,9 +2616,17 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                            base, (uint32_t)n, frag_len, out, dst, dst_stride);
         return hipGetLastError();
     }
-    const uint32_t fpw = pick_fpw(n, 1);
-    hipLaunchKernelGGL(sum_rows_kernel<MsgCopySource>, grid_for(n, fpw), dim3(kBlock), 0, s,
-                       MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, fpw, out);
+    // ragged or unaligned: the fused-copy piece streams as for descriptor batches (4-byte-aligned
+    // destinations), sum_rows_kernel for the workgroups with byte-misaligned ones
+    const MsgCopySource src{base, msg_len, frag_len, 0u, dst, dst_stride};
+    if (!img) return hipErrorInvalidValue;
+    uint32_t fpg = 96;  // a multiple of 4 (kWaves): sum_rows_kernel's workgroups cover the same fragments
+    while (fpg > 4 && n / fpg < 2048) fpg = fpg > 12 ? fpg / 2 : 4;
+    uint8_t *trash = (uint8_t *)(uintptr_t)(img + kImgWords);
+    hipLaunchKernelGGL((crc_stream_kernel<MsgCopySource, kCopyD, 0, 1, true, kStreamWv, kStreamCap, 16, true>),
+                       frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, src, n, fpg, img, out, trash);
+    hipLaunchKernelGGL((sum_rows_kernel<MsgCopySource, uint32_t, true>), frags_grid(n, fpg), dim3(kBlock), 0, s, src,
+                       n, fpg / kWaves, out);
     return hipGetLastError();
 }
 

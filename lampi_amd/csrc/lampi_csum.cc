@@ -409,11 +409,9 @@ int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_
     int dev = 0;
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
-    const uint32_t *img = nullptr;
-    if (mode == LAMPI_CSUM_CRC32) {
-        e = device_tables(dev, &img);
-        if (e != hipSuccess) return to_int(e);
-    }
+    const uint32_t *img = nullptr;  // CRC: the tables; SUM: the zero chunk and trash slots of the streams
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
     return to_int(launch_msg_bcopy((const uint8_t *)d_msg, msg_len, frag_len, partial, (uint8_t *)d_dst, dst_stride, n,
                                    d_out, mode, img, (hipStream_t)stream));
 }

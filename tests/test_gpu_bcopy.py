@@ -197,6 +197,8 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     (4096 * 4097, 4096, 4096 + 32, 0),      # regular, 4 KiB, odd count in the last wave
     (65456 * 300 + 17, 65456, 65528, 0),    # GM payload into 72 + 65456-byte slots (general path)
     (1000003, 4096, 4100, 3),               # ragged everything
+    (65456 * 300 + 1000, 65456, 65536, 72),  # GM slots: payload after the 72-byte header (dst % 16 = 8)
+    (4096 * 5000 + 17, 4096, 4096 + 80, 72),  # 4 KiB payloads into 72-byte-header slots, ragged tail
     (5, 4096, 4096, 1),                     # one short fragment
 ])
 def test_msg_bcopy(cuda, oracle, mode, msg_len, frag_len, stride, dst_off):
