@@ -80,6 +80,7 @@ def parse():
                          "C: mixed 64 B - 64 KiB Zipf sizes, >= 4 GiB, seed 5 (1 GPU, descriptor batch); "
                          "D: 32M x 16 KiB over N GPUs, seed 3 (BASELINE config D, N >= 2)")
     ap.add_argument("--e2e", action="store_true", help="host-memory end-to-end path (config E)")
+    ap.add_argument("--latency", action="store_true", help="small-batch call latency (eager, synchronous, graph)")
     ap.add_argument("--bcopy", action="store_true",
                     help="fused copy + checksum batch (lampi_frag_bcopy_batch) on the config B shape")
     ap.add_argument("--desc", action="store_true",
@@ -542,8 +543,80 @@ def run_bcopy(args):
         "cpu_baseline": None}))
 
 
+def run_latency(args):
+    """Small batches: per-call time of lampi_frag_csum_batch over n 4 KiB descriptor
+    fragments, three ways -- stream-ordered back-to-back calls (device time per call, HIP events),
+    one call + synchronize (host round trip), and the same call replayed from a captured HIP graph.
+    Results are checked against a committed digest only where one exists (the full batch)."""
+    import numpy as np
+    import torch
+
+    from lampi_amd import device as dv
+
+    rank, world, _ = dist_setup()
+    if world != 1:
+        raise SystemExit("--latency is a single-GPU measurement")
+    L = 4096
+    nmax = 65536
+    buf = torch.empty(nmax * L, dtype=torch.uint8, device="cuda")
+    dv.fill_stream_frags(buf, nmax, L, 2)
+    descs = dv.make_descs(buf, np.arange(nmax, dtype=np.uint64) * L, np.full(nmax, L, np.uint64))
+    out = torch.empty(nmax, dtype=torch.int32, device="cuda")
+    rows = []
+    for n in (1, 16, 256, 4096, 65536):
+        run = lambda: dv.frag_csum_batch(descs, n=n, out=out)  # noqa: E731
+        for _ in range(20):
+            run()
+        torch.cuda.synchronize()
+        reps = 200
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        stream_us = e0.elapsed_time(e1) / reps * 1e3
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            run()
+            torch.cuda.synchronize()
+            t.append(time.perf_counter() - t0)
+        sync_us = float(np.median(t)) * 1e6
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            run()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            for _ in range(8):  # eight batches per replay (a send loop over eight messages)
+                run()
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(reps // 8):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        graph_us = e0.elapsed_time(e1) / (reps // 8 * 8) * 1e3
+        rows.append({"fragments": n, "bytes": n * L, "stream_us_per_call": round(stream_us, 2),
+                     "sync_round_trip_us": round(sync_us, 2), "graph_us_per_call": round(graph_us, 2),
+                     "GiB_per_s_stream": round(n * L / GIB / (stream_us / 1e6), 2)})
+    got = dv.as_u32(out[:nmax])
+    from lampi_amd import shard
+
+    digest = shard.digest(got, np.arange(nmax, dtype=np.uint64))
+    print(json.dumps({"metric": "small-batch latency of lampi_frag_csum_batch (4 KiB CRC descriptors)",
+                      "unit": "us", "results": rows, "last_batch_xor": f"{digest[0]:08x}"}), flush=True)
+
+
 def main():
     args = parse()
+    if args.latency:
+        run_latency(args)
+        return
     if args.bcopy:
         run_bcopy(args)
         return
