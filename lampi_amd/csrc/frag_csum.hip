@@ -2434,11 +2434,13 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
 // fragments per workgroup of crc_stream_kernel: 96 (measured: tools/microbench/frags_ablation.hip,
 // 12-wave workgroups -- 96 beat 64/128/192/256 on config C and on 4 KiB descriptors: shorter
 // workgroups shrink the end-of-kernel tail, and 96 uniform 4 KiB fragments are 8 rows per chain),
-// halved for small batches so that they still spread over the chip (a 16 MiB chunk of
-// 65,456-byte fragments is only 256 fragments)
+// halved for small batches until they give one workgroup per CU (a 16 MiB chunk of 65,456-byte
+// fragments is only 256 fragments).  Every workgroup stages ~77 KiB of LDS tables, so more
+// workgroups than CUs only repeat that prologue: 4,096 x 4 KiB took 21.9 us at >= 2048
+// workgroups, 14.6 us at >= 512, 9.95 us at >= 256 (bench.py --latency); config C unchanged.
 static uint32_t frags_per_wg(size_t n) {
     uint32_t fpg = 96;
-    while (fpg > 3 && n / fpg < 2048) fpg >>= 1;
+    while (fpg > 3 && n / fpg < 256) fpg >>= 1;
     return fpg;
 }
 
