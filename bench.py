@@ -604,6 +604,24 @@ def run_latency(args):
         rows.append({"fragments": n, "bytes": n * L, "stream_us_per_call": round(stream_us, 2),
                      "sync_round_trip_us": round(sync_us, 2), "graph_us_per_call": round(graph_us, 2),
                      "GiB_per_s_stream": round(n * L / GIB / (stream_us / 1e6), 2)})
+    # the same fragments as one contiguous message (lampi_msg_csum: the regular kernel)
+    msg_rows = []
+    for n in (256, 4096, 65536):
+        run = lambda: dv.msg_csum(buf[:n * L], L, out=out)  # noqa: E731
+        for _ in range(20):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(200):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / 200 * 1e3
+        msg_rows.append({"fragments": n, "bytes": n * L, "stream_us_per_call": round(us, 2),
+                         "GiB_per_s_stream": round(n * L / GIB / (us / 1e6), 2)})
+    rows.append({"lampi_msg_csum": msg_rows})
+    dv.frag_csum_batch(descs, n=nmax, out=out)
     got = dv.as_u32(out[:nmax])
     from lampi_amd import shard
 
