@@ -507,6 +507,10 @@ def run_bcopy(args):
     descs_d8 = dv.make_copy_descs(src, offs[:-1], dst, offs[:-1] + np.uint64(8), np.full(n - 1, L), np.full(n - 1, L))
     _, kern_dst8 = timed(lambda: dv.frag_bcopy_batch(descs_d8, n=n - 1, mode=mode, out=out))
     copyd8_ok = bool(torch.equal(src[:(n - 1) * L], dst[8:8 + (n - 1) * L]))
+    # byte-misaligned destinations (dst + 1)
+    descs_d1 = dv.make_copy_descs(src, offs[:-1], dst, offs[:-1] + np.uint64(1), np.full(n - 1, L), np.full(n - 1, L))
+    _, kern_dst1 = timed(lambda: dv.frag_bcopy_batch(descs_d1, n=n - 1, mode=mode, out=out))
+    copyd1_ok = bool(torch.equal(src[:(n - 1) * L], dst[1:1 + (n - 1) * L]))
     _, kern_copy = timed(lambda: dst.copy_(src))
     moved = 2.0 * n * L
     achieved = moved / kern / 1e9
@@ -535,6 +539,10 @@ def run_bcopy(args):
                                           "72-byte header); copy checked", "kernel_avg_ms": round(kern_dst8 * 1e3, 4),
                                   "frac": round(2.0 * (n - 1) * L / kern_dst8 / 1e9 / HBM_PEAK_GBS, 4),
                                   "copy_ok": copyd8_ok},
+        "descriptor_batch_dst1": {"what": "n-1 fragments from aligned src to dst + 1 (byte-misaligned); copy checked",
+                                  "kernel_avg_ms": round(kern_dst1 * 1e3, 4),
+                                  "frac": round(2.0 * (n - 1) * L / kern_dst1 / 1e9 / HBM_PEAK_GBS, 4),
+                                  "copy_ok": copyd1_ok},
         "copy_reference": {"what": "torch dst.copy_(src), same bytes, no checksum",
                            "kernel_avg_ms": round(kern_copy * 1e3, 4),
                            "achieved_GBs": round(moved / kern_copy / 1e9, 1)},

@@ -460,7 +460,8 @@ __device__ __forceinline__ void store64(uint8_t *dst, long long o, const uint32_
 // carried bytes and 21% for word stores).  LDS operations of one wave complete in order, so the
 // area is reused without a barrier; the asm fences only keep the compiler from reordering them.
 template <uint32_t kStage>
-__device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *dst, const uint32_t d[16], int lane) {
+__device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *dst, const uint32_t d[16], int lane,
+                                                    bool skip0 = false) {
     static_assert(kStage == 1024 || kStage == 2048, "half- or quarter-row staging");
     constexpr int kParts = kRowBytes / kStage;  // lanes 64/kParts per part
     constexpr int kLanes = 64 / kParts;
@@ -481,7 +482,16 @@ __device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *ds
         asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int i = 0; i < kRd; ++i) *(gwu32x4 *)(dst + h * kStage + 1024 * i + 16 * lane) = v[i];
+        for (int i = 0; i < kRd; ++i) {
+            gwbyte *c = (gwbyte *)(dst + h * kStage + 1024 * i + 16 * lane);
+            if (h == 0 && i == 0 && lane == 0 && skip0) {  // the row's first word is the caller's
+                *(gwuint *)(c + 4) = v[i].y;
+                *(gwuint *)(c + 8) = v[i].z;
+                *(gwuint *)(c + 12) = v[i].w;
+            } else {
+                *(gwu32x4 *)c = v[i];
+            }
+        }
     }
 }
 
@@ -706,6 +716,24 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                 uint32_t *area = lds + (kLdsBytes + (threadIdx.x >> 6) * kArea) / 4;
                 if (whole && (dm & 3u) == 0) {
                     store_row_coalesced<kStage>(area, cur.dst + row0, d, lane);
+                } else if (whole) {
+                    // byte-misaligned: the aligned words covering [row0 - m, row0 - m + 4096) (as
+                    // store64 forms them) go out coalesced at the dword-aligned dst + row0 - m; the
+                    // row's first word (when it reaches before the copy) and, on the frame's last
+                    // row, the word holding its last m bytes go through bounded word stores
+                    if (r == 0) carry = 0;
+                    const uint32_t m = dm & 3u, sh = 4u - m;
+                    const uint32_t prev = prev_lane_top(d[15], carry, lane);
+                    uint32_t v[16];
+                    v[0] = __builtin_amdgcn_alignbyte(d[0], prev, sh);
+#pragma unroll
+                    for (int w = 1; w < 16; ++w) v[w] = __builtin_amdgcn_alignbyte(d[w], d[w - 1], sh);
+                    const bool skip0 = row0 < 4;
+                    store_row_coalesced<kStage>(area, cur.dst + row0 - m, v, lane, skip0);
+                    if (skip0 && lane == 0) store_word(cur.dst, row0 - (long long)m, v[0], 0, (long long)cur.copylen);
+                    if (lane == 63 && r + 1 == g.R)
+                        store_word(cur.dst, row0 - (long long)m + kRowBytes, __builtin_amdgcn_alignbyte(0u, d[15], sh), 0,
+                                   (long long)cur.copylen);
                 } else {
                     if (r == 0) carry = 0;
                     const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
