@@ -1929,6 +1929,7 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 template <class Src, class Acc = uint32_t, bool kSkipFast = false>
 __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uint32_t fpw, Acc *__restrict__ out) {
     const int lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) uint32_t stage[Src::kCopy ? kWaves * 1024 / 4 : 1];  // per-wave copy staging
     if constexpr (kSkipFast) {
         const size_t g = (size_t)blockIdx.x * kWaves * fpw + threadIdx.x;
         bool slow = false;
@@ -1966,8 +1967,31 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
             load64(fb, o, ph, (long long)span, mask, s16, d);
             if constexpr (Src::kCopy) {
                 if (fi.copylen) {
-                    const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
-                    store64(db, o, d, ph, (long long)fi.copylen + ph, dm & 3u, dm == 0, prev, lane == 63 && r + 1 == R);
+                    // whole rows inside the copy: staged 1 KiB-coalesced stores at the dword-aligned
+                    // db + row0 - m (as in crc_rows_kernel); edge rows: word/byte stores
+                    const long long row0 = (long long)r * kRowBytes, lo = ph, hi = (long long)fi.copylen + ph;
+                    const uint32_t m = dm & 3u;
+                    const uint32_t prev = m ? prev_lane_top(d[15], carry, lane) : 0u;
+                    if (row0 >= lo && row0 + kRowBytes <= hi) {
+                        uint32_t *area = stage + (threadIdx.x >> 6) * (1024 / 4);
+                        if (m == 0) {
+                            store_row_coalesced<1024>(area, db + row0, d, lane);
+                        } else {
+                            const uint32_t sh = 4u - m;
+                            uint32_t v[16];
+                            v[0] = __builtin_amdgcn_alignbyte(d[0], prev, sh);
+#pragma unroll
+                            for (int w = 1; w < 16; ++w) v[w] = __builtin_amdgcn_alignbyte(d[w], d[w - 1], sh);
+                            const bool skip0 = row0 < lo + 4;
+                            store_row_coalesced<1024>(area, db + row0 - m, v, lane, skip0);
+                            if (skip0 && lane == 0) store_word(db, row0 - (long long)m, v[0], lo, hi);
+                            if (lane == 63 && r + 1 == R)
+                                store_word(db, row0 - (long long)m + kRowBytes, __builtin_amdgcn_alignbyte(0u, d[15], sh),
+                                           lo, hi);
+                        }
+                    } else {
+                        store64(db, o, d, ph, hi, m, dm == 0, prev, lane == 63 && r + 1 == R);
+                    }
                     carry = __builtin_amdgcn_readlane(d[15], 63);
                 }
             }
