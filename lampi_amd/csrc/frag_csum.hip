@@ -2657,8 +2657,8 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                             size_t dst_stride, size_t n, uint32_t *out, int mode, const uint32_t *img, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const bool regular = msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 &&
-                         ((uintptr_t)base & 15u) == 0 && ((uintptr_t)dst & 15u) == 0 && dst_stride % 16 == 0 &&
-                         n <= 0xFFFFFFFFull;
+                         ((uintptr_t)base & 15u) == 0 && ((uintptr_t)dst & 3u) == 0 && dst_stride % 4 == 0 &&
+                         n <= 0xFFFFFFFFull;  // dword-aligned dwordx4 stores run at the aligned rate (GM slots)
     if (mode == LAMPI_CSUM_CRC32) {
         if (regular) return launch_crc_regular_copy(base, n, frag_len, partial, dst, dst_stride, out, img, s);
         launch_crc_rows_copy(MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n,

@@ -199,6 +199,8 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     (1000003, 4096, 4100, 3),               # ragged everything
     (65456 * 300 + 1000, 65456, 65536, 72),  # GM slots: payload after the 72-byte header (dst % 16 = 8)
     (4096 * 5000 + 17, 4096, 4096 + 80, 72),  # 4 KiB payloads into 72-byte-header slots, ragged tail
+    (4096 * 20001, 4096, 4096 + 80, 72),    # regular kernel into 72-byte-header slots (dst % 16 = 8)
+    (16384 * 3001, 16384, 16384 + 76, 4),   # regular, 16 KiB, slot stride and base only 4-byte aligned
     (5, 4096, 4096, 1),                     # one short fragment
 ])
 def test_msg_bcopy(cuda, oracle, mode, msg_len, frag_len, stride, dst_off):
