@@ -14,12 +14,22 @@ Prints ONE JSON line (rank 0):
   roofline   = dominant kernel's algorithmic bytes per launch (= 16 GiB payload) / its
                average launch duration from HIP events on the launch stream, vs 8.0 TB/s
   cpu_baseline = the reference's uicrc (oracle/_ref, compiled from /root/reference) or the
-               clean-room port, on this host's cores, over a bounded sample of the workload
+               clean-room port, on this host's cores (1 and the affinity mask), over BASELINE
+               config A exactly (seed 1, 1M x 1 KiB), digest-checked
   parity     = digest of all ranks' results (global fragment indices) vs committed digests
                (tests/golden/bench_digests.json, made by the oracle in the build
                container).  Only the cpu_baseline leg imports oracle/.
 
+Multi-GPU: under torchrun (WORLD_SIZE set) WORLD_SIZE must equal --gpus; `python bench.py
+--gpus N` without a launcher starts the N rank processes itself (the parent never touches the
+GPU).  Every rank's kernel average is gathered into `per_gpu` (GiB/s and roofline fraction per
+GPU) and `aggregate` (all bytes / slowest kernel / N x 8 TB/s).  A node with fewer GPUs than
+ranks fails loudly.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frags F] [--frag-bytes L]
+       python bench.py --config D --gpus N   # 32M x 16 KiB over N >= 4 GPUs (<= 200 GiB per rank)
+       python bench.py --config D --shard g  # GPU g's full 64 GiB shard of the 8-GPU partition, 1 GPU
+       python bench.py --gpus 2 --dry-run    # CPU rehearsal of the rank launch (gloo, no kernel)
        python bench.py --e2e        # host-memory path (config E), for DESIGN.md
 """
 from __future__ import annotations
@@ -58,27 +68,46 @@ def golden_digest(seed: int, n_total: int, L: int, crc: bool):
             entries = json.load(f)["entries"]
     except (OSError, ValueError, KeyError):
         return None
+    m = "crc" if crc else "sum"
     for e in entries:
-        if (e["seed"], e["n_total"], e["frag_bytes"], e["mode"]) == (seed, n_total, L, "crc" if crc else "sum"):
+        if (e["seed"], e["n_total"], e["frag_bytes"], e["mode"], e.get("nshard", 1)) == (seed, n_total, L, m, 1):
             return e["xor"], e["wsum"]
+    # the whole batch from a complete set of committed shard digests (config D: 8 shards)
+    shards = {}
+    for e in entries:
+        if (e["seed"], e["n_total"], e["frag_bytes"], e["mode"]) == (seed, n_total, L, m) and "nshard" in e:
+            shards.setdefault(e["nshard"], {})[e["shard"]] = (e["xor"], e["wsum"])
+    for ns, parts in shards.items():
+        if len(parts) == ns:
+            x, w = 0, 0
+            for px, pw in parts.values():
+                x, w = x ^ px, (w + pw) & 0xFFFFFFFF
+            return x, w
     return None
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU). Without WORLD_SIZE in the environment, bench.py starts N rank "
+                         "processes itself; under torchrun WORLD_SIZE must equal N")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--frags", type=int, default=4194304, help="fragments per GPU")
+    ap.add_argument("--frags", type=int, default=None, help="fragments per GPU (default: the config's)")
     ap.add_argument("--frag-bytes", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--mode", choices=["crc", "sum"], default="crc")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-bytes", type=int, default=1 << 30)
     ap.add_argument("--config", choices=["B", "C", "D"], default="B",
                     help="B: 4M x 4 KiB per GPU, seed 2 (default, weak scaling); "
                          "C: mixed 64 B - 64 KiB Zipf sizes, >= 4 GiB, seed 5 (1 GPU, descriptor batch); "
-                         "D: 32M x 16 KiB over N GPUs, seed 3 (BASELINE config D, N >= 2)")
+                         "D: 32M x 16 KiB over N GPUs, seed 3 (BASELINE config D; per-rank shard <= 200 GiB)")
+    ap.add_argument("--shard", type=int, default=None,
+                    help="with --config D on one GPU: checksum GPU g's full shard of the 8-GPU partition "
+                         "(4M x 16 KiB = 64 GiB, k = g mod 8) and check BASELINE.md's per-GPU digest")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the rank launch (gloo, no GPU): per-rank checksums come from "
+                         "tests/golden/config_b_head.json instead of a kernel; nothing is measured")
     ap.add_argument("--e2e", action="store_true", help="host-memory end-to-end path (config E)")
     ap.add_argument("--latency", action="store_true", help="small-batch call latency (eager, synchronous, graph)")
     ap.add_argument("--bcopy", action="store_true",
@@ -86,21 +115,91 @@ def parse():
     ap.add_argument("--desc", action="store_true",
                     help="run the batch through descriptors (lampi_frag_csum_batch, the general kernel) "
                          "instead of the contiguous-message entry point (diagnostic)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.frags is None:
+        args.frags = (1024 // args.gpus) if args.dry_run else 4194304
+    return args
 
 
-def dist_setup():
-    import torch
-    import torch.distributed as dist
+MAX_SHARD_BYTES = 200 << 30  # per-rank payload cap: 288 GB of HBM less the allocator's and runtime's share
 
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` (N > 1) without a launcher: start N rank processes of this
+    script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), the
+    same environment torchrun gives them.  This parent never touches the GPU (it does not even
+    import torch), so the children are ordinary processes, not re-execs of a GPU process.  If
+    a rank fails, the others are stopped and the parent exits with the failing rank's code."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    def forward(signum, _frame):  # a launcher stopped by a time limit takes its ranks with it
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(signal.SIGTERM)
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.05)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+    return rc
+
+
+def dist_setup(args):
+    """Rank, world size and local rank from the launcher's environment; the world size must be
+    the --gpus the driver asked for, and a node must have a GPU for every local rank."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    import torch.distributed as dist
+
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        return rank, world, local
+    import torch
+
+    ndev = torch.cuda.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if ndev < local_world or local >= ndev:
+        raise SystemExit(f"bench.py: {local_world} ranks on this node need {local_world} GPUs; "
+                         f"{ndev} visible (rank {rank}, local rank {local})")
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return rank, world, local
+
+
+def _coll_device(args):
+    return "cpu" if args.dry_run else "cuda"
 
 
 def barrier(world):
@@ -110,36 +209,59 @@ def barrier(world):
         dist.barrier()
 
 
-def max_over_ranks(x: float, world: int) -> float:
+def max_over_ranks(x: float, world: int, args=None) -> float:
     import torch
     import torch.distributed as dist
 
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_coll_device(args) if args else "cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
-def cpu_baseline(L: int, seed: int, sample_bytes: int):
-    """Time the reference's uicrc (or the port) on the host cores over a bounded sample."""
+def gather_rows(row, world: int, args) -> list:
+    """Every rank's `row` (list of floats), in rank order (all_gather; rank 0 reports them)."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return [list(row)]
+    t = torch.tensor(row, dtype=torch.float64, device=_coll_device(args))
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]
+
+
+def cpu_baseline():
+    """BASELINE config A exactly (BASELINE.md "CPU-baseline plan"): the reference's uicrc
+    (oracle/_ref, compiled from /root/reference/src/util/MemFunctions.cc) -- or the clean-room
+    port where that library was not built -- over seed 1, 1,048,576 x 1,024 B, on 1 core and on
+    every core of this process's affinity mask; both results are checked against config A's
+    digest (feb61101 / 41fadf13)."""
+    import numpy as np
+
+    from lampi_amd import shard
     from oracle.oracle import Reference, Restatement
 
+    seed, n, L = 1, 1048576, 1024
+    want = GOLDEN[(seed, n, L)]
     port = Restatement()
     kind, fn, src = "port", port.uicrc_addr(), "oracle/libcsum_ref.so (clean-room restatement)"
     try:
         ref = Reference()
-        kind, fn, src = "reference", ref.uicrc_addr(), "oracle/_ref/libref_memfunctions.so (ref MemFunctions.cc)"
+        kind, fn, src = "reference", ref.uicrc_addr(), "oracle/_ref/libref_memfunctions.so (reference MemFunctions.cc)"
     except (FileNotFoundError, OSError):
         pass
-    n = max(1, sample_bytes // L)
     buf = port.stream(seed, 0, n * L)
-    t1, x1 = port.time_crc_fn(fn, buf, n, L, 1)
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", cores))))
-    tn, xn = port.time_crc_fn(fn, buf, n, L, cores)
-    if x1 != xn:
-        raise RuntimeError("CPU baseline single/multi-thread results differ")
+    out1 = np.empty(n, dtype=np.uint32)
+    t1, _ = port.time_crc_fn(fn, buf, n, L, 1, out=out1)
+    mask = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
+    cores = len(mask)
+    outn = np.empty(n, dtype=np.uint32)
+    tn, _ = port.time_crc_fn(fn, buf, n, L, cores, out=outn)
+    ks = np.arange(n, dtype=np.uint64)
+    d1, dn = shard.digest(out1, ks), shard.digest(outn, ks)
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -151,9 +273,13 @@ def cpu_baseline(L: int, seed: int, sample_bytes: int):
         pass
     return {
         "value": round(n * L / GIB / t1, 4), "unit": "GiB/s", "cores": 1, "kind": kind,
-        "sample": f"{n} x {L} B fragments of stream seed {seed} ({n * L / GIB:.2f} GiB), uicrc init 0xFFFFFFFF, "
-                  f"{src}; timed {t1:.2f} s on 1 core",
-        "all_cores": {"value": round(n * L / GIB / tn, 3), "cores": cores, "seconds": round(tn, 3)},
+        "sample": f"BASELINE config A exactly: {n} x {L} B fragments of stream seed {seed} (1 GiB), "
+                  f"uicrc init 0xFFFFFFFF, {src}; {t1:.2f} s on 1 core",
+        "parity_ok": bool(d1 == want and dn == want),
+        "digest": f"{d1[0]:08x}/{d1[1]:08x} (config A: {want[0]:08x}/{want[1]:08x})",
+        "all_cores": {"value": round(n * L / GIB / tn, 3), "cores": cores, "seconds": round(tn, 3),
+                      "affinity": f"{cores} of the host's {os.cpu_count()} CPUs are in this process's affinity mask; "
+                                  f"one thread each"},
         "cpu_model": model,
     }
 
@@ -170,84 +296,176 @@ def read_traffic(config_key: str):
         return None
 
 
+def shard_golden(seed: int, n_total: int, L: int, crc: bool, nshard: int, shard_id: int):
+    """Committed digest (XOR, WSUM with global k) of shard k = shard_id (mod nshard), or None."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")) as f:
+            entries = json.load(f)["entries"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for e in entries:
+        if (e["seed"], e["n_total"], e["frag_bytes"], e["mode"], e.get("nshard", 1), e.get("shard", 0)) == \
+                (seed, n_total, L, "crc" if crc else "sum", nshard, shard_id):
+            return e["xor"], e["wsum"]
+    return None
+
+
+def shard_plan(args, world: int, rank: int):
+    """(fragments on this rank n, L, seed, first global index k0, index step, global count) for
+    the uniform configs -- checked before any GPU is touched.  Config D is 32M x 16 KiB over
+    the ranks (or, with --shard g, GPU g's shard of the 8-GPU partition on one GPU); no rank may
+    hold more than MAX_SHARD_BYTES."""
+    n, L, seed = args.frags, args.frag_bytes, args.seed
+    k0, kstep, n_global = rank, world, n * world  # round-robin shard k = rank (mod world)
+    if args.config == "D":
+        L, seed = 16384, 3
+        if args.shard is not None:
+            if world != 1 or not 0 <= args.shard < 8:
+                raise SystemExit("--shard g (0..7) runs one 8-GPU config D shard on a single GPU")
+            n, n_global, k0, kstep = 33554432 // 8, 33554432, args.shard, 8
+        else:
+            if 33554432 % world:
+                raise SystemExit("config D: 32M fragments do not split evenly over this many GPUs")
+            n, n_global = 33554432 // world, 33554432
+        if n * L > MAX_SHARD_BYTES:
+            raise SystemExit(f"config D on {world} GPU(s): {n * L / GIB:.0f} GiB per rank exceeds the "
+                             f"{MAX_SHARD_BYTES / GIB:.0f} GiB per-GPU cap (use >= 4 GPUs, or --shard g)")
+    elif args.shard is not None:
+        raise SystemExit("--shard is a config D option")
+    if n * L > MAX_SHARD_BYTES:
+        raise SystemExit(f"{n * L / GIB:.0f} GiB per rank exceeds the {MAX_SHARD_BYTES / GIB:.0f} GiB per-GPU cap")
+    return n, L, seed, k0, kstep, n_global
+
+
 def run_device(args):
+    """One rank of the device-resident bench: fill this rank's shard in HBM, time K launches."""
     import numpy as np
     import torch
 
-    from lampi_amd import device as dv
     from lampi_amd import shard
 
-    rank, world, _ = dist_setup()
-    n, L = args.frags, args.frag_bytes
-    if args.config == "D":
-        if world < 2:
-            raise SystemExit("config D (512 GiB) needs N >= 2 GPUs")
-        n, L, args.seed = 33554432 // world, 16384, 3
-    mode = dv.CRC32 if args.mode == "crc" else dv.SUM32
-    stream = torch.cuda.current_stream()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    n, L, seed, k0, kstep, n_global = shard_plan(args, world, int(os.environ.get("RANK", "0")))
+    rank, world, local = dist_setup(args)
+    crc = args.mode == "crc"
+    ks = np.arange(n, dtype=np.uint64) * np.uint64(kstep) + np.uint64(k0)  # global fragment indices
 
-    buf = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    dv.fill_stream_frags(buf, n, L, args.seed, k0=rank, kstep=world)  # shard k = rank (mod world)
-    out = torch.empty(n, dtype=torch.int32, device="cuda")
-    if args.desc:
-        descs = dv.make_descs(buf, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint64))
-        run = lambda: dv.frag_csum_batch(descs, mode=mode, out=out)  # noqa: E731
+    if args.dry_run:
+        # CPU rehearsal: no kernel; the rank's "checksums" are the reference's, committed
+        with open(os.path.join(ROOT, "tests", "golden", "config_b_head.json")) as f:
+            head = json.load(f)
+        if (seed, L) != (head["seed"], head["frag_bytes"]) or n_global > head["n"]:
+            raise SystemExit(f"--dry-run covers config B's first {head['n']} fragments (seed 2, 4 KiB)")
+        table = np.array(head["crc" if crc else "sum"], dtype=np.uint32)
+        box = {}
+
+        def run():
+            box["vals"] = table[ks.astype(np.int64)]
     else:
-        run = lambda: dv.msg_csum(buf, L, mode=mode, out=out)  # noqa: E731
-    torch.cuda.synchronize()
+        from lampi_amd import device as dv
+
+        mode = dv.CRC32 if crc else dv.SUM32
+        stream = torch.cuda.current_stream()
+        buf = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+        dv.fill_stream_frags(buf, n, L, seed, k0=k0, kstep=kstep)
+        out = torch.empty(n, dtype=torch.int32, device="cuda")
+        if args.desc:
+            descs = dv.make_descs(buf, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint64))
+            run = lambda: dv.frag_csum_batch(descs, mode=mode, out=out)  # noqa: E731
+        else:
+            run = lambda: dv.msg_csum(buf, L, mode=mode, out=out)  # noqa: E731
+        torch.cuda.synchronize()
+
+    def sync():
+        if not args.dry_run:
+            torch.cuda.synchronize()
 
     # warm-up: the W launches, then more until 0.5 s have passed (the first dispatches of a fresh
     # process ramp from 2.8-3.4 ms down to the steady 2.63 ms: clock/power ramp)
     nw, t_w = 0, time.perf_counter()
-    while nw < args.warmup or time.perf_counter() - t_w < 0.5:
+    while nw < args.warmup or (not args.dry_run and time.perf_counter() - t_w < 0.5):
         run()
-        torch.cuda.synchronize()
+        sync()
         nw += 1
 
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    evs[0].record(stream)
-    for i in range(args.steps):
-        run()
-        evs[i + 1].record(stream)
-    torch.cuda.synchronize()
+    sync()
+    if args.dry_run:
+        t0 = time.perf_counter()
+        kern_ms = []
+        for i in range(args.steps):
+            ts = time.perf_counter()
+            run()
+            kern_ms.append((time.perf_counter() - ts) * 1e3)
+        t1 = time.perf_counter()
+        vals = box["vals"]
+    else:
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        t0 = time.perf_counter()
+        evs[0].record(stream)
+        for i in range(args.steps):
+            run()
+            evs[i + 1].record(stream)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+        vals = dv.as_u32(out)
     barrier(world)
-    t1 = time.perf_counter()
-    wall = max_over_ranks(t1 - t0, world)
-    kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    t2 = time.perf_counter()
+    wall = max_over_ranks(t2 - t0, world, args)
     kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
 
-    # parity: the digest over all ranks' checksums (global fragment indices) vs committed digests
-    vals = dv.as_u32(out)
-    gk = np.arange(n, dtype=np.uint64) * world + rank
-    want = golden_digest(args.seed, n * world, L, mode == dv.CRC32)
-    local = shard.digest(vals, gk)
-    whole = shard.allreduce_digest(local) if world > 1 else local
+    # parity: this rank's shard digest (global fragment indices), combined over the ranks, vs
+    # committed digests
+    local = shard.digest(vals, ks)
+    if args.dry_run:
+        whole = shard.allreduce_digest(local) if world > 1 else local
+        want = tuple(head["digest_crc" if crc else "digest_sum"]) if n_global == head["n"] else None
+        check = "combined shard digests vs tests/golden/config_b_head.json (reference values)"
+    elif args.shard is not None:
+        whole = local
+        want = shard_golden(seed, n_global, L, crc, 8, args.shard)
+        check = f"config D shard {args.shard} of 8 (64 GiB): digest vs tests/golden/bench_digests.json" + \
+                (" and BASELINE.md per-GPU XOR" if crc else "")
+        if want is not None and crc and want[0] != CONFIG_D_SHARD_XOR[args.shard]:
+            raise SystemExit("tests/golden/bench_digests.json disagrees with BASELINE.md")
+    else:
+        whole = shard.allreduce_digest(local) if world > 1 else local
+        want = golden_digest(seed, n_global, L, crc)
+        check = "full digest vs BASELINE.md / tests/golden/bench_digests.json"
     if want is not None:
         ok = whole == tuple(want)
-        if args.config == "D" and world == 8:
+        if args.config == "D" and world == 8 and crc:
             ok = ok and local[0] == CONFIG_D_SHARD_XOR[rank]
-        parity = {"check": "full digest vs BASELINE.md / tests/golden/bench_digests.json"
-                           + (" (per-GPU shard XOR too)" if args.config == "D" and world == 8 else ""),
-                  "xor": f"{whole[0]:08x}", "wsum": f"{whole[1]:08x}", "ok": ok}
+            check += " (per-GPU shard XOR too)"
+        parity = {"check": check, "xor": f"{whole[0]:08x}", "wsum": f"{whole[1]:08x}", "ok": ok}
     else:
         parity = {"check": "no committed digest for this shape (tests/golden/make_bench_digests.py)",
                   "xor": f"{whole[0]:08x}", "wsum": f"{whole[1]:08x}", "ok": None}
-    ok_all = parity["ok"] is not False
-    if world > 1:
-        t = torch.tensor([0 if ok_all else 1], device="cuda")
-        torch.distributed.all_reduce(t)
-        ok_all = int(t.item()) == 0
+    bad = 0 if parity["ok"] is not False else 1
+    # per-rank rows: [kernel avg s, bytes, parity failure, local wall s]
+    rows = gather_rows([kern_avg_s, float(n) * L, float(bad), t1 - t0], world, args)
 
-    bytes_total = float(n) * L * world
-    value = bytes_total / GIB / wall * args.steps
-    achieved = n * L / kern_avg_s / 1e9
     result = None
     if rank == 0:
-        cfg_key = f"{'crc' if mode == dv.CRC32 else 'sum'}_{n}x{L}"
-        traffic = read_traffic(cfg_key)
+        bytes_total = sum(r[1] for r in rows)
+        value = bytes_total / GIB / wall * args.steps
+        achieved = n * L / kern_avg_s / 1e9
+        kmax = max(r[0] for r in rows)
+        per_gpu = [{"rank": i, "bytes": int(r[1]), "kernel_avg_ms": round(r[0] * 1e3, 4),
+                    "GiB_per_s": round(r[1] / GIB / r[0], 2),
+                    "roofline_frac": round(r[1] / r[0] / 1e9 / HBM_PEAK_GBS, 4),
+                    "parity_ok": r[2] == 0} for i, r in enumerate(rows)]
+        cfg_key = f"{'crc' if crc else 'sum'}_{n}x{L}"
+        traffic = None if args.dry_run else read_traffic(cfg_key)
+        kernel = ("none (dry run)" if args.dry_run else
+                  "crc_stream_kernel (descriptors)" if args.desc and crc else
+                  "crc_stream_kernel<kSum> (descriptors)" if args.desc else
+                  "crc_regular_kernel" if crc else "crc_regular_kernel (kSum: uicsum on the same schedule)")
+        workload = (f"config D shard {args.shard} of 8: {n} x {L} B fragments k = {args.shard} (mod 8), seed 3"
+                    if args.shard is not None else
+                    f"{n} x {L} B fragments per GPU, device-resident, "
+                    f"{'CRC-32/MPEG-2 (uicrc)' if crc else 'uicsum'}, one wavefront per fragment")
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -261,30 +479,35 @@ def run_device(args):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": f"synthetic: splitmix64 stream seed {args.seed} (SURVEY.md 8(d)), generated on device",
+            "data": (f"synthetic: splitmix64 stream seed {seed} (SURVEY.md 8(d)), generated on device"
+                     if not args.dry_run else "dry run: reference checksums of config B's first fragments"),
             "config": {
-                "workload": f"{n} x {L} B fragments per GPU, device-resident, "
-                            f"{'CRC-32/MPEG-2 (uicrc)' if mode == dv.CRC32 else 'uicsum'}, one wavefront per fragment",
+                "workload": workload,
                 "fragments_per_gpu": n, "frag_bytes": L, "bytes_per_gpu": n * L,
-                "sharding": "round-robin k = rank (mod N), no collective",
+                "sharding": f"round-robin k = {'g' if args.shard is not None else 'rank'} (mod {kstep}), "
+                            f"no collective",
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic.get("hbm_bytes_per_launch"),
-                "kernel": ("crc_stream_kernel (descriptors)" if args.desc and mode == dv.CRC32 else
-                           "sum_rows_kernel (descriptors)" if args.desc else
-                           "crc_regular_kernel" if mode == dv.CRC32 else
-                           "crc_regular_kernel (kSum: uicsum on the same schedule)"),
+                "kernel": kernel,
                 "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                 "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2], max(kern_ms))],
                 "algorithmic_bytes_per_launch": n * L,
                 "traffic_source": None if traffic is None else traffic.get("source"),
+                "note": "rank 0's kernel; every rank's in per_gpu",
             },
-            "parity": {**parity, "all_ranks_ok": ok_all},
+            "per_gpu": per_gpu,
+            "aggregate": {"GiB_per_s_kernel": round(bytes_total / GIB / kmax, 2),
+                          "roofline_frac": round(bytes_total / kmax / 1e9 / (HBM_PEAK_GBS * world), 4),
+                          "note": "sum of all ranks' bytes / slowest rank's kernel average / (N x 8 TB/s)"},
+            "parity": {**parity, "all_ranks_ok": all(r[2] == 0 for r in rows)},
         }
-        if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(L, args.seed, args.cpu_sample_bytes)
+        if args.dry_run:
+            result["dry_run"] = True
+        if world == 1 and not args.no_cpu_baseline and not args.dry_run and args.shard is None:
+            result["cpu_baseline"] = cpu_baseline()
         else:
             result["cpu_baseline"] = None
     return rank, world, result
@@ -299,7 +522,7 @@ def run_mixed(args):
     from lampi_amd import shard
     from lampi_amd.workload import zipf_lengths
 
-    rank, world, _ = dist_setup()
+    rank, world, _ = dist_setup(args)
     if world != 1:
         raise SystemExit("config C is a single-GPU configuration")
     lens = zipf_lengths(4 << 30)
@@ -454,7 +677,7 @@ def run_bcopy(args):
     from lampi_amd import device as dv
     from lampi_amd import shard
 
-    rank, world, _ = dist_setup()
+    rank, world, _ = dist_setup(args)
     if world != 1:
         raise SystemExit("--bcopy is a single-GPU measurement")
     n, L = args.frags, args.frag_bytes
@@ -561,7 +784,7 @@ def run_latency(args):
 
     from lampi_amd import device as dv
 
-    rank, world, _ = dist_setup()
+    rank, world, _ = dist_setup(args)
     if world != 1:
         raise SystemExit("--latency is a single-GPU measurement")
     L = 4096
@@ -640,6 +863,8 @@ def run_latency(args):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     if args.latency:
         run_latency(args)
         return
@@ -659,6 +884,8 @@ def main():
         import torch.distributed as dist
 
         dist.destroy_process_group()
+    if result is not None and not result["parity"]["all_ranks_ok"]:
+        sys.exit(3)  # a rank's checksums differ from the committed digests
 
 
 if __name__ == "__main__":

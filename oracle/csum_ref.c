@@ -323,17 +323,23 @@ double oracle_time_uniform(uint64_t seed, size_t n, size_t L, int mode, int nthr
 
 /* Time `fn` (a uicrc-shaped function: the restatement's oracle_uicrc or the reference's
  * uicrc(const void*, unsigned long, unsigned int)) over n fragments of L bytes in buf,
- * nthreads threads, init register 0xFFFFFFFF.  Returns seconds; XOR of results in *xor_out. */
+ * nthreads threads, init register 0xFFFFFFFF.  Returns seconds; XOR of results in *xor_out;
+ * the per-fragment values in out[0..n) when out is not NULL (the caller's parity check). */
 typedef uint32_t (*oracle_crc_fn)(const void *, unsigned long, unsigned int);
 
-double oracle_time_fn(void *fn, const uint8_t *buf, size_t n, size_t L, int nthreads, uint32_t *xor_out)
+double oracle_time_fn(void *fn, const uint8_t *buf, size_t n, size_t L, int nthreads, uint32_t *xor_out,
+                      uint32_t *out)
 {
     oracle_crc_fn f = (oracle_crc_fn)fn;
     int nt = resolve_threads(nthreads);
     uint32_t x = 0;
     double t0 = now_s();
 #pragma omp parallel for num_threads(nt) schedule(static) reduction(^ : x)
-    for (long long k = 0; k < (long long)n; ++k) x ^= f(buf + (size_t)k * L, (unsigned long)L, ORACLE_CRC_INIT);
+    for (long long k = 0; k < (long long)n; ++k) {
+        uint32_t c = f(buf + (size_t)k * L, (unsigned long)L, ORACLE_CRC_INIT);
+        if (out) out[k] = c;
+        x ^= c;
+    }
     double t1 = now_s();
     if (xor_out) *xor_out = x;
     return t1 - t0;

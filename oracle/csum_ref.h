@@ -87,7 +87,8 @@ double oracle_time_uniform(uint64_t seed, size_t n, size_t L, int mode, int nthr
 size_t oracle_zipf_lengths(uint64_t min_total, size_t cap, uint32_t *len_out);
 
 /* Time a uicrc-shaped function pointer over n fragments of L bytes of buf (see .c). */
-double oracle_time_fn(void *fn, const uint8_t *buf, size_t n, size_t L, int nthreads, uint32_t *xor_out);
+double oracle_time_fn(void *fn, const uint8_t *buf, size_t n, size_t L, int nthreads, uint32_t *xor_out,
+                      uint32_t *out);
 
 #ifdef __cplusplus
 }

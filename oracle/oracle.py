@@ -109,7 +109,7 @@ class Restatement(_Api):
         L.oracle_time_uniform.argtypes = [ctypes.c_uint64, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.c_int, _vp]
         L.oracle_time_fn.restype = ctypes.c_double
-        L.oracle_time_fn.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, _vp]
+        L.oracle_time_fn.argtypes = [_vp, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, _vp, _vp]
         L.oracle_zipf_lengths.restype = ctypes.c_size_t
         L.oracle_zipf_lengths.argtypes = [ctypes.c_uint64, ctypes.c_size_t, _vp]
         L.oracle_header_checksum.restype = _u
@@ -148,10 +148,15 @@ class Restatement(_Api):
         t = self.lib.oracle_time_uniform(seed, n, L, mode, nthreads, ctypes.byref(x))
         return float(t), x.value
 
-    def time_crc_fn(self, fn_addr: int, buf: np.ndarray, n: int, L: int, nthreads: int) -> tuple[float, int]:
-        """Seconds for `fn` (uicrc-shaped C function address) over n fragments of L bytes."""
+    def time_crc_fn(self, fn_addr: int, buf: np.ndarray, n: int, L: int, nthreads: int,
+                    out: np.ndarray | None = None) -> tuple[float, int]:
+        """Seconds for `fn` (uicrc-shaped C function address) over n fragments of L bytes;
+        the per-fragment values land in `out` (u32[n]) when given."""
         x = ctypes.c_uint(0)
-        t = self.lib.oracle_time_fn(fn_addr, buf.ctypes.data, n, L, nthreads, ctypes.byref(x))
+        if out is not None and (out.dtype != np.uint32 or out.size < n or not out.flags.c_contiguous):
+            raise ValueError("out must be a contiguous u32 array of n values")
+        t = self.lib.oracle_time_fn(fn_addr, buf.ctypes.data, n, L, nthreads, ctypes.byref(x),
+                                    None if out is None else out.ctypes.data)
         return float(t), x.value
 
     def uicrc_addr(self) -> int:

@@ -7,7 +7,14 @@ fragments k = 0 .. n_total-1 of stream `seed` at L bytes, as the oracle (oracle/
 computes them; a weak-scaled N-GPU run of bench.py covers n_total = N x fragments-per-GPU
 (rank r holds k = r mod N) and combines the per-rank digests (lampi_amd/shard.py).
 
-Run in the build container (8 threads, ~6 min):  python tests/golden/make_bench_digests.py
+Shard entries (`nshard`, `shard` keys) cover only k = shard (mod nshard) of the n_total
+fragments, with the global k in the weighted sum: BASELINE config D's per-GPU shards
+(seed 3, 32M x 16 KiB, 8 GPUs), whose CRC XORs BASELINE.md lists from the compiled reference
+(the generator checks its XORs against those before writing).
+
+Existing entries are kept; only missing ones are computed.
+Run in the build container (8 threads; config D shards ~8 min):
+    python tests/golden/make_bench_digests.py
 """
 import json
 import os
@@ -27,22 +34,44 @@ CASES = [
     (2, 1048576, 16384, 1, (1,)),
     (1, 1048576, 1024, 0, (1,)),           # config A shape
 ]
+# config D per-GPU shards: (seed, n_total, L, mode, nshard)
+SHARD_CASES = [(3, 33554432, 16384, 0, 8), (3, 33554432, 16384, 1, 8)]
+# CRC XOR of GPU g's shard (computed there from the compiled reference)
+CONFIG_D_SHARD_XOR = [0x54862C49, 0x046DA633, 0x53ABB493, 0xEB1A2E44, 0xB9EACC67, 0x0BEC3926, 0x937B2402, 0x3B821C43]
+
+
+def key(e):
+    return (e["seed"], e["n_total"], e["frag_bytes"], e["mode"], e.get("nshard", 1), e.get("shard", 0))
 
 
 def main():
     ref = Restatement()
-    out = []
-    for seed, n, L, mode, gpus in CASES:
-        for g in gpus:
-            t = time.time()
-            x, s = ref.uniform_digest(seed, n * g, L, mode, nthreads=os.cpu_count())
-            out.append({"seed": seed, "n_total": n * g, "frag_bytes": L, "mode": "crc" if mode == 0 else "sum",
-                        "xor": x, "wsum": s})
-            print(f"seed {seed} n {n * g} L {L} mode {mode}: {x:08x} {s:08x} ({time.time() - t:.1f} s)", flush=True)
     path = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
+    try:
+        with open(path) as f:
+            out = json.load(f)["entries"]
+    except (OSError, ValueError, KeyError):
+        out = []
+    have = {key(e) for e in out}
+    todo = [(seed, n * g, L, mode, 1, 0) for seed, n, L, mode, gpus in CASES for g in gpus]
+    todo += [(seed, n, L, mode, ns, s) for seed, n, L, mode, ns in SHARD_CASES for s in range(ns)]
+    for seed, n, L, mode, ns, s in todo:
+        e = {"seed": seed, "n_total": n, "frag_bytes": L, "mode": "crc" if mode == 0 else "sum"}
+        if ns > 1:
+            e.update(nshard=ns, shard=s)
+        if key(e) in have:
+            continue
+        t = time.time()
+        x, w = ref.uniform_digest(seed, n, L, mode, nshard=ns, shard=s, nthreads=os.cpu_count())
+        if ns == 8 and seed == 3 and mode == 0 and x != CONFIG_D_SHARD_XOR[s]:
+            raise SystemExit(f"shard {s}: XOR {x:08x} differs from BASELINE.md {CONFIG_D_SHARD_XOR[s]:08x}")
+        e.update(xor=x, wsum=w)
+        out.append(e)
+        print(f"{e}: ({time.time() - t:.1f} s)", flush=True)
     with open(path, "w") as f:
         json.dump({"generator": "tests/golden/make_bench_digests.py (oracle/csum_ref.c uniform_digest)",
-                   "digest": "xor, sum c_k*(2k+1) mod 2^32 over k = 0..n_total-1 (SURVEY.md 8(d))",
+                   "digest": "xor, sum c_k*(2k+1) mod 2^32 over k = 0..n_total-1 (SURVEY.md 8(d)); "
+                             "shard entries: only k = shard (mod nshard), global k in the weights",
                    "entries": out}, f, indent=1)
     print("wrote", path)
 

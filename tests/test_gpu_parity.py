@@ -4,6 +4,8 @@ Sizes the oracle finishes in seconds are compared fragment by fragment; the BASE
 config B (4M x 4 KiB, 16 GiB device-resident) is compared through its committed digests
 (computed by the reference-pinned oracle).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -279,6 +281,40 @@ def test_config_d_shard_digest_sample(cuda, oracle):
     assert np.array_equal(got[idx], want)
     if g == 3:
         assert got[0] == oracle.uniform_batch(3, 3, 1, L, 0)[0]
+
+
+def _bench_digests():
+    import json
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "bench_digests.json")) as f:
+        return json.load(f)["entries"]
+
+
+@pytest.mark.parametrize("g,mode", [(0, "crc"), (7, "crc"), (3, "sum")])
+def test_config_d_full_shard_digest(cuda, g, mode):
+    """BASELINE config D, GPU g's whole shard of the 8-GPU partition on this one GPU: 4,194,304 x
+    16 KiB = 64 GiB (k = g mod 8, seed 3), one lampi_msg_csum launch; XOR and WSUM (global k)
+    vs tests/golden/bench_digests.json, and for CRC the XOR vs BASELINE.md's per-GPU value."""
+    import torch
+
+    from lampi_amd import shard
+
+    dv = _dv()
+    per_gpu_xor = [0x54862C49, 0x046DA633, 0x53ABB493, 0xEB1A2E44, 0xB9EACC67, 0x0BEC3926, 0x937B2402, 0x3B821C43]
+    want = [(e["xor"], e["wsum"]) for e in _bench_digests()
+            if (e["seed"], e["frag_bytes"], e["mode"], e.get("nshard"), e.get("shard")) == (3, 16384, mode, 8, g)]
+    assert len(want) == 1
+    if mode == "crc":
+        assert want[0][0] == per_gpu_xor[g]
+    n, L = 33554432 // 8, 16384
+    torch.cuda.empty_cache()
+    buf = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    dv.fill_stream_frags(buf, n, L, seed=3, k0=g, kstep=8)
+    vals = dv.as_u32(dv.msg_csum(buf, L, mode=dv.CRC32 if mode == "crc" else dv.SUM32))
+    del buf
+    torch.cuda.empty_cache()
+    got = shard.digest(vals, np.arange(n, dtype=np.uint64) * 8 + g)
+    assert got == want[0]
 
 
 def test_host_api_matches_reference_semantics(cuda, oracle):
