@@ -112,6 +112,8 @@ def parse():
     ap.add_argument("--latency", action="store_true", help="small-batch call latency (eager, synchronous, graph)")
     ap.add_argument("--bcopy", action="store_true",
                     help="fused copy + checksum batch (lampi_frag_bcopy_batch) on the config B shape")
+    ap.add_argument("--recv", action="store_true",
+                    help="batched receive step (lampi_copy_to_app_batch) on the config B shape in GM slots")
     ap.add_argument("--desc", action="store_true",
                     help="run the batch through descriptors (lampi_frag_csum_batch, the general kernel) "
                          "instead of the contiguous-message entry point (diagnostic)")
@@ -256,8 +258,17 @@ def cpu_baseline():
     buf = port.stream(seed, 0, n * L)
     out1 = np.empty(n, dtype=np.uint32)
     t1, _ = port.time_crc_fn(fn, buf, n, L, 1, out=out1)
-    mask = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
-    cores = len(mask)
+    mask = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None  # cgroup v2 CPU quota (the box's CPU share), in whole CPUs
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(q) // int(period))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    cores = min([mask] + [c for c in (quota, int(omp) if omp and omp.isdigit() else None) if c])
     outn = np.empty(n, dtype=np.uint32)
     tn, _ = port.time_crc_fn(fn, buf, n, L, cores, out=outn)
     ks = np.arange(n, dtype=np.uint64)
@@ -278,8 +289,8 @@ def cpu_baseline():
         "parity_ok": bool(d1 == want and dn == want),
         "digest": f"{d1[0]:08x}/{d1[1]:08x} (config A: {want[0]:08x}/{want[1]:08x})",
         "all_cores": {"value": round(n * L / GIB / tn, 3), "cores": cores, "seconds": round(tn, 3),
-                      "affinity": f"{cores} of the host's {os.cpu_count()} CPUs are in this process's affinity mask; "
-                                  f"one thread each"},
+                      "threads": f"one per usable CPU: min(affinity mask {mask} of the host's {os.cpu_count()} CPUs, "
+                                 f"cgroup quota {quota}, OMP_NUM_THREADS {omp})"},
         "cpu_model": model,
     }
 
@@ -397,8 +408,6 @@ def run_device(args):
             ts = time.perf_counter()
             run()
             kern_ms.append((time.perf_counter() - ts) * 1e3)
-        t1 = time.perf_counter()
-        vals = box["vals"]
     else:
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         t0 = time.perf_counter()
@@ -407,12 +416,14 @@ def run_device(args):
             run()
             evs[i + 1].record(stream)
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
+    barrier(world)
+    t1 = time.perf_counter()
+    wall = max_over_ranks(t1 - t0, world, args)
+    if args.dry_run:
+        vals = box["vals"]
+    else:
         kern_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
         vals = dv.as_u32(out)
-    barrier(world)
-    t2 = time.perf_counter()
-    wall = max_over_ranks(t2 - t0, world, args)
     kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
 
     # parity: this rank's shard digest (global fragment indices), combined over the ranks, vs
@@ -774,6 +785,83 @@ def run_bcopy(args):
         "cpu_baseline": None}))
 
 
+def run_recv(args):
+    """The receive step (RecvDesc_t::CopyToApp, ref src/path/common/BaseDesc.cc:288-342) over the
+    config B shape in GM receive slots: n fragments of L bytes, each behind a 72-byte gmHeaderData
+    whose dataChecksum (@64) the send side stamped (slot stride 72 + L + 8), delivered into one
+    contiguous application buffer with the checksum verified in the same pass
+    (lampi_copy_to_app_batch).  Roofline bytes = L read + L written per fragment."""
+    import numpy as np
+    import torch
+
+    from lampi_amd import device as dv
+    from lampi_amd import shard
+
+    rank, world, _ = dist_setup(args)
+    if world != 1:
+        raise SystemExit("--recv is a single-GPU measurement")
+    n, L = args.frags, args.frag_bytes
+    mode = dv.CRC32 if args.mode == "crc" else dv.SUM32
+    stride = 72 + L + 8
+    src = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    dv.fill_stream_frags(src, n, L, args.seed)
+    nic = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+    # send side: gather every fragment into its slot behind the header, checksum fused, and stamp
+    # it into the header's dataChecksum (lampi_msg_bcopy + a strided store of the u32 array)
+    sent = dv.msg_bcopy(src, L, nic[72:], dst_stride=stride, mode=mode)
+    nic.view(n, stride)[:, 64:68].copy_(sent.view(torch.uint8).view(n, 4))
+    del src
+    app = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+    offs = np.arange(n, dtype=np.uint64)
+    descs = dv.make_recv_descs(nic, offs * np.uint64(stride) + np.uint64(72), app, offs * np.uint64(L),
+                               np.full(n, L), np.full(n, 1 << 40, dtype=np.int64))
+    run = lambda: dv.copy_to_app_batch(descs, nic, expected_stride=stride, expected_offset=64, n=n, mode=mode)  # noqa
+    for _ in range(args.warmup):
+        res = run()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(args.steps):
+        res = run()
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern = sum(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) / args.steps / 1e3
+    copied, csum, mask, nbad = res
+    vals = dv.as_u32(csum)
+    got = shard.digest(vals, np.arange(n, dtype=np.uint64))
+    want = golden_digest(args.seed, n, L, mode == dv.CRC32)
+    app_ok = bool(torch.equal(app.view(n, L), nic.view(n, stride)[:, 72:72 + L]))
+    ok = (int(nbad.item()) == 0 and bool((copied == L).all().item()) and app_ok
+          and (want is None or got == tuple(want)))
+    moved = 2.0 * n * L
+    achieved = moved / kern / 1e9
+    print(json.dumps({
+        "metric": "device-resident batched receive step (CopyToApp: copy + checksum + CheckData), GiB/s of "
+                  "payload; % of HBM roofline",
+        "value": round(n * L / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic: splitmix64 stream seed {args.seed} (SURVEY.md 8(d)) in GM receive slots",
+        "config": {"workload": f"{n} x {L} B fragments, 72-byte gmHeaderData + payload slots (stride {stride}), "
+                               f"{'CRC' if mode == dv.CRC32 else 'sum'} verified against dataChecksum, delivered "
+                               "into one application buffer (lampi_copy_to_app_batch)", "fragments": n,
+                   "frag_bytes": L},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "crc_rows_kernel<RecvSource, 8>" if mode == dv.CRC32 else
+                               "crc_stream_kernel<RecvSource, kPB = 16, kCopy> (+ sum_rows_kernel fallback)",
+                     "kernel_avg_ms": round(kern * 1e3, 4), "algorithmic_bytes_per_launch": int(moved),
+                     "note": "algorithmic bytes = payload read + payload written; the 4-byte expected value and "
+                             "32-byte descriptor per fragment excluded"},
+        "parity": {"check": "nbad == 0, every fragment fully copied, app == slot payloads, checksum digest vs "
+                            "committed config digest", "xor": f"{got[0]:08x}", "wsum": f"{got[1]:08x}",
+                   "ok": bool(ok)},
+        "cpu_baseline": None}), flush=True)
+
+
 def run_latency(args):
     """Small batches: per-call time of lampi_frag_csum_batch over n 4 KiB descriptor
     fragments, three ways -- stream-ordered back-to-back calls (device time per call, HIP events),
@@ -870,6 +958,9 @@ def main():
         return
     if args.bcopy:
         run_bcopy(args)
+        return
+    if args.recv:
+        run_recv(args)
         return
     if args.e2e:
         run_e2e(args)

@@ -200,6 +200,37 @@ int lampi_check_data_batch(const uint32_t *d_calc, const void *d_expected, size_
                            const void *d_lengths, size_t lengths_stride, size_t n, uint32_t *d_mask,
                            uint32_t *d_nbad, void *stream);
 
+/* One received fragment to deliver (32 bytes, little-endian): offset 0 frag, 8 app,
+ * 16 app_len, 24 length, 28 reserved. */
+typedef struct lampi_recv_desc {
+    uint64_t frag;      /* device address of the received payload (BaseRecvFragDesc_t::addr_m) */
+    uint64_t app;       /* device address it is delivered to: RecvDesc_t::addr_m + dataOffset() */
+    int64_t  app_len;   /* room left in the posted buffer at that offset: posted_m.length_m - Offset
+                           (ref BaseDesc.cc:307); may be <= 0 */
+    uint32_t length;    /* bytes received, length_m; all of them are checksummed */
+    uint32_t reserved;  /* 0 */
+} lampi_recv_desc;
+
+/* RecvDesc_t::CopyToApp for a batch of contiguous fragments, fused in one pass over the payload
+ * (ref src/path/common/BaseDesc.cc:288-342, locked twin :380-434; GM hooks CopyFunction
+ * src/path/gm/recvFrag.h:165-182 and CheckData :213-257; IB src/path/ib/recvFrag.cc:182-245):
+ *   lengthToCopy = app_len <= 0 ? 0 : min(length, app_len);
+ *   lengthToCopy > 0:  copy lengthToCopy bytes frag -> app, checksum all `length` bytes
+ *                      (bcopy_uicrc / bcopy_uicsum with copylen < csumlen, the bytes past the
+ *                      posted buffer go to the bit bucket) and compare with the expected value;
+ *   lengthToCopy == 0: nothing copied or checksummed, DataOK (CopyFunction returns the CRC
+ *                      initial register or 0, CheckData passes a zero length).
+ * d_copied[i] = lengthToCopy, or -1 when the checksum differs (CopyToApp's return value);
+ * d_csum[i] = the calculated checksum (what the reference logs as "calculated=");
+ * the expected checksum of fragment i is the 32-bit value at d_expected + i*expected_stride --
+ * e.g. dataChecksum (@64) of an array of 72-byte gmHeaderData records (expected_stride 72).
+ * d_mask: bit (i % 32) of word i / 32 set iff fragment i is corrupt (zeroed by the call);
+ * *d_nbad: number of corrupt fragments.  One wavefront per fragment (CRC) / 16-byte-piece
+ * streams (SUM); every payload byte is read from HBM once. */
+int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void *d_expected,
+                            size_t expected_stride, int64_t *d_copied, uint32_t *d_csum, uint32_t *d_mask,
+                            uint32_t *d_nbad, int mode, void *stream);
+
 /* ------------------------------------------------------------------------------------
  * Utilities (bench/test support, device-side).
  * ---------------------------------------------------------------------------------- */

@@ -38,6 +38,16 @@ class CopyDesc(ctypes.Structure):
 
 assert ctypes.sizeof(CopyDesc) == 32
 
+
+class RecvDesc(ctypes.Structure):
+    """struct lampi_recv_desc (32 bytes): frag u64, app u64, app_len i64, length u32, reserved u32."""
+
+    _fields_ = [("frag", ctypes.c_uint64), ("app", ctypes.c_uint64), ("app_len", ctypes.c_int64),
+                ("length", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(RecvDesc) == 32
+
 _lock = threading.Lock()
 _lib = None
 
@@ -70,6 +80,8 @@ PROTOTYPES = {
     "lampi_frag_csum_batch_strided": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.c_int, c_void_p]),
     "lampi_check_data_batch": (ctypes.c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_void_p,
                                               c_void_p, c_void_p]),
+    "lampi_copy_to_app_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
+                                               c_void_p, ctypes.c_int, c_void_p]),
     "lampi_msg_csum": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, c_void_p, ctypes.c_int,
                                       c_void_p]),
     "lampi_fill_stream": (ctypes.c_int, [c_void_p, c_size_t, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),

@@ -162,6 +162,53 @@ struct PieceSource {
     }
 };
 
+// RecvDesc_t::CopyToApp (ref src/path/common/BaseDesc.cc:288-342): copy lengthToCopy =
+// min(length_m, AppBufferLen) bytes (none when AppBufferLen <= 0), checksum all length_m bytes
+// (CopyFunction, gm/recvFrag.h:165-182: bcopy with copylen < csumlen), and -- where the kernel
+// stores the checksum (emit) -- apply CheckData (gm/recvFrag.h:213-257) against the expected
+// value.  A fragment with nothing to copy is not checksummed: CopyFunction returns the CRC
+// initial register (or 0) for length 0 and CheckData passes it.
+struct RecvSource {
+    static constexpr bool kCopy = true;
+    static constexpr bool kPhase = false;
+    const lampi_recv_desc *d;
+    uint32_t empty;            // CopyFunction of 0 bytes: 0xFFFFFFFF (CRC) or 0 (SUM)
+    const uint8_t *expected;   // expected checksum of fragment f at expected + f * exp_stride
+    size_t exp_stride;
+    int64_t *copied;           // CopyToApp's return: lengthToCopy, or -1 when corrupt
+    uint32_t *mask;            // bit f set when corrupt (zeroed by the launcher)
+    uint32_t *nbad;
+    __device__ static uint32_t to_copy(const lampi_recv_desc &x) {
+        return x.app_len <= 0 ? 0u : (x.app_len < (int64_t)x.length ? (uint32_t)x.app_len : x.length);
+    }
+    __device__ FragInfo get(size_t f) const {
+        const lampi_recv_desc x = d[f];
+        const uint32_t c = to_copy(x);
+        return {(gbyte *)(uintptr_t)x.frag, c ? x.length : 0u, empty, (uint8_t *)(uintptr_t)x.app, c};
+    }
+    __device__ void verdict(size_t f, uint32_t v) const {
+        const uint32_t c = to_copy(d[f]);
+        const bool bad = c != 0u && v != *(const guint *)(expected + f * exp_stride);
+        copied[f] = bad ? -1ll : (int64_t)c;
+        if (bad) {  // rare: one atomic per corrupt fragment
+            atomicOr(mask + (f >> 5), 1u << (f & 31u));
+            atomicAdd(nbad, 1u);
+        }
+    }
+};
+
+template <class S>
+struct IsRecv : std::false_type {};
+template <>
+struct IsRecv<RecvSource> : std::true_type {};
+
+// every kernel stores a fragment's checksum through this: receive sources also decide it
+template <class Src, class Acc>
+__device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v) {
+    out[f] = v;
+    if constexpr (IsRecv<Src>::value) src.verdict(f, v);
+}
+
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
     uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
@@ -677,7 +724,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                 fi.copylen = uniform(fi.copylen);
             }
             if (fi.len) return x;
-            if (lane == 0) out[x] = fi.partial;  // uicrc(p, 0, s) == s
+            if (lane == 0) emit(src, out, x, fi.partial);  // uicrc(p, 0, s) == s
         }
         return n;
     };
@@ -763,7 +810,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
             if (lane == 0) {
                 uint32_t res = __builtin_bswap32(C);
                 if (cur.len < 4) res ^= cur.partial << (8 * cur.len);
-                out[f] = res;
+                emit(src, out, f, res);
             }
         }
         if (!more) break;
@@ -1583,7 +1630,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
         }
     }
     __syncthreads();
-    if (t < nwg) out[base + t] = sres[t];
+    if (t < nwg) emit(src, out, base + t, sres[t]);
 }
 
 // ---- CRC fast path: regular batches -------------------------------------------------------
@@ -2009,7 +2056,7 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
 #pragma unroll
             for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
         }
-        if (lane == 0) out[f] = acc;
+        if (lane == 0) emit(src, out, f, acc);
     }
 }
 
@@ -2578,25 +2625,56 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
     return hipGetLastError();
 }
 
+// Fused-copy SUM launches pair crc_stream_kernel (workgroups whose destinations are all 4-byte
+// aligned) with sum_rows_kernel<..., kSkipFast> (the others) over the SAME partition: fpg fragments
+// per crc_stream_kernel workgroup = kWaves * fpw fragments per sum_rows_kernel workgroup.  One
+// helper picks fpg for every such pair, so the two kernels can never split a batch differently.
+static uint32_t bcopy_frags_per_wg(size_t n) {
+    uint32_t fpg = 96;
+    while (fpg > 4 && n / fpg < 2048) fpg = fpg > 12 ? fpg / 2 : 4;
+    return fpg;
+}
+static_assert(96 % kWaves == 0 && 48 % kWaves == 0 && 24 % kWaves == 0 && 12 % kWaves == 0 && 4 % kWaves == 0,
+              "every fpg bcopy_frags_per_wg can return is a multiple of kWaves");
+
 // SUM: crc_stream_kernel's fused copy (16-byte pieces, coalesced loads and stores) for workgroups
-// whose fragments all have 4-byte-aligned destinations, then sum_rows_kernel for the others (same
-// partition: 4*fpw = fpg fragments per workgroup).  img must be an allocation of the table image
-// followed by kImgTrashBytes of device memory (device_tables()).
+// whose fragments all have 4-byte-aligned destinations, then sum_rows_kernel for the others.
+// img must be an allocation of the table image followed by kImgTrashBytes of device memory
+// (device_tables()).
+template <class Src>
+static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, const uint32_t *img, hipStream_t s) {
+    const uint32_t fpg = bcopy_frags_per_wg(n);
+    uint8_t *trash = (uint8_t *)(uintptr_t)(img + kImgWords);
+    hipLaunchKernelGGL((crc_stream_kernel<Src, kCopyD, 0, 1, true, kStreamWv, kStreamCap, 16, true>), frags_grid(n, fpg),
+                       dim3(64 * kStreamWv), 0, s, src, n, fpg, img, out, trash);
+    hipLaunchKernelGGL((sum_rows_kernel<Src, uint32_t, true>), frags_grid(n, fpg), dim3(kBlock), 0, s, src, n,
+                       fpg / kWaves, out);
+}
+
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                              hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC) / zero chunk and trash slots (SUM)
-    if (mode == LAMPI_CSUM_CRC32) {
+    if (mode == LAMPI_CSUM_CRC32)
         launch_crc_rows_copy(CopySource{d}, n, 1, img, out, s);
-        return hipGetLastError();
-    }
-    uint32_t fpg = 96;  // a multiple of 4 (kWaves): sum_rows_kernel's workgroups cover the same fragments
-    while (fpg > 4 && n / fpg < 2048) fpg = fpg > 12 ? fpg / 2 : 4;
-    uint8_t *trash = (uint8_t *)(uintptr_t)(img + kImgWords);
-    hipLaunchKernelGGL((crc_stream_kernel<CopySource, kCopyD, 0, 1, true, kStreamWv, kStreamCap, 16, true>),
-                       frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, CopySource{d}, n, fpg, img, out, trash);
-    hipLaunchKernelGGL((sum_rows_kernel<CopySource, uint32_t, true>), frags_grid(n, fpg), dim3(kBlock), 0, s,
-                       CopySource{d}, n, fpg / kWaves, out);
+    else
+        launch_sum_copy(CopySource{d}, n, out, img, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t *expected, size_t exp_stride,
+                              int64_t *copied, uint32_t *csum, uint32_t *mask, uint32_t *nbad, int mode,
+                              const uint32_t *img, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(nbad, 0, sizeof(uint32_t), s);
+    if (e == hipSuccess && n) e = hipMemsetAsync(mask, 0, (n + 31) / 32 * sizeof(uint32_t), s);
+    if (e != hipSuccess || n == 0) return e;
+    if (!img) return hipErrorInvalidValue;
+    const bool crc = mode == LAMPI_CSUM_CRC32;
+    const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
+    if (crc)
+        launch_crc_rows_copy(src, n, 1, img, csum, s);
+    else
+        launch_sum_copy(src, n, csum, img, s);
     return hipGetLastError();
 }
 
@@ -2672,15 +2750,8 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
     }
     // ragged or unaligned: the fused-copy piece streams as for descriptor batches (4-byte-aligned
     // destinations), sum_rows_kernel for the workgroups with byte-misaligned ones
-    const MsgCopySource src{base, msg_len, frag_len, 0u, dst, dst_stride};
     if (!img) return hipErrorInvalidValue;
-    uint32_t fpg = 96;  // a multiple of 4 (kWaves): sum_rows_kernel's workgroups cover the same fragments
-    while (fpg > 4 && n / fpg < 2048) fpg = fpg > 12 ? fpg / 2 : 4;
-    uint8_t *trash = (uint8_t *)(uintptr_t)(img + kImgWords);
-    hipLaunchKernelGGL((crc_stream_kernel<MsgCopySource, kCopyD, 0, 1, true, kStreamWv, kStreamCap, 16, true>),
-                       frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, src, n, fpg, img, out, trash);
-    hipLaunchKernelGGL((sum_rows_kernel<MsgCopySource, uint32_t, true>), frags_grid(n, fpg), dim3(kBlock), 0, s, src,
-                       n, fpg / kWaves, out);
+    launch_sum_copy(MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, out, img, s);
     return hipGetLastError();
 }
 

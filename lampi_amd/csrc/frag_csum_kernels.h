@@ -27,6 +27,10 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 // Fragments of a message, each copied to dst + k*dst_stride with its checksum fused.
 hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, uint8_t *dst,
                             size_t dst_stride, size_t n, uint32_t *out, int mode, const uint32_t *img, hipStream_t s);
+// RecvDesc_t::CopyToApp per descriptor (copy min(length, app_len), checksum length, verify).
+hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t *expected, size_t exp_stride,
+                              int64_t *copied, uint32_t *csum, uint32_t *mask, uint32_t *nbad, int mode,
+                              const uint32_t *img, hipStream_t s);
 // headerChecksum per header / receiver header check / CheckData (mask bit set = corrupt).
 hipError_t launch_header_csum(const uint8_t *hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
                               int mode, const uint32_t *img, uint32_t *out, hipStream_t s);

@@ -377,6 +377,23 @@ int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d
     return to_int(launch_bcopy_desc(d_descs, n, d_out, mode, img, (hipStream_t)stream));
 }
 
+int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void *d_expected, size_t expected_stride,
+                            int64_t *d_copied, uint32_t *d_csum, uint32_t *d_mask, uint32_t *d_nbad, int mode,
+                            void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (!d_nbad || (n && (!d_descs || !d_expected || !d_copied || !d_csum || !d_mask)) ||
+        ((uintptr_t)d_expected & 3u) || (expected_stride & 3u) || n > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;  // CRC: the tables; SUM: the zero chunk and trash slots of the streams
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_copy_to_app(d_descs, n, (const uint8_t *)d_expected, expected_stride, d_copied, d_csum, d_mask,
+                                     d_nbad, mode, img, (hipStream_t)stream));
+}
+
 int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t partial, uint32_t *d_out, int mode,
                    void *stream) {
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);

@@ -13,7 +13,7 @@ from ._lib import CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
 
 __all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
            "make_descs", "make_copy_descs", "as_u32", "chain_csum_batch", "header_csum_batch", "header_check_batch", "check_data_batch",
-           "mask_bits"]
+           "mask_bits", "make_recv_descs", "copy_to_app_batch"]
 
 
 def _stream_handle(stream: torch.cuda.Stream | None) -> int:
@@ -253,6 +253,53 @@ def check_data_batch(calc: torch.Tensor, expected: torch.Tensor, expected_stride
                                        lp or None, lengths_stride, count, mask.data_ptr(), nbad.data_ptr(),
                                        _stream_handle(stream)), "lampi_check_data_batch")
     return mask, nbad
+
+
+def make_recv_descs(frag: torch.Tensor, frag_offsets, app: torch.Tensor, app_offsets, lengths,
+                    app_lens) -> torch.Tensor:
+    """Build a device array of ``lampi_recv_desc`` (n x 32 bytes, int64 [n, 4] storage): fragment i
+    = ``lengths[i]`` received bytes at frag + frag_offsets[i], delivered to app + app_offsets[i]
+    with ``app_lens[i]`` bytes of room left in the posted buffer (posted length - offset, may be
+    <= 0; ref src/path/common/BaseDesc.cc:300-307)."""
+    _require_cuda(frag, "frag")
+    _require_cuda(app, "app")
+    fo = np.asarray(frag_offsets, dtype=np.uint64)
+    ao = np.asarray(app_offsets, dtype=np.uint64)
+    ln = np.asarray(lengths, dtype=np.uint64)
+    al = np.asarray(app_lens, dtype=np.int64)
+    n = fo.size
+    if not (ao.size == ln.size == al.size == n):
+        raise ValueError("descriptor fields differ in size")
+    if n:
+        if int(ln.max()) > 0xFFFFFFFF:
+            raise ValueError("fragment length exceeds 32 bits")
+        if int((fo + ln).max()) > frag.numel() * frag.element_size():
+            raise ValueError("a fragment extends past the end of frag")
+        copy = np.minimum(ln.astype(np.int64), np.maximum(al, 0))
+        if int((ao.astype(np.int64) + copy).max()) > app.numel() * app.element_size():
+            raise ValueError("a delivery extends past the end of app")
+    host = np.empty((n, 4), dtype=np.uint64)
+    host[:, 0] = np.uint64(frag.data_ptr()) + fo
+    host[:, 1] = np.uint64(app.data_ptr()) + ao
+    host[:, 2] = al.view(np.uint64)
+    host[:, 3] = ln
+    return torch.from_numpy(host.view(np.int64)).to(frag.device)
+
+
+def copy_to_app_batch(descs: torch.Tensor, expected: torch.Tensor, expected_stride: int = 4, expected_offset: int = 0,
+                      n: int | None = None, mode: int = CRC32, stream: torch.cuda.Stream | None = None):
+    """RecvDesc_t::CopyToApp over a batch (src/path/common/BaseDesc.cc:288-342): returns
+    (copied int64[n] -- bytes copied or -1 when corrupt --, csum int32[n], mask, nbad)."""
+    _require_cuda(descs, "descs")
+    count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
+    _records(expected.view(torch.uint8)[expected_offset:] if count else expected, count, expected_stride, "expected")
+    copied = torch.empty(max(count, 1), dtype=torch.int64, device=descs.device)
+    csum = torch.empty(max(count, 1), dtype=torch.int32, device=descs.device)
+    mask, nbad = _mask_out(count, descs.device)
+    check(lib().lampi_copy_to_app_batch(descs.data_ptr(), count, expected.data_ptr() + expected_offset, expected_stride,
+                                        copied.data_ptr(), csum.data_ptr(), mask.data_ptr(), nbad.data_ptr(), mode,
+                                        _stream_handle(stream)), "lampi_copy_to_app_batch")
+    return copied[:count], csum[:count], mask, nbad
 
 
 def mask_bits(mask: torch.Tensor, n: int) -> np.ndarray:

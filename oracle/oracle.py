@@ -78,6 +78,25 @@ class _Api:
         return int(r), pi.value, pl.value
 
 
+def copy_to_app(api: "_Api", frag: np.ndarray, length: int, app_len: int, expected: int, usecrc: bool):
+    """RecvDesc_t::CopyToApp for one contiguous fragment (ref src/path/common/BaseDesc.cc:288-342)
+    with the GM hooks CopyFunction (src/path/gm/recvFrag.h:165-182) and CheckData (:213-257),
+    checksumming on: lengthToCopy = min(length_m, AppBufferLen); AppBufferLen <= 0 is DataOK with
+    nothing copied; otherwise bcopy_uicrc / bcopy_uicsum(frag, app, lengthToCopy, length_m)
+    (CRC_INITIAL_REGISTER or 0 for a zero lengthToCopy) and CheckData(csum, lengthToCopy).
+    Returns (CopyToApp's return value -- bytes or -1 --, the checksum CopyFunction returned (the
+    CopyFunction-of-nothing value when it is not called), the bytes delivered)."""
+    empty = CRC_INIT if usecrc else 0
+    if app_len <= 0:
+        return 0, empty, np.zeros(0, np.uint8)
+    n = min(length, app_len)
+    dst = np.zeros(n, np.uint8)
+    if n == 0:
+        return 0, empty, dst
+    c = api.bcopy_uicrc(frag, dst, n, length) if usecrc else api.bcopy_uicsum(frag, dst, n, length)[0]
+    return (n if c == expected else -1), c, dst
+
+
 class Restatement(_Api):
     def __init__(self, path: str = RESTATEMENT_SO):
         if not os.path.exists(path):
