@@ -348,6 +348,12 @@ def shard_plan(args, world: int, rank: int):
     return n, L, seed, k0, kstep, n_global
 
 
+def _traffic(key: str, field: str = "hbm_bytes_per_launch"):
+    """A field of a committed PMC traffic entry (profiles/traffic.json), or None."""
+    e = read_traffic(key)
+    return None if e is None else e.get(field)
+
+
 def run_device(args):
     """One rank of the device-resident bench: fill this rank's shard in HBM, time K launches."""
     import numpy as np
@@ -759,7 +765,10 @@ def run_bcopy(args):
                                f"{'CRC' if mode == dv.CRC32 else 'sum'} fused (lampi_msg_bcopy)",
                    "fragments": n, "frag_bytes": L},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_bcopy_{n}x{L}"),
+                     "traffic_source": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_bcopy_{n}x{L}", "source"),
+                     "kernel": kname,
                      "kernel_avg_ms": round(kern * 1e3, 4), "algorithmic_bytes_per_launch": int(moved),
                      "note": "algorithmic bytes = payload read + payload written"},
         "descriptor_batch": {"kernel_avg_ms": round(kern_desc * 1e3, 4),
@@ -850,7 +859,9 @@ def run_recv(args):
                                "into one application buffer (lampi_copy_to_app_batch)", "fragments": n,
                    "frag_bytes": L},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}"),
+                     "traffic_source": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}", "source"),
                      "kernel": "crc_rows_kernel<RecvSource, 8>" if mode == dv.CRC32 else
                                "crc_stream_kernel<RecvSource, kPB = 16, kCopy> (+ sum_rows_kernel fallback)",
                      "kernel_avg_ms": round(kern * 1e3, 4), "algorithmic_bytes_per_launch": int(moved),

@@ -6,8 +6,9 @@
  *     #include "util/MemFunctions.h"   ->   #include "lampi/MemFunctions.h"
  *     link:  -L<repo>/lampi_amd -llampi_csum
  *
- * The 32-bit functions (the only ones with callers in src/) are provided.
- * The unused 64-bit csum/bcopy_csum overloads (MemFunctions.h:43-50) are not.
+ * All twelve overloads are provided: the 32-bit uicrc/bcopy_uicrc/uicsum/bcopy_uicsum (the
+ * only ones with callers in src/) and the 64-bit csum/bcopy_csum
+ * (MemFunctions.h:43-50, no path caller).
  */
 #ifndef LAMPI_DROPIN_MEMFUNCTIONS_H
 #define LAMPI_DROPIN_MEMFUNCTIONS_H

@@ -246,6 +246,11 @@ int lampi_fill_stream(void *d_dst, size_t nbytes, uint64_t seed, uint64_t byte_o
 int lampi_fill_stream_frags(void *d_dst, size_t n, size_t frag_len, uint64_t seed, uint64_t k0,
                             uint64_t kstep, void *stream);
 
+/* Release the calling thread's staging resources of the host entry points (stream, device
+ * buffers, pinned bounce buffer).  They are also released automatically when the thread exits
+ * or switches to another device; the next host call on the thread allocates them again. */
+void lampi_host_release(void);
+
 /* Version string of the engine and the gfx target it was built for. */
 const char *lampi_csum_version(void);
 

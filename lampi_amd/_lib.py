@@ -87,6 +87,7 @@ PROTOTYPES = {
     "lampi_fill_stream": (ctypes.c_int, [c_void_p, c_size_t, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
     "lampi_fill_stream_frags": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                                ctypes.c_uint64, c_void_p]),
+    "lampi_host_release": (None, []),
     "lampi_csum_version": (ctypes.c_char_p, []),
 }
 

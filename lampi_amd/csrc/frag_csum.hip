@@ -68,6 +68,11 @@ typedef __attribute__((address_space(1))) const uint32_t guint;
 typedef __attribute__((address_space(1))) uint8_t gwbyte;
 typedef __attribute__((address_space(1))) uint32_t gwuint;
 typedef __attribute__((address_space(1))) u32x4 gwu32x4;
+// 16-byte stores to destinations that are only dword-aligned (GM ring slots after a 72-byte
+// header): the type says 4-byte alignment, so the compiler assumes nothing more than the host
+// gates guarantee; global_store_dwordx4 at a dword-aligned address runs at the aligned rate
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+typedef __attribute__((address_space(1))) u32x4_a4 gwu32x4_a4;
 
 struct FragInfo {
     gbyte *addr;
@@ -247,7 +252,7 @@ __device__ __forceinline__ void issue_row(gbyte *p, Row &r) {
 
 template <int N>
 __device__ __forceinline__ void wait_row(Row &r) {
-    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(r.q[0]), "+v"(r.q[1]), "+v"(r.q[2]), "+v"(r.q[3]) : "n"(N) : "memory");
+    asm volatile("s_waitcnt vmcnt(%4) ; lampi-wait %0 %1 %2 %3" : "+v"(r.q[0]), "+v"(r.q[1]), "+v"(r.q[2]), "+v"(r.q[3]) : "n"(N) : "memory");
 }
 
 __device__ __forceinline__ u32x4 issue_b128(gbyte *p) {
@@ -385,7 +390,7 @@ __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__re
     char *b = reinterpret_cast<char *>(lds);
     if (kParts & 1) build_slices(b);
     if (kParts & 4) build_horner<kCoal>(b);
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(cb.a), "+v"(cb.b) : "n"(kPre) : "memory");
+    asm volatile("s_waitcnt vmcnt(%2) ; lampi-wait %0 %1" : "+v"(cb.a), "+v"(cb.b) : "n"(kPre) : "memory");
     if (kParts & 2) build_combine(b, cb);
     if (kSync) lds_barrier();
 }
@@ -536,7 +541,7 @@ __device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *ds
                 *(gwuint *)(c + 8) = v[i].z;
                 *(gwuint *)(c + 12) = v[i].w;
             } else {
-                *(gwu32x4 *)c = v[i];
+                *(gwu32x4_a4 *)c = v[i];  // dst is 4-byte aligned (dword-aligned dwordx4 store)
             }
         }
     }
@@ -917,7 +922,7 @@ __device__ __forceinline__ void issue_rowN(const AddrN<2> &a, RowN<2> &r) {
 // threaded through so no use is scheduled above the wait
 template <int N>
 __device__ __forceinline__ void wait_rows2(RowN<4> &a, RowN<4> &b) {
-    asm volatile("s_waitcnt vmcnt(%8)"
+    asm volatile("s_waitcnt vmcnt(%8) ; lampi-wait %0 %1 %2 %3 %4 %5 %6 %7"
                  : "+v"(a.q[0]), "+v"(a.q[1]), "+v"(a.q[2]), "+v"(a.q[3]), "+v"(b.q[0]), "+v"(b.q[1]),
                    "+v"(b.q[2]), "+v"(b.q[3])
                  : "n"(N)
@@ -925,7 +930,7 @@ __device__ __forceinline__ void wait_rows2(RowN<4> &a, RowN<4> &b) {
 }
 template <int N>
 __device__ __forceinline__ void wait_rows2(RowN<5> &a, RowN<5> &b) {
-    asm volatile("s_waitcnt vmcnt(%10)"
+    asm volatile("s_waitcnt vmcnt(%10) ; lampi-wait %0 %1 %2 %3 %4 %5 %6 %7 %8 %9"
                  : "+v"(a.q[0]), "+v"(a.q[1]), "+v"(a.q[2]), "+v"(a.q[3]), "+v"(a.q[4]), "+v"(b.q[0]),
                    "+v"(b.q[1]), "+v"(b.q[2]), "+v"(b.q[3]), "+v"(b.q[4])
                  : "n"(N)
@@ -936,7 +941,7 @@ __device__ __forceinline__ void wait_rows2(RowN<5> &a, RowN<5> &b) {
 // waits on two branches make the compiler merge the ring registers through a phi, and it then
 // copies registers whose loads are still in flight before the wait (garbage; seen in the ISA).
 // sel (SGPR): 0 -> vmcnt(A), 1 -> vmcnt(B), else vmcnt(C).
-#define LAMPI_WAIT_SEL_ASM                 \
+#define LAMPI_WAIT_SEL_ASM(OPS)            \
     "s_cmp_eq_u32 %[sel], 0\n\t"          \
     "s_cbranch_scc1 1f\n\t"               \
     "s_cmp_eq_u32 %[sel], 1\n\t"          \
@@ -948,18 +953,19 @@ __device__ __forceinline__ void wait_rows2(RowN<5> &a, RowN<5> &b) {
     "s_branch 3f\n"                        \
     "2:\n\t"                              \
     "s_waitcnt vmcnt(%[b])\n"              \
-    "3:"
+    "3:\n\t"                              \
+    "; lampi-wait " OPS
 
 template <int A, int B, int C>
 __device__ __forceinline__ void wait_sel(uint32_t sel, u32x4 &r) {
-    asm volatile(LAMPI_WAIT_SEL_ASM
+    asm volatile(LAMPI_WAIT_SEL_ASM("%0")
                  : "+v"(r)
                  : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
                  : "scc", "memory");
 }
 template <int A, int B, int C>
 __device__ __forceinline__ void wait_sel(uint32_t sel, u32x4 &r0, u32x4 &r1) {
-    asm volatile(LAMPI_WAIT_SEL_ASM
+    asm volatile(LAMPI_WAIT_SEL_ASM("%0 %1")
                  : "+v"(r0), "+v"(r1)
                  : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
                  : "scc", "memory");
@@ -1421,14 +1427,14 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         } else if constexpr (kK == 2) {
             wait_rows2<(kD - 1) * 2 * NL>(r[0], r[1]);
         } else if constexpr (NL == 4) {
-            asm volatile("s_waitcnt vmcnt(%4)"
+            asm volatile("s_waitcnt vmcnt(%4) ; lampi-wait %0 %1 %2 %3"
                          : "+v"(r[0].q[0]), "+v"(r[0].q[1]), "+v"(r[0].q[2]), "+v"(r[0].q[3])
                          : "n"((kD - 1) * NL)
                          : "memory");
         } else if constexpr (NL == 1) {
-            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(r[0].q[0]) : "n"((kD - 1) * NL) : "memory");
+            asm volatile("s_waitcnt vmcnt(%1) ; lampi-wait %0" : "+v"(r[0].q[0]) : "n"((kD - 1) * NL) : "memory");
         } else {
-            asm volatile("s_waitcnt vmcnt(%5)"
+            asm volatile("s_waitcnt vmcnt(%5) ; lampi-wait %0 %1 %2 %3 %4"
                          : "+v"(r[0].q[0]), "+v"(r[0].q[1]), "+v"(r[0].q[2]), "+v"(r[0].q[3]), "+v"(r[0].q[4])
                          : "n"((kD - 1) * NL)
                          : "memory");
@@ -1470,8 +1476,8 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 // 2 = everything but the table lookups of the pieces.  kK: chains per wave, kWv: waves per
 // workgroup (kWv * kK chains); kWaveCap > 0 asks the compiler for that many waves per SIMD.
 // kPB / kCopy: see stream_body (the fused copy: SUM, 16-byte pieces; a workgroup with a fragment
-// whose dst is not 16-byte aligned does nothing -- sum_rows_kernel<CopySource, ..., true> takes
-// those).  trash: 1 KiB of device memory the copy's masked lanes store to.
+// whose dst is not 4-byte (dword) aligned does nothing -- sum_rows_kernel<..., kSkipFast> takes
+// those; dword-aligned dwordx4 stores run at the aligned rate).  trash: 1 KiB of device memory the copy's masked lanes store to.
 template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0,
           int kPB = 64, bool kCopy = false>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kWaveCap > 0 ? kWaveCap : 1)))
@@ -1515,7 +1521,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
             CombineBasis cb = issue_combine_basis<false>(img);
             char *b = reinterpret_cast<char *>(lds);
             build_slices(b);
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(cb.a), "+v"(cb.b) : : "memory");
+            asm volatile("s_waitcnt vmcnt(0) ; lampi-wait %0 %1" : "+v"(cb.a), "+v"(cb.b) : : "memory");
             build_combine(b, cb);
         }
         __syncthreads();
@@ -1652,19 +1658,19 @@ struct RowsK {
 template <int N, int K>
 __device__ __forceinline__ void wait_rows(RowsK<K> &b) {
     if constexpr (K == 1) {
-        asm volatile("s_waitcnt vmcnt(%4)"
+        asm volatile("s_waitcnt vmcnt(%4) ; lampi-wait %0 %1 %2 %3"
                      : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3])
                      : "n"(N)
                      : "memory");
     } else if constexpr (K == 2) {
-        asm volatile("s_waitcnt vmcnt(%8)"
+        asm volatile("s_waitcnt vmcnt(%8) ; lampi-wait %0 %1 %2 %3 %4 %5 %6 %7"
                      : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
                        "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3])
                      : "n"(N)
                      : "memory");
     } else {
         static_assert(K == 4, "kChains is 1, 2 or 4");
-        asm volatile("s_waitcnt vmcnt(%16)"
+        asm volatile("s_waitcnt vmcnt(%16) ; lampi-wait %0 %1 %2 %3 %4 %5 %6 %7 %8 %9 %10 %11 %12 %13 %14 %15"
                      : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
                        "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3]),
                        "+v"(b.x[2].q[0]), "+v"(b.x[2].q[1]), "+v"(b.x[2].q[2]), "+v"(b.x[2].q[3]),
@@ -1679,19 +1685,19 @@ __device__ __forceinline__ void wait_rows(RowsK<K> &b) {
 template <int A, int B, int C, int K>
 __device__ __forceinline__ void wait_rows_sel(uint32_t sel, RowsK<K> &b) {
     if constexpr (K == 1) {
-        asm volatile(LAMPI_WAIT_SEL_ASM
+        asm volatile(LAMPI_WAIT_SEL_ASM("%0 %1 %2 %3")
                      : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3])
                      : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
                      : "scc", "memory");
     } else if constexpr (K == 2) {
-        asm volatile(LAMPI_WAIT_SEL_ASM
+        asm volatile(LAMPI_WAIT_SEL_ASM("%0 %1 %2 %3 %4 %5 %6 %7")
                      : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
                        "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3])
                      : [sel] "s"(sel), [a] "n"(A), [b] "n"(B), [c] "n"(C)
                      : "scc", "memory");
     } else {
         static_assert(K == 4, "kChains is 1, 2 or 4");
-        asm volatile(LAMPI_WAIT_SEL_ASM
+        asm volatile(LAMPI_WAIT_SEL_ASM("%0 %1 %2 %3 %4 %5 %6 %7 %8 %9 %10 %11 %12 %13 %14 %15")
                      : "+v"(b.x[0].q[0]), "+v"(b.x[0].q[1]), "+v"(b.x[0].q[2]), "+v"(b.x[0].q[3]),
                        "+v"(b.x[1].q[0]), "+v"(b.x[1].q[1]), "+v"(b.x[1].q[2]), "+v"(b.x[1].q[3]),
                        "+v"(b.x[2].q[0]), "+v"(b.x[2].q[1]), "+v"(b.x[2].q[2]), "+v"(b.x[2].q[3]),
@@ -1767,7 +1773,8 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 
 // kAblate (tools/microbench/crc_ablation.hip only; the product launches 0):
 //   1 = loads only (words XOR-folded, no table lookups), 2 = lookups only (no global loads)
-// kCopy: fused bcopy -- each row is also stored to dst + f*dst_stride (16-byte aligned) as soon
+// kCopy: fused bcopy -- each row is also stored to dst + f*dst_stride (dst and dst_stride 4-byte
+// aligned: asm global_store_dwordx4 at dword-aligned addresses, launch_msg_bcopy's gate) as soon
 // as it arrives; per step the ring then carries 4K stores beside 4K loads, and the waits count
 // them (first pass: 8K / 12K / 16K younger operations, then 16K).  Rows move in the coalesced
 // layout (crc_chunks): lane-contiguous 64-byte stores run at 51% of the HBM roofline on
@@ -2087,7 +2094,7 @@ __global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__re
         for (int k = 0; k < 16; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)(r + k / 4) * kRowBytes + kS * (k & 3));
         if constexpr (kCopy) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) *(gwu32x4 *)(q + (uint64_t)(r + k / 4) * kRowBytes + kS * (k & 3)) = v[k];
+            for (int k = 0; k < 16; ++k) *(gwu32x4_a4 *)(q + (uint64_t)(r + k / 4) * kRowBytes + kS * (k & 3)) = v[k];
         }
 #pragma unroll
         for (int k = 0; k < 16; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
@@ -2098,7 +2105,7 @@ __global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__re
         for (int k = 0; k < 4; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)r * kRowBytes + kS * k);
         if constexpr (kCopy) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) *(gwu32x4 *)(q + (uint64_t)r * kRowBytes + kS * k) = v[k];
+            for (int k = 0; k < 4; ++k) *(gwu32x4_a4 *)(q + (uint64_t)r * kRowBytes + kS * k) = v[k];
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;

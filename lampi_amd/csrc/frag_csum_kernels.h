@@ -21,7 +21,7 @@ hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, ui
 // Fused copy + checksum (bcopy_uicrc / bcopy_uicsum per descriptor), mode = lampi_csum_mode.
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                              hipStream_t s);
-// Fused copy of regular batches: fragment f -> dst + f*dst_stride (16-byte aligned).
+// Fused copy of regular batches: fragment f -> dst + f*dst_stride (dst, dst_stride 4-byte aligned).
 hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint8_t *dst,
                                    size_t dst_stride, uint32_t *out, const uint32_t *img, hipStream_t s);
 // Fragments of a message, each copied to dst + k*dst_stride with its checksum fused.

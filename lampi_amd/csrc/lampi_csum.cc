@@ -73,10 +73,20 @@ int to_int(hipError_t e) { return (int)e; }
         if (e_ != hipSuccess) die(#call, e_);  \
     } while (0)
 
-// Per-thread staging for the synchronous host entry points.
+// Per-thread staging for the synchronous host entry points: a stream, device buffers and a
+// pinned host bounce buffer on the thread's current device.  Everything is released when the
+// thread exits (thread_local destructor -- LA-MPI progress threads come and go), when the
+// thread switches devices (the buffers belong to the old one), and on lampi_host_release().
+constexpr size_t kBounceHalf = 4u << 20;  // pinned bounce buffer: two halves (ping-pong pieces)
+constexpr uint64_t kPieceMin = 64 * 1024;  // host path: bytes per fragment piece
+constexpr uint32_t kMaxPieces = 16384;     // combine kernel capacity (LDS ping-pong)
+
 struct HostCtx {
     int dev = -1;
     hipStream_t stream = nullptr;
+    hipEvent_t half_free[2] = {nullptr, nullptr};  // the last transfer through each bounce half
+    uint8_t *pin = nullptr;                       // 2 x kBounceHalf pinned bytes
+    uint64_t *pres = nullptr;                     // pinned result words (4 x u64)
     uint8_t *dbuf = nullptr;
     size_t dcap = 0;
     uint32_t *dvals = nullptr;  // per-piece checksums + 4 result words
@@ -85,18 +95,63 @@ struct HostCtx {
     size_t desccap = 0;
     uint64_t *dvals64 = nullptr;  // 64-bit csum: per-piece sums + 3 result words
     size_t v64cap = 0;
-    std::vector<lampi_frag_desc> hdesc;
+    lampi_frag_desc *hdesc = nullptr;             // pinned piece descriptors (kMaxPieces)
     std::map<uint64_t, uint32_t *> combine_tabs;  // piece size -> device nibble tables
+
+    HostCtx() = default;
+    HostCtx(const HostCtx &) = delete;
+    HostCtx &operator=(const HostCtx &) = delete;
+    ~HostCtx() { release(); }
+
+    // Free every resource on the device it was made on; errors are ignored (this also runs at
+    // thread exit, where there is nobody to report them to).
+    void release() {
+        if (dev < 0) return;
+        int cur = -1;
+        const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+        if (have_cur && cur != dev) (void)hipSetDevice(dev);
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (dbuf) (void)hipFree(dbuf);
+        if (dvals) (void)hipFree(dvals);
+        if (ddesc) (void)hipFree(ddesc);
+        if (dvals64) (void)hipFree(dvals64);
+        for (auto &kv : combine_tabs) (void)hipFree(kv.second);
+        if (pin) (void)hipHostFree(pin);
+        if (pres) (void)hipHostFree(pres);
+        if (hdesc) (void)hipHostFree(hdesc);
+        for (hipEvent_t &e : half_free)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+        if (have_cur && cur != dev) (void)hipSetDevice(cur);
+        dev = -1;
+        stream = nullptr;
+        half_free[0] = half_free[1] = nullptr;
+        pin = nullptr;
+        pres = nullptr;
+        dbuf = nullptr;
+        dvals = nullptr;
+        ddesc = nullptr;
+        dvals64 = nullptr;
+        dcap = vcap = desccap = v64cap = 0;
+        hdesc = nullptr;
+        combine_tabs.clear();
+    }
 };
 
+thread_local HostCtx t_ctx;
+
 HostCtx &host_ctx() {
-    thread_local HostCtx ctx;
+    HostCtx &ctx = t_ctx;
     int dev = 0;
     LAMPI_CHECK(current_device(&dev));
     if (ctx.dev != dev) {
-        ctx = HostCtx();  // device changed: start over (old buffers belong to the old device)
+        ctx.release();  // device changed (or first use): the old buffers belong to the old device
         ctx.dev = dev;
         LAMPI_CHECK(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
+        for (hipEvent_t &e : ctx.half_free) LAMPI_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        LAMPI_CHECK(hipHostMalloc((void **)&ctx.pin, 2 * kBounceHalf, hipHostMallocDefault));
+        LAMPI_CHECK(hipHostMalloc((void **)&ctx.pres, 4 * sizeof(uint64_t), hipHostMallocDefault));
+        LAMPI_CHECK(hipHostMalloc((void **)&ctx.hdesc, kMaxPieces * sizeof(lampi_frag_desc), hipHostMallocDefault));
     }
     return ctx;
 }
@@ -111,8 +166,6 @@ void ensure(T *&p, size_t &cap, size_t n) {
     cap = c;
 }
 
-constexpr uint64_t kPieceMin = 64 * 1024;  // host path: bytes per fragment piece
-constexpr uint32_t kMaxPieces = 16384;     // combine kernel capacity (LDS ping-pong)
 
 uint64_t piece_size(uint64_t len) {
     uint64_t b = (len + kMaxPieces - 1) / kMaxPieces;
@@ -152,8 +205,7 @@ uint32_t device_crc(HostCtx &c, uint64_t len, uint32_t partial) {
     const uint32_t n = (uint32_t)((len + B - 1) / B);
     // pieces of the front-padded message: piece 0 holds the first len - (n-1)*B bytes
     const uint64_t first = len - (uint64_t)(n - 1) * B;
-    c.hdesc.resize(n);
-    for (uint32_t k = 0; k < n; ++k) {
+        for (uint32_t k = 0; k < n; ++k) {
         const uint64_t off = k == 0 ? 0 : first + (uint64_t)(k - 1) * B;
         c.hdesc[k].addr = (uint64_t)(uintptr_t)(c.dbuf + off);
         c.hdesc[k].length = (uint32_t)(k == 0 ? first : B);
@@ -161,7 +213,7 @@ uint32_t device_crc(HostCtx &c, uint64_t len, uint32_t partial) {
     }
     ensure(c.ddesc, c.desccap, n);
     ensure(c.dvals, c.vcap, (size_t)n + 4);
-    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc.data(), n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
+    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc, n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
                                c.stream));
     LAMPI_CHECK(launch_crc_desc(c.ddesc, n, c.dvals, img, grid, c.stream));
     uint32_t *res = c.dvals;
@@ -169,10 +221,10 @@ uint32_t device_crc(HostCtx &c, uint64_t len, uint32_t partial) {
         res = c.dvals + n;
         LAMPI_CHECK(launch_crc_combine(c.dvals, n, combine_tables(c, B), next_pow2(n), res, c.stream));
     }
-    uint32_t h = 0;
-    LAMPI_CHECK(hipMemcpyAsync(&h, res, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+    uint32_t *h = (uint32_t *)c.pres;
+    LAMPI_CHECK(hipMemcpyAsync(h, res, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
     LAMPI_CHECK(hipStreamSynchronize(c.stream));
-    return h;
+    return h[0];
 }
 
 // uicsum of c.dbuf[0..len) with chaining state, computed on the GPU.
@@ -183,8 +235,7 @@ uint32_t device_sum(HostCtx &c, uint64_t len, unsigned int *pint, unsigned int *
     const uint64_t body = (len - head) & ~3ull;
     const uint64_t B = piece_size(body ? body : 1);
     const uint32_t n = (uint32_t)((body + B - 1) / B);
-    c.hdesc.resize(n);
-    for (uint32_t i = 0; i < n; ++i) {
+        for (uint32_t i = 0; i < n; ++i) {
         c.hdesc[i].addr = (uint64_t)(uintptr_t)(c.dbuf + head + (uint64_t)i * B);
         c.hdesc[i].length = (uint32_t)std::min<uint64_t>(B, body - (uint64_t)i * B);
         c.hdesc[i].partial = 0;
@@ -192,14 +243,14 @@ uint32_t device_sum(HostCtx &c, uint64_t len, unsigned int *pint, unsigned int *
     ensure(c.ddesc, c.desccap, std::max<uint32_t>(n, 1));
     ensure(c.dvals, c.vcap, (size_t)n + 4);
     if (n) {
-        LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc.data(), n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
+        LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc, n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
                                    c.stream));
         LAMPI_CHECK(launch_sum_desc(c.ddesc, n, c.dvals, nullptr, grid, c.stream));
     }
     uint32_t *out3 = c.dvals + n;
     LAMPI_CHECK(launch_sum_finish(c.dvals, n, c.dbuf, len, *pint, *plen, out3, c.stream));
-    uint32_t h[3];
-    LAMPI_CHECK(hipMemcpyAsync(h, out3, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+    uint32_t *h = (uint32_t *)c.pres;
+    LAMPI_CHECK(hipMemcpyAsync(h, out3, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
     LAMPI_CHECK(hipStreamSynchronize(c.stream));
     *pint = h[1];
     *plen = h[2];
@@ -213,20 +264,19 @@ uint64_t device_sum64(HostCtx &c, uint64_t len, unsigned long *plong, unsigned l
     const uint64_t k = *plen >= 8 ? 0u : *plen;
     const uint64_t B = piece_size(len);
     const uint32_t n = (uint32_t)((len + B - 1) / B);
-    c.hdesc.resize(n);
-    for (uint32_t i = 0; i < n; ++i) {
+        for (uint32_t i = 0; i < n; ++i) {
         c.hdesc[i].addr = (uint64_t)(uintptr_t)(c.dbuf + (uint64_t)i * B);
         c.hdesc[i].length = (uint32_t)std::min<uint64_t>(B, len - (uint64_t)i * B);
         c.hdesc[i].partial = (uint32_t)((k + (uint64_t)i * B) & 7u);
     }
     ensure(c.ddesc, c.desccap, std::max<uint32_t>(n, 1));
     ensure(c.dvals64, c.v64cap, (size_t)n + 3);
-    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc.data(), n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice, c.stream));
+    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc, n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice, c.stream));
     LAMPI_CHECK(launch_sum64_desc(c.ddesc, n, c.dvals64, true, c.stream));
     uint64_t *out3 = c.dvals64 + n;
     LAMPI_CHECK(launch_sum64_finish(c.dvals64, n, c.dbuf, len, k ? (uint64_t)*plong : 0u, k, out3, c.stream));
-    uint64_t h[3];
-    LAMPI_CHECK(hipMemcpyAsync(h, out3, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+    uint64_t *h = c.pres;
+    LAMPI_CHECK(hipMemcpyAsync(h, out3, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
     LAMPI_CHECK(hipStreamSynchronize(c.stream));
     *plong = (unsigned long)h[1];
     *plen = (unsigned long)h[2];
@@ -241,15 +291,40 @@ unsigned long empty_sum64(unsigned long *plong, unsigned long *plen) {
     return 0;
 }
 
+// host -> c.dbuf through the pinned bounce buffer: pieces of kBounceHalf bytes alternate between
+// its two halves; a half is refilled once its previous DMA has completed (event), so the CPU
+// copy of one piece overlaps the DMA of the other.
 void stage_in(HostCtx &c, const void *src, uint64_t len) {
     ensure(c.dbuf, c.dcap, (size_t)len);
-    LAMPI_CHECK(hipMemcpyAsync(c.dbuf, src, len, hipMemcpyHostToDevice, c.stream));
+    const uint8_t *s = (const uint8_t *)src;
+    for (uint64_t off = 0, i = 0; off < len; off += kBounceHalf, ++i) {
+        const size_t n = (size_t)std::min<uint64_t>(kBounceHalf, len - off);
+        uint8_t *half = c.pin + (i & 1) * kBounceHalf;
+        LAMPI_CHECK(hipEventSynchronize(c.half_free[i & 1]));
+        std::memcpy(half, s + off, n);
+        LAMPI_CHECK(hipMemcpyAsync(c.dbuf + off, half, n, hipMemcpyHostToDevice, c.stream));
+        LAMPI_CHECK(hipEventRecord(c.half_free[i & 1], c.stream));
+    }
 }
 
+// c.dbuf -> host through the bounce buffer: the DMA of piece i+1 runs while piece i is copied out
 void stage_out(HostCtx &c, void *dst, uint64_t len) {
     if (!len) return;
-    LAMPI_CHECK(hipMemcpyAsync(dst, c.dbuf, len, hipMemcpyDeviceToHost, c.stream));
-    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    uint8_t *d = (uint8_t *)dst;
+    const uint64_t np = (len + kBounceHalf - 1) / kBounceHalf;
+    auto issue = [&](uint64_t i) {
+        const uint64_t off = i * kBounceHalf;
+        const size_t n = (size_t)std::min<uint64_t>(kBounceHalf, len - off);
+        LAMPI_CHECK(hipMemcpyAsync(c.pin + (i & 1) * kBounceHalf, c.dbuf + off, n, hipMemcpyDeviceToHost, c.stream));
+        LAMPI_CHECK(hipEventRecord(c.half_free[i & 1], c.stream));
+    };
+    issue(0);
+    for (uint64_t i = 0; i < np; ++i) {
+        if (i + 1 < np) issue(i + 1);  // the other half: free, its last use was copied out below
+        LAMPI_CHECK(hipEventSynchronize(c.half_free[i & 1]));
+        const uint64_t off = i * kBounceHalf;
+        std::memcpy(d + off, c.pin + (i & 1) * kBounceHalf, (size_t)std::min<uint64_t>(kBounceHalf, len - off));
+    }
 }
 
 // zero-length uicsum: no bytes, only the state convention of the reference
@@ -524,6 +599,8 @@ int lampi_fill_stream_frags(void *d_dst, size_t n, size_t frag_len, uint64_t see
     return to_int(launch_fill_frags((uint64_t *)d_dst, n, frag_len / 8, seed, k0, kstep, crc_grid(dev),
                                     (hipStream_t)stream));
 }
+
+void lampi_host_release(void) { t_ctx.release(); }
 
 const char *lampi_csum_version(void) { return "lampi-frag-csum 0.1 (gfx950, CDNA4)"; }
 

@@ -1,0 +1,84 @@
+"""GPU: native C++ programs through the drop-in boundary (VERDICT r1 "next" #8).
+
+* tests/native/dropin_caller -- written against the reference's MemFunctions.h overloads
+  (ref src/util/MemFunctions.h:43-65), compiled against include/lampi/MemFunctions.h and linked to
+  liblampi_csum.so exactly as INTEGRATION.md section 1 tells a maintainer; it runs the src/path
+  call shapes (uicrc over a DMA source, bcopy_uicrc with copylen < crclen, chained uicsum state,
+  the 64-bit overloads) on four threads and on the main thread around lampi_host_release().
+  Every printed result is recomputed here with the oracle (reference-pinned restatement).
+* tests/native/host_leak -- 1,000 short-lived threads making host calls (thread-exit release of
+  the staging context) and 1,000 call + lampi_host_release() rounds (the release a device switch
+  runs): device memory in use must not grow.
+Both binaries are built on the CPU by __graft_entry__.build() (make -C tests/native).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _bin(name):
+    p = os.path.join(HERE, "native", name)
+    if not os.path.exists(p):
+        pytest.fail(f"{p} not built: run __graft_entry__.build() (make -C tests/native)")
+    return p
+
+
+def test_native_dropin_caller_matches_oracle(cuda, oracle):
+    seed = 11
+    r = subprocess.run([_bin("dropin_caller"), str(seed), "4"], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if "->" in ln]
+    assert r.stdout.strip().endswith("done")
+    buf = oracle.stream(seed, 0, 3 << 20)
+    seen = set()
+    for ln in lines:
+        lhs, rhs = ln.split("->")
+        tid, op, off, doff, copylen, csumlen, partial, pint, plen = lhs.split()
+        off, copylen, csumlen, partial, pint, plen = map(int, (off, copylen, csumlen, partial, pint, plen))
+        res, pi_out, pl_out, ok = map(int, rhs.split())
+        src = buf[off:off + max(copylen, csumlen)]
+        dst = np.zeros(max(copylen, 1), np.uint8)
+        if op == "uicrc":
+            want = (oracle.uicrc(src, csumlen),)
+        elif op == "uicrc_p":
+            want = (oracle.uicrc(src, csumlen, partial),)
+        elif op == "bcopy_uicrc":
+            want = (oracle.bcopy_uicrc(src, dst, copylen, csumlen),)
+        elif op == "bcopy_uicrc_p":
+            want = (oracle.bcopy_uicrc(src, dst, copylen, csumlen, partial),)
+        elif op == "uicsum":
+            want = (oracle.uicsum(src, csumlen)[0],)
+        elif op == "uicsum_s":
+            want = oracle.uicsum(src, csumlen, pint, plen)
+        elif op == "bcopy_uicsum":
+            want = (oracle.bcopy_uicsum(src, dst, copylen, csumlen)[0],)
+        elif op == "bcopy_uicsum_s":
+            want = oracle.bcopy_uicsum(src, dst, copylen, csumlen, pint, plen)
+        elif op == "csum":
+            want = (oracle.csum(src, csumlen)[0],)
+        elif op == "bcopy_csum":
+            want = (oracle.bcopy_csum(src, dst, copylen, csumlen)[0],)
+        else:
+            raise AssertionError(op)
+        got = (res, pi_out, pl_out) if len(want) == 3 else (res,)
+        assert got == tuple(want), ln
+        assert ok == 1, ln
+        seen.add((tid, op))
+    assert len({t for t, _ in seen}) == 5  # four worker threads + the main thread
+    assert len(lines) == (4 + 2) * 16 * 10  # (4 worker threads + 2 main-thread rounds) x 16 cases x 10 ops
+
+
+def test_native_host_staging_does_not_leak(cuda):
+    r = subprocess.run([_bin("host_leak"), "1000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    f = dict(zip(r.stdout.split()[0::2], map(int, r.stdout.split()[1::2])))
+    assert f["rounds"] == 1000 and f["bad"] == 0
+    # a leaked context holds >= 1 MiB of device buffers: 1,000 leaks would be >= 1 GiB
+    assert f["after_threads"] - f["used_before"] < (64 << 20), r.stdout
+    assert f["after_release"] - f["used_before"] < (64 << 20), r.stdout

@@ -7,6 +7,11 @@ coalesced streaming read, so read bytes = 2 x FETCH_SIZE x 1024.  TCC_EA0_RDREQ 
 is reported beside it as a cross-check.  Values are per dispatch of the named kernel,
 averaged over the profiled launches.
 
+WRITE_SIZE (its own pass, --write) reads the bytes exactly for 16-B-per-lane streaming stores
+(same guide section); with it, hbm_bytes_per_launch = read + written bytes (fused copies).
+--skip/--take select matched dispatches in dispatch order (a bench run that launches one kernel
+template for several layouts in turn).
+
 Usage: tools/pmc_traffic.py --fetch gpurun_out/pmc_fetch --ea gpurun_out/pmc_ea \
            --kernel crc_regular_kernel --key crc_4194304x4096 --out profiles/traffic.json
 """
@@ -18,28 +23,34 @@ import json
 import os
 
 
-def per_dispatch(root, kernel_substr):
+def per_dispatch(root, kernel_substr, skip=0, take=None):
     files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
+    if os.path.isfile(root):
+        files = [root]
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     for f in files:
         for r in csv.DictReader(open(f)):
             if kernel_substr not in r["Kernel_Name"]:
                 continue
-            vals[(f, r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
-    return list(vals.values())
+            vals[(f, int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(r["Counter_Value"])
+    out = [vals[k] for k in sorted(vals)][skip:]
+    return out if take is None else out[:take]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--ea")
+    ap.add_argument("--write", help="WRITE_SIZE pass (fused copies: traffic = read + written bytes)")
+    ap.add_argument("--skip", type=int, default=0)
+    ap.add_argument("--take", type=int, default=None)
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--key", required=True)
     ap.add_argument("--algorithmic-bytes", type=int, required=True)
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--source", default="")
     a = ap.parse_args()
-    fd = per_dispatch(a.fetch, a.kernel)
+    fd = per_dispatch(a.fetch, a.kernel, a.skip, a.take)
     if not fd:
         raise SystemExit(f"no dispatches of {a.kernel} in {a.fetch}")
     fetch_kb = sum(d["FETCH_SIZE"] for d in fd) / len(fd)
@@ -52,6 +63,16 @@ def main():
         "correction": "x2 (gfx950 FETCH_SIZE counts 128-B requests at 64 B, MI355X_MICROARCH.md HBM section)",
         "source": a.source,
     }
+    if a.write:
+        wd = per_dispatch(a.write, a.kernel, a.skip, a.take)
+        if not wd:
+            raise SystemExit(f"no dispatches of {a.kernel} in {a.write}")
+        write_kb = sum(d["WRITE_SIZE"] for d in wd) / len(wd)
+        entry["WRITE_SIZE_kB"] = write_kb
+        entry["read_bytes_per_launch"] = entry["hbm_bytes_per_launch"]
+        entry["write_bytes_per_launch"] = int(write_kb * 1024)
+        entry["hbm_bytes_per_launch"] += int(write_kb * 1024)
+        entry["correction"] += "; WRITE_SIZE x1 (exact for 16-B-per-lane streaming stores)"
     if a.ea:
         ed = per_dispatch(a.ea, a.kernel)
         if ed:
