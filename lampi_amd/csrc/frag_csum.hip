@@ -72,6 +72,8 @@ typedef __attribute__((address_space(1))) u32x4 gwu32x4;
 // header): the type says 4-byte alignment, so the compiler assumes nothing more than the host
 // gates guarantee; global_store_dwordx4 at a dword-aligned address runs at the aligned rate
 typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
+typedef __attribute__((address_space(1))) const u32x4_a1 gu32x4_a1;  // unaligned 16-byte loads
 typedef __attribute__((address_space(1))) u32x4_a4 gwu32x4_a4;
 
 struct FragInfo {
@@ -80,6 +82,8 @@ struct FragInfo {
     uint32_t partial;
     uint8_t *dst;      // copy sources only: destination of the first copylen bytes
     uint32_t copylen;
+    uint32_t aux = 0;  // receive sources: the expected checksum, loaded with the descriptor so its
+                       // latency hides under the fragment's rows (emit compares against it)
 };
 
 // ---- fragment sources (wave-uniform) ----------------------------------------------
@@ -189,11 +193,12 @@ struct RecvSource {
     __device__ FragInfo get(size_t f) const {
         const lampi_recv_desc x = d[f];
         const uint32_t c = to_copy(x);
-        return {(gbyte *)(uintptr_t)x.frag, c ? x.length : 0u, empty, (uint8_t *)(uintptr_t)x.app, c};
+        const uint32_t e = c ? *(const guint *)(expected + f * exp_stride) : 0u;
+        return {(gbyte *)(uintptr_t)x.frag, c ? x.length : 0u, empty, (uint8_t *)(uintptr_t)x.app, c, e};
     }
-    __device__ void verdict(size_t f, uint32_t v) const {
-        const uint32_t c = to_copy(d[f]);
-        const bool bad = c != 0u && v != *(const guint *)(expected + f * exp_stride);
+    __device__ void verdict(size_t f, uint32_t v, const FragInfo &fi) const {
+        const uint32_t c = fi.copylen;
+        const bool bad = c != 0u && v != fi.aux;
         copied[f] = bad ? -1ll : (int64_t)c;
         if (bad) {  // rare: one atomic per corrupt fragment
             atomicOr(mask + (f >> 5), 1u << (f & 31u));
@@ -209,9 +214,9 @@ struct IsRecv<RecvSource> : std::true_type {};
 
 // every kernel stores a fragment's checksum through this: receive sources also decide it
 template <class Src, class Acc>
-__device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v) {
+__device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v, const FragInfo &fi) {
     out[f] = v;
-    if constexpr (IsRecv<Src>::value) src.verdict(f, v);
+    if constexpr (IsRecv<Src>::value) src.verdict(f, v, fi);
 }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -413,6 +418,22 @@ __device__ __forceinline__ uint32_t byte_keep_mask(long long ow, long long lo, l
 
 __device__ __forceinline__ void load64(gbyte *frag, long long o, long long lo, long long hi,
                                        bool mask, uint32_t s16, uint32_t d[16]) {
+    if (s16 != 0 && !mask) {
+        // misaligned, every byte inside [lo, hi): four unaligned 16-byte loads (one
+        // global_load_dwordx4 each; the memory pipeline splits them at line boundaries).  A plain
+        // copy from 8-byte-aligned GM slot payloads runs at the aligned rate this way
+        // (profiles/r02_copy_lds.txt, SLOT gather); the five aligned chunks + funnel shift below
+        // cost one more load and 16 v_alignbyte per row.
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32x4 v = *(gu32x4_a1 *)(frag + o + 16 * k);
+            d[4 * k + 0] = v.x;
+            d[4 * k + 1] = v.y;
+            d[4 * k + 2] = v.z;
+            d[4 * k + 3] = v.w;
+        }
+        return;
+    }
     if (s16 == 0) {
         // 16-byte aligned chunks
 #pragma unroll
@@ -729,7 +750,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                 fi.copylen = uniform(fi.copylen);
             }
             if (fi.len) return x;
-            if (lane == 0) emit(src, out, x, fi.partial);  // uicrc(p, 0, s) == s
+            if (lane == 0) emit(src, out, x, fi.partial, fi);  // uicrc(p, 0, s) == s
         }
         return n;
     };
@@ -815,7 +836,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
             if (lane == 0) {
                 uint32_t res = __builtin_bswap32(C);
                 if (cur.len < 4) res ^= cur.partial << (8 * cur.len);
-                emit(src, out, f, res);
+                emit(src, out, f, res, cur);
             }
         }
         if (!more) break;
@@ -1636,7 +1657,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
         }
     }
     __syncthreads();
-    if (t < nwg) emit(src, out, base + t, sres[t]);
+    if (t < nwg) emit(src, out, base + t, sres[t], mine);
 }
 
 // ---- CRC fast path: regular batches -------------------------------------------------------
@@ -2016,7 +2037,9 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
         uint32_t carry = 0;
         for (uint32_t r = 0; r < R; ++r) {
             const long long o = (long long)r * kRowBytes + lane * kLaneBytes;
-            const bool mask = (r == 0 && ph != 0) || (r + 1 == R && span % kRowBytes != 0) || s16 != 0;
+            // rows wholly inside the fragment load unmasked (also when misaligned: load64's
+            // unaligned path); edge rows read only the aligned chunks that hold fragment bytes
+            const bool mask = (r == 0 && ph != 0) || (r + 1 == R && span % kRowBytes != 0);
             uint32_t d[16];
             load64(fb, o, ph, (long long)span, mask, s16, d);
             if constexpr (Src::kCopy) {
@@ -2063,7 +2086,7 @@ __global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uin
 #pragma unroll
             for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
         }
-        if (lane == 0) emit(src, out, f, acc);
+        if (lane == 0) emit(src, out, f, acc, fi);
     }
 }
 

@@ -92,15 +92,56 @@ __global__ void __launch_bounds__(T) cp_wg(const u32x4 *__restrict__ s, u32x4 *_
     if (LDSB && lds[(lane * 7) % (LDSB / 4 > 0 ? LDSB / 4 : 1)] == 0xFFFFFFFFu) sink[0] = 1;
 }
 
+// GM ring slots: block k's 4096 payload bytes live at slot k (stride 4176) + 72 -- 8 bytes past a
+// 16-byte boundary.  G = gather (slots -> contiguous, the receive side), S = scatter (contiguous ->
+// slots, the send side).  16-byte accesses at 8-byte-aligned addresses (aligned(8) vector type).
+typedef u32x4 u32x4_a8 __attribute__((aligned(8)));
+template <int T, int LDSB, int J, bool kGather>
+__global__ void __launch_bounds__(T) cp_slot(const unsigned char *__restrict__ s, unsigned char *__restrict__ d,
+                                             size_t nblk, unsigned steps, unsigned *sink) {
+    __shared__ unsigned lds[LDSB / 4 > 0 ? LDSB / 4 : 1];
+    constexpr unsigned nw = T / 64;
+    const unsigned w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (LDSB) {
+        lds[threadIdx.x % (LDSB / 4 > 0 ? LDSB / 4 : 1)] = threadIdx.x;
+        __syncthreads();
+    }
+    // unit u = 1 KiB quarter of block u/4; the workgroup walks `steps` super-rows of nw*J units
+    const size_t row = (size_t)nw * J;
+    const size_t base = (size_t)blockIdx.x * steps * row;
+    for (unsigned st = 0; st < steps; ++st) {
+        u32x4 v[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const size_t u = base + st * row + (size_t)(j * nw + w);
+            const size_t blk = u >> 2, q = u & 3;
+            if (blk < nblk) {
+                const size_t so = kGather ? blk * 4176 + 72 + q * 1024 + 16 * lane : u * 1024 + 16 * lane;
+                v[j] = *(const u32x4_a8 *)(s + so);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const size_t u = base + st * row + (size_t)(j * nw + w);
+            const size_t blk = u >> 2, q = u & 3;
+            if (blk < nblk) {
+                const size_t dof = kGather ? u * 1024 + 16 * lane : blk * 4176 + 72 + q * 1024 + 16 * lane;
+                *(u32x4_a8 *)(d + dof) = v[j];
+            }
+        }
+    }
+    if (LDSB && lds[(lane * 7) % (LDSB / 4 > 0 ? LDSB / 4 : 1)] == 0xFFFFFFFFu) sink[0] = 1;
+}
+
 int main(int argc, char **argv) {
     const size_t bytes = argc > 1 ? strtoull(argv[1], 0, 0) : (8ull << 30);
     unsigned char *s, *d;
     unsigned *sink;
-    CK(hipMalloc(&s, bytes));
-    CK(hipMalloc(&d, bytes));
+    CK(hipMalloc(&s, bytes + bytes / 32));  // room for the slot layout (4176 / 4096 of the payload)
+    CK(hipMalloc(&d, bytes + bytes / 32));
     CK(hipMalloc(&sink, 64));
-    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)s, bytes / 8);
-    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)d, bytes / 8);
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)s, (bytes + bytes / 32) / 8);
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)d, (bytes + bytes / 32) / 8);
     CK(hipDeviceSynchronize());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -148,6 +189,22 @@ int main(int argc, char **argv) {
     ADD(1024, 100000, 1, true, 48)
     ADD(1024, 100000, 2, true, 24)
     ADD(1024, 100000, 4, true, 12)
+    const size_t nblk = bytes / 4096;
+#define SLOT(T, LDSB, J, G, STEPS)                                                                              \
+    vs.push_back({std::string(G ? "SLOT gather" : "SLOT scatter") + " T=" #T " lds=" #LDSB " J=" #J " steps=" #STEPS, \
+                  [=] {                                                                                          \
+                      const size_t per = (size_t)(T / 64) * J * STEPS;                                           \
+                      hipLaunchKernelGGL((cp_slot<T, LDSB, J, G>), dim3((unsigned)((nblk * 4 + per - 1) / per)), \
+                                         dim3(T), 0, 0, s, d, nblk, STEPS, sink);                                \
+                  }});
+    SLOT(256, 0, 1, true, 1)
+    SLOT(256, 0, 1, false, 1)
+    SLOT(256, 65536, 2, true, 16)
+    SLOT(256, 65536, 2, false, 16)
+    SLOT(512, 65536, 2, true, 24)
+    SLOT(512, 65536, 2, false, 24)
+    SLOT(1024, 100000, 4, true, 12)
+    SLOT(1024, 100000, 4, false, 12)
     for (auto &v : vs) v.f();
     CK(hipGetLastError());
     CK(hipDeviceSynchronize());

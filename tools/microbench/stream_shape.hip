@@ -1,0 +1,147 @@
+// stream_shape.hip -- the read shape of crc_stream_kernel, and alternatives, without the CRC work.
+// crc_stream_kernel (config C): 768-thread workgroups (12 waves, one chain each), ~77 KiB LDS (two
+// workgroups per CU), a workgroup owns ~620 KiB of fragments cut into 4 KiB rows (64 lanes x 64
+// contiguous bytes); chain c walks rows [c*R/12, (c+1)*R/12) with two rows in flight.  Question:
+// does the spread of the 12 chains over the workgroup's region (12 streams ~52 KiB apart) cost
+// read bandwidth against shapes whose chains read adjacent rows?
+//   CONTIG     : the product's shape
+//   SUB(S)     : chain c reads sub-blocks of S rows: c, c + 12, c + 24, ... (a 12*S-row window)
+//   INTER      : SUB(1) -- chain c reads rows c, c + 12, ...
+// Rows per workgroup R = 155 (~620 KiB), 4 GiB total, random payload, 3 rounds x 4 launches.
+// Build: hipcc --offload-arch=gfx950 -O3 stream_shape.hip -o stream_shape
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                                       \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) {                                                                     \
+            fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+            exit(1);                                                                                \
+        }                                                                                           \
+    } while (0)
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void fill(uint64_t *p, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t z = 0x1234567ull + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+// row index (within the workgroup) of chain c's i-th row, for sub-block size S (0: contiguous)
+__device__ __forceinline__ int row_of(int c, int i, int R, int S, int nch) {
+    if (S == 0) return c * R / nch + i;
+    const int blk = i / S, k = i % S;
+    return (blk * nch + c) * S + k;
+}
+__device__ __forceinline__ int rows_of(int c, int R, int S, int nch) {
+    if (S == 0) return (c + 1) * R / nch - c * R / nch;
+    int n = 0;
+    for (int b = 0;; ++b) {
+        const int r0 = (b * nch + c) * S;
+        if (r0 >= R) break;
+        n += min(S, R - r0);
+    }
+    return n;
+}
+
+template <int NW, int LDSB>
+__global__ void __launch_bounds__(64 * NW) rd_stream(const unsigned char *__restrict__ s, size_t nrows_total,
+                                                     int R, int S, unsigned *sink) {
+    __shared__ unsigned lds[LDSB / 4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    lds[threadIdx.x % (LDSB / 4)] = threadIdx.x;
+    __syncthreads();
+    const size_t wg_row0 = (size_t)blockIdx.x * R;
+    const int n = rows_of(w, R, S, NW);
+    unsigned x = 0;
+    u32x4 a[4], b[4];
+    auto ld = [&](int i, u32x4 (&v)[4]) {
+        const size_t row = wg_row0 + row_of(w, i, R, S, NW);
+        const u32x4 *p = (const u32x4 *)(s + row * 4096 + lane * 64);
+        if (row < nrows_total) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = p[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = u32x4{0, 0, 0, 0};
+        }
+    };
+    if (n > 0) ld(0, a);
+    for (int i = 0; i < n; i += 2) {
+        if (i + 1 < n) ld(i + 1, b);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x ^= a[k].x ^ a[k].y ^ a[k].z ^ a[k].w;
+        if (i + 2 < n) ld(i + 2, a);
+        if (i + 1 < n) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x ^= b[k].x ^ b[k].y ^ b[k].z ^ b[k].w;
+        }
+    }
+    if (x == 0x9E3779B9u || lds[(lane * 5) % (LDSB / 4)] == 0xFFFFFFFFu) sink[0] = x;
+}
+
+int main(int argc, char **argv) {
+    const size_t bytes = argc > 1 ? strtoull(argv[1], 0, 0) : (4ull << 30);
+    unsigned char *s;
+    unsigned *sink;
+    CK(hipMalloc(&s, bytes));
+    CK(hipMalloc(&sink, 64));
+    hipLaunchKernelGGL(fill, dim3(4096), dim3(256), 0, 0, (uint64_t *)s, bytes / 8);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const size_t nrows = bytes / 4096;
+    struct V {
+        std::string name;
+        std::function<void()> f;
+        float sum = 0;
+    };
+    std::vector<V> vs;
+    auto add = [&](std::string nm, int R, int S, bool small) {
+        vs.push_back({nm + " R=" + std::to_string(R) + " S=" + std::to_string(S), [=] {
+                          const unsigned g = (unsigned)((nrows + R - 1) / R);
+                          if (small)
+                              hipLaunchKernelGGL((rd_stream<12, 40000>), dim3(g), dim3(768), 0, 0, s, nrows, R, S, sink);
+                          else
+                              hipLaunchKernelGGL((rd_stream<12, 79000>), dim3(g), dim3(768), 0, 0, s, nrows, R, S, sink);
+                      }});
+    };
+    for (int R : {155, 96, 48}) {
+        add("CONTIG 2wg/cu", R, 0, false);
+        for (int S : {1, 2, 4, 8}) add("SUB 2wg/cu", R, S, false);
+    }
+    add("CONTIG 4wg/cu(40K lds)", 155, 0, true);
+    add("SUB 4wg/cu(40K lds)", 155, 2, true);
+    for (auto &v : vs) v.f();
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    const int rounds = 3, reps = 4;
+    for (int r = 0; r < rounds; ++r)
+        for (auto &v : vs)
+            for (int k = 0; k < reps; ++k) {
+                CK(hipEventRecord(e0));
+                v.f();
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                v.sum += ms;
+            }
+    for (auto &v : vs) {
+        const double avg = v.sum / (rounds * reps) / 1e3;
+        const double gb = (double)bytes / avg / 1e9;
+        printf("%-36s avg %7.3f ms  %7.1f GB/s  %5.1f%% of 8 TB/s\n", v.name.c_str(), avg * 1e3, gb, gb / 80.0);
+    }
+    return 0;
+}
