@@ -118,6 +118,12 @@ def parse():
                     help="run the batch through descriptors (lampi_frag_csum_batch, the general kernel) "
                          "instead of the contiguous-message entry point (diagnostic)")
     args = ap.parse_args()
+    # rehearsal knobs (not for measurements): the bookkeeping backend, and ranks sharing GPUs so the
+    # N-rank flow can be exercised on a smaller box (LAMPI_BENCH_SHARE_GPU=1: rank r on GPU r % ndev)
+    args.backend = os.environ.get("LAMPI_BENCH_BACKEND", "nccl")
+    args.share_gpu = os.environ.get("LAMPI_BENCH_SHARE_GPU") == "1"
+    if args.backend not in ("nccl", "gloo"):
+        ap.error("LAMPI_BENCH_BACKEND must be nccl or gloo")
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
     if args.frags is None:
@@ -190,18 +196,24 @@ def dist_setup(args):
 
     ndev = torch.cuda.device_count()
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    if ndev < local_world or local >= ndev:
+    if not args.share_gpu and (ndev < local_world or local >= ndev):
         raise SystemExit(f"bench.py: {local_world} ranks on this node need {local_world} GPUs; "
                          f"{ndev} visible (rank {rank}, local rank {local})")
-    torch.cuda.set_device(local)
+    if ndev == 0:
+        raise SystemExit("bench.py: no GPU visible")
+    dev = local % ndev if args.share_gpu else local
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":  # RCCL: bookkeeping only (barrier, max time, digests)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
     return rank, world, local
 
 
 def _coll_device(args):
-    return "cpu" if args.dry_run else "cuda"
+    return "cpu" if args.dry_run or args.backend != "nccl" else "cuda"
 
 
 def barrier(world):
@@ -523,6 +535,9 @@ def run_device(args):
         }
         if args.dry_run:
             result["dry_run"] = True
+        if args.share_gpu and world > 1:
+            result["rehearsal"] = (f"{world} ranks shared the visible GPU(s) (LAMPI_BENCH_SHARE_GPU=1, backend "
+                                   f"{args.backend}): checks the N-rank flow; the numbers are not a scaling result")
         if world == 1 and not args.no_cpu_baseline and not args.dry_run and args.shard is None:
             result["cpu_baseline"] = cpu_baseline()
         else:
@@ -951,6 +966,27 @@ def run_latency(args):
         msg_rows.append({"fragments": n, "bytes": n * L, "stream_us_per_call": round(us, 2),
                          "GiB_per_s_stream": round(n * L / GIB / (us / 1e6), 2)})
     rows.append({"lampi_msg_csum": msg_rows})
+    # the drop-in host entry points (pageable host buffer in, checksum out; pinned bounce buffer
+    # inside the library): what an unchanged src/path call site pays per call
+    from lampi_amd._lib import lib as _clib
+
+    host_rows = []
+    hb = np.frombuffer(np.random.default_rng(3).bytes(1 << 20), dtype=np.uint8).copy()
+    hd = np.empty_like(hb)
+    for nb in (1976, 4096, 65456, 1 << 20):
+        t = []
+        for i in range(220):
+            t0 = time.perf_counter()
+            _clib().lampi_uicrc(hb.ctypes.data, nb, 0xFFFFFFFF)
+            t.append(time.perf_counter() - t0)
+        tc = []
+        for i in range(220):
+            t0 = time.perf_counter()
+            _clib().lampi_bcopy_uicrc(hb.ctypes.data, hd.ctypes.data, nb, nb, 0xFFFFFFFF)
+            tc.append(time.perf_counter() - t0)
+        host_rows.append({"bytes": nb, "uicrc_us_median": round(float(np.median(t[20:])) * 1e6, 2),
+                          "bcopy_uicrc_us_median": round(float(np.median(tc[20:])) * 1e6, 2)})
+    rows.append({"host_entry_points": host_rows})
     dv.frag_csum_batch(descs, n=nmax, out=out)
     got = dv.as_u32(out[:nmax])
     from lampi_amd import shard
