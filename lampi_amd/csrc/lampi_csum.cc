@@ -78,6 +78,11 @@ int to_int(hipError_t e) { return (int)e; }
 // thread exits (thread_local destructor -- LA-MPI progress threads come and go), when the
 // thread switches devices (the buffers belong to the old one), and on lampi_host_release().
 constexpr size_t kBounceHalf = 4u << 20;  // pinned bounce buffer: two halves (ping-pong pieces)
+// Calls of up to kZeroCopy bytes skip the DMA engines: the bytes are copied into a host-coherent
+// pinned buffer the kernels read directly over PCIe, the descriptors are read from pinned memory
+// too and the result is written straight to pinned memory -- one kernel launch (two for SUM or a
+// CRC of more than one piece) and one synchronize per call instead of three DMA round trips.
+constexpr size_t kZeroCopy = 256u << 10;
 constexpr uint64_t kPieceMin = 64 * 1024;  // host path: bytes per fragment piece
 constexpr uint32_t kMaxPieces = 16384;     // combine kernel capacity (LDS ping-pong)
 
@@ -86,7 +91,11 @@ struct HostCtx {
     hipStream_t stream = nullptr;
     hipEvent_t half_free[2] = {nullptr, nullptr};  // the last transfer through each bounce half
     uint8_t *pin = nullptr;                       // 2 x kBounceHalf pinned bytes
-    uint64_t *pres = nullptr;                     // pinned result words (4 x u64)
+    uint64_t *pres = nullptr;                     // pinned, host-coherent result words (4 x u64)
+    uint8_t *zpin = nullptr;                      // pinned, host-coherent staging of small calls
+    uint8_t *zpin_d = nullptr;                    // ... and the device's view of it,
+    uint64_t *pres_d = nullptr;                   //     of pres
+    lampi_frag_desc *hdesc_d = nullptr;           //     and of hdesc
     uint8_t *dbuf = nullptr;
     size_t dcap = 0;
     uint32_t *dvals = nullptr;  // per-piece checksums + 4 result words
@@ -119,6 +128,7 @@ struct HostCtx {
         if (pin) (void)hipHostFree(pin);
         if (pres) (void)hipHostFree(pres);
         if (hdesc) (void)hipHostFree(hdesc);
+        if (zpin) (void)hipHostFree(zpin);
         for (hipEvent_t &e : half_free)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -134,6 +144,9 @@ struct HostCtx {
         dvals64 = nullptr;
         dcap = vcap = desccap = v64cap = 0;
         hdesc = nullptr;
+        zpin = zpin_d = nullptr;
+        pres_d = nullptr;
+        hdesc_d = nullptr;
         combine_tabs.clear();
     }
 };
@@ -150,8 +163,13 @@ HostCtx &host_ctx() {
         LAMPI_CHECK(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
         for (hipEvent_t &e : ctx.half_free) LAMPI_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         LAMPI_CHECK(hipHostMalloc((void **)&ctx.pin, 2 * kBounceHalf, hipHostMallocDefault));
-        LAMPI_CHECK(hipHostMalloc((void **)&ctx.pres, 4 * sizeof(uint64_t), hipHostMallocDefault));
-        LAMPI_CHECK(hipHostMalloc((void **)&ctx.hdesc, kMaxPieces * sizeof(lampi_frag_desc), hipHostMallocDefault));
+        constexpr unsigned kCoherent = hipHostMallocMapped | hipHostMallocCoherent;
+        LAMPI_CHECK(hipHostMalloc((void **)&ctx.pres, 4 * sizeof(uint64_t), kCoherent));
+        LAMPI_CHECK(hipHostMalloc((void **)&ctx.hdesc, kMaxPieces * sizeof(lampi_frag_desc), kCoherent));
+        LAMPI_CHECK(hipHostMalloc((void **)&ctx.zpin, kZeroCopy, kCoherent));
+        LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.zpin_d, ctx.zpin, 0));
+        LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.pres_d, ctx.pres, 0));
+        LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.hdesc_d, ctx.hdesc, 0));
     }
     return ctx;
 }
@@ -196,8 +214,24 @@ uint32_t *combine_tables(HostCtx &c, uint64_t B) {
     return d;
 }
 
-// CRC of c.dbuf[0..len) from register `partial`, computed on the GPU.
-uint32_t device_crc(HostCtx &c, uint64_t len, uint32_t partial) {
+// The staged bytes of a host call: small calls in the host-coherent pinned buffer (read by the
+// kernels over PCIe), larger ones DMA'd into c.dbuf through the bounce buffer.
+struct Staged {
+    const uint8_t *base;  // device address of the bytes
+    bool zero_copy;
+};
+
+// Piece descriptors for the kernels: zero-copy calls hand the kernels the pinned array itself.
+const lampi_frag_desc *upload_descs(HostCtx &c, uint32_t n, bool zero_copy) {
+    if (zero_copy) return c.hdesc_d;
+    ensure(c.ddesc, c.desccap, std::max<uint32_t>(n, 1));
+    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc, n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice, c.stream));
+    return c.ddesc;
+}
+
+// CRC of the staged bytes [0, len) from register `partial`, computed on the GPU; the result is
+// written by the last kernel straight into pinned host memory.
+uint32_t device_crc(HostCtx &c, const Staged &st, uint64_t len, uint32_t partial) {
     const uint32_t *img = nullptr;
     LAMPI_CHECK(device_tables(c.dev, &img));
     const int grid = crc_grid(c.dev);
@@ -205,79 +239,71 @@ uint32_t device_crc(HostCtx &c, uint64_t len, uint32_t partial) {
     const uint32_t n = (uint32_t)((len + B - 1) / B);
     // pieces of the front-padded message: piece 0 holds the first len - (n-1)*B bytes
     const uint64_t first = len - (uint64_t)(n - 1) * B;
-        for (uint32_t k = 0; k < n; ++k) {
+    for (uint32_t k = 0; k < n; ++k) {
         const uint64_t off = k == 0 ? 0 : first + (uint64_t)(k - 1) * B;
-        c.hdesc[k].addr = (uint64_t)(uintptr_t)(c.dbuf + off);
+        c.hdesc[k].addr = (uint64_t)(uintptr_t)(st.base + off);
         c.hdesc[k].length = (uint32_t)(k == 0 ? first : B);
         c.hdesc[k].partial = k == 0 ? partial : 0u;
     }
-    ensure(c.ddesc, c.desccap, n);
-    ensure(c.dvals, c.vcap, (size_t)n + 4);
-    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc, n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
-                               c.stream));
-    LAMPI_CHECK(launch_crc_desc(c.ddesc, n, c.dvals, img, grid, c.stream));
-    uint32_t *res = c.dvals;
-    if (n > 1) {
-        res = c.dvals + n;
+    const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
+    uint32_t *res = (uint32_t *)c.pres_d;
+    if (n == 1) {
+        LAMPI_CHECK(launch_crc_desc(d, 1, res, img, grid, c.stream));
+    } else {
+        ensure(c.dvals, c.vcap, (size_t)n + 4);
+        LAMPI_CHECK(launch_crc_desc(d, n, c.dvals, img, grid, c.stream));
         LAMPI_CHECK(launch_crc_combine(c.dvals, n, combine_tables(c, B), next_pow2(n), res, c.stream));
     }
-    uint32_t *h = (uint32_t *)c.pres;
-    LAMPI_CHECK(hipMemcpyAsync(h, res, sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
     LAMPI_CHECK(hipStreamSynchronize(c.stream));
-    return h[0];
+    return ((const volatile uint32_t *)c.pres)[0];
 }
 
-// uicsum of c.dbuf[0..len) with chaining state, computed on the GPU.
-uint32_t device_sum(HostCtx &c, uint64_t len, unsigned int *pint, unsigned int *plen) {
+// uicsum of the staged bytes [0, len) with chaining state, computed on the GPU.
+uint32_t device_sum(HostCtx &c, const Staged &st, uint64_t len, unsigned int *pint, unsigned int *plen) {
     const int grid = crc_grid(c.dev);
     const uint32_t k = *plen >= 4 ? 0u : *plen;
     const uint64_t head = k ? std::min<uint64_t>(4 - k, len) : 0;
     const uint64_t body = (len - head) & ~3ull;
     const uint64_t B = piece_size(body ? body : 1);
     const uint32_t n = (uint32_t)((body + B - 1) / B);
-        for (uint32_t i = 0; i < n; ++i) {
-        c.hdesc[i].addr = (uint64_t)(uintptr_t)(c.dbuf + head + (uint64_t)i * B);
+    for (uint32_t i = 0; i < n; ++i) {
+        c.hdesc[i].addr = (uint64_t)(uintptr_t)(st.base + head + (uint64_t)i * B);
         c.hdesc[i].length = (uint32_t)std::min<uint64_t>(B, body - (uint64_t)i * B);
         c.hdesc[i].partial = 0;
     }
-    ensure(c.ddesc, c.desccap, std::max<uint32_t>(n, 1));
     ensure(c.dvals, c.vcap, (size_t)n + 4);
     if (n) {
-        LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc, n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice,
-                                   c.stream));
-        LAMPI_CHECK(launch_sum_desc(c.ddesc, n, c.dvals, nullptr, grid, c.stream));
+        const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
+        LAMPI_CHECK(launch_sum_desc(d, n, c.dvals, nullptr, grid, c.stream));
     }
-    uint32_t *out3 = c.dvals + n;
-    LAMPI_CHECK(launch_sum_finish(c.dvals, n, c.dbuf, len, *pint, *plen, out3, c.stream));
-    uint32_t *h = (uint32_t *)c.pres;
-    LAMPI_CHECK(hipMemcpyAsync(h, out3, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c.stream));
+    uint32_t *out3 = (uint32_t *)c.pres_d;
+    LAMPI_CHECK(launch_sum_finish(c.dvals, n, st.base, len, *pint, *plen, out3, c.stream));
     LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    const volatile uint32_t *h = (const volatile uint32_t *)c.pres;
     *pint = h[1];
     *plen = h[2];
     return h[0];
 }
 
-// csum (64-bit words) of c.dbuf[0..len) with chaining state, computed on the GPU: every piece
-// is summed at its byte phase in the caller's word grid, the finish kernel adds them up and
-// forms the new trailing partial word.
-uint64_t device_sum64(HostCtx &c, uint64_t len, unsigned long *plong, unsigned long *plen) {
+// csum (64-bit words) of the staged bytes [0, len) with chaining state, computed on the GPU:
+// every piece is summed at its byte phase in the caller's word grid, the finish kernel adds them
+// up and forms the new trailing partial word.
+uint64_t device_sum64(HostCtx &c, const Staged &st, uint64_t len, unsigned long *plong, unsigned long *plen) {
     const uint64_t k = *plen >= 8 ? 0u : *plen;
     const uint64_t B = piece_size(len);
     const uint32_t n = (uint32_t)((len + B - 1) / B);
-        for (uint32_t i = 0; i < n; ++i) {
-        c.hdesc[i].addr = (uint64_t)(uintptr_t)(c.dbuf + (uint64_t)i * B);
+    for (uint32_t i = 0; i < n; ++i) {
+        c.hdesc[i].addr = (uint64_t)(uintptr_t)(st.base + (uint64_t)i * B);
         c.hdesc[i].length = (uint32_t)std::min<uint64_t>(B, len - (uint64_t)i * B);
         c.hdesc[i].partial = (uint32_t)((k + (uint64_t)i * B) & 7u);
     }
-    ensure(c.ddesc, c.desccap, std::max<uint32_t>(n, 1));
     ensure(c.dvals64, c.v64cap, (size_t)n + 3);
-    LAMPI_CHECK(hipMemcpyAsync(c.ddesc, c.hdesc, n * sizeof(lampi_frag_desc), hipMemcpyHostToDevice, c.stream));
-    LAMPI_CHECK(launch_sum64_desc(c.ddesc, n, c.dvals64, true, c.stream));
-    uint64_t *out3 = c.dvals64 + n;
-    LAMPI_CHECK(launch_sum64_finish(c.dvals64, n, c.dbuf, len, k ? (uint64_t)*plong : 0u, k, out3, c.stream));
-    uint64_t *h = c.pres;
-    LAMPI_CHECK(hipMemcpyAsync(h, out3, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, c.stream));
+    const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
+    LAMPI_CHECK(launch_sum64_desc(d, n, c.dvals64, true, c.stream));
+    uint64_t *out3 = c.pres_d;
+    LAMPI_CHECK(launch_sum64_finish(c.dvals64, n, st.base, len, k ? (uint64_t)*plong : 0u, k, out3, c.stream));
     LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    const volatile uint64_t *h = (const volatile uint64_t *)c.pres;
     *plong = (unsigned long)h[1];
     *plen = (unsigned long)h[2];
     return h[0];
@@ -294,7 +320,11 @@ unsigned long empty_sum64(unsigned long *plong, unsigned long *plen) {
 // host -> c.dbuf through the pinned bounce buffer: pieces of kBounceHalf bytes alternate between
 // its two halves; a half is refilled once its previous DMA has completed (event), so the CPU
 // copy of one piece overlaps the DMA of the other.
-void stage_in(HostCtx &c, const void *src, uint64_t len) {
+Staged stage_in(HostCtx &c, const void *src, uint64_t len) {
+    if (len <= kZeroCopy) {
+        std::memcpy(c.zpin, src, (size_t)len);
+        return {c.zpin_d, true};
+    }
     ensure(c.dbuf, c.dcap, (size_t)len);
     const uint8_t *s = (const uint8_t *)src;
     for (uint64_t off = 0, i = 0; off < len; off += kBounceHalf, ++i) {
@@ -305,11 +335,18 @@ void stage_in(HostCtx &c, const void *src, uint64_t len) {
         LAMPI_CHECK(hipMemcpyAsync(c.dbuf + off, half, n, hipMemcpyHostToDevice, c.stream));
         LAMPI_CHECK(hipEventRecord(c.half_free[i & 1], c.stream));
     }
+    return {c.dbuf, false};
 }
 
 // c.dbuf -> host through the bounce buffer: the DMA of piece i+1 runs while piece i is copied out
-void stage_out(HostCtx &c, void *dst, uint64_t len) {
+// the copy half of a host bcopy: the bytes the GPU checksummed, from the staging buffer they sit
+// in (the pinned buffer of a zero-copy call; c.dbuf, DMA'd back, otherwise)
+void stage_out(HostCtx &c, const Staged &st, void *dst, uint64_t len) {
     if (!len) return;
+    if (st.zero_copy) {
+        std::memcpy(dst, c.zpin, (size_t)len);
+        return;
+    }
     uint8_t *d = (uint8_t *)dst;
     const uint64_t np = (len + kBounceHalf - 1) / kBounceHalf;
     auto issue = [&](uint64_t i) {
@@ -347,8 +384,8 @@ extern "C" {
 unsigned int lampi_uicrc(const void *src, unsigned long crclen, unsigned int partial_crc) {
     if (crclen == 0) return partial_crc;  // no bytes: the register is unchanged
     HostCtx &c = host_ctx();
-    stage_in(c, src, crclen);
-    return device_crc(c, crclen, partial_crc);
+    const Staged st = stage_in(c, src, crclen);
+    return device_crc(c, st, crclen, partial_crc);
 }
 
 unsigned int lampi_bcopy_uicrc(const void *src, void *dst, unsigned long copylen, unsigned long crclen,
@@ -356,17 +393,17 @@ unsigned int lampi_bcopy_uicrc(const void *src, void *dst, unsigned long copylen
     const uint64_t n = std::max<uint64_t>(copylen, crclen);
     if (n == 0) return partial_crc;
     HostCtx &c = host_ctx();
-    stage_in(c, src, n);
-    const uint32_t r = device_crc(c, n, partial_crc);
-    stage_out(c, dst, copylen);
+    const Staged st = stage_in(c, src, n);
+    const uint32_t r = device_crc(c, st, n, partial_crc);
+    stage_out(c, st, dst, copylen);
     return r;
 }
 
 unsigned int lampi_uicsum(const void *src, unsigned long csumlen, unsigned int *pint, unsigned int *plen) {
     if (csumlen == 0) return empty_sum(pint, plen);
     HostCtx &c = host_ctx();
-    stage_in(c, src, csumlen);
-    return device_sum(c, csumlen, pint, plen);
+    const Staged st = stage_in(c, src, csumlen);
+    return device_sum(c, st, csumlen, pint, plen);
 }
 
 unsigned int lampi_bcopy_uicsum(const void *src, void *dst, unsigned long copylen, unsigned long csumlen,
@@ -374,17 +411,17 @@ unsigned int lampi_bcopy_uicsum(const void *src, void *dst, unsigned long copyle
     const uint64_t n = std::max<uint64_t>(copylen, csumlen);
     if (n == 0) return empty_sum(pint, plen);
     HostCtx &c = host_ctx();
-    stage_in(c, src, n);
-    const uint32_t r = device_sum(c, n, pint, plen);
-    stage_out(c, dst, copylen);
+    const Staged st = stage_in(c, src, n);
+    const uint32_t r = device_sum(c, st, n, pint, plen);
+    stage_out(c, st, dst, copylen);
     return r;
 }
 
 unsigned long lampi_csum(const void *src, unsigned long csumlen, unsigned long *plong, unsigned long *plen) {
     if (csumlen == 0) return empty_sum64(plong, plen);
     HostCtx &c = host_ctx();
-    stage_in(c, src, csumlen);
-    return device_sum64(c, csumlen, plong, plen);
+    const Staged st = stage_in(c, src, csumlen);
+    return device_sum64(c, st, csumlen, plong, plen);
 }
 
 unsigned long lampi_bcopy_csum(const void *src, void *dst, unsigned long copylen, unsigned long csumlen,
@@ -392,9 +429,9 @@ unsigned long lampi_bcopy_csum(const void *src, void *dst, unsigned long copylen
     const uint64_t n = std::max<uint64_t>(copylen, csumlen);
     if (n == 0) return empty_sum64(plong, plen);
     HostCtx &c = host_ctx();
-    stage_in(c, src, n);
-    const uint64_t r = device_sum64(c, n, plong, plen);
-    stage_out(c, dst, copylen);
+    const Staged st = stage_in(c, src, n);
+    const uint64_t r = device_sum64(c, st, n, plong, plen);
+    stage_out(c, st, dst, copylen);
     return r;
 }
 
