@@ -596,6 +596,19 @@ def run_mixed(args):
     else:  # SUM: total of the sums and the weighted sum
         got = (int(np.sum(vals, dtype=np.uint64) & 0xFFFFFFFF), got[1])
         want = (gold["sum_total"], gold["sum_wsum"])
+    # the north_star's one-wavefront-per-fragment schedule on the same batch, beside the product
+    pw_out = torch.empty_like(out)
+    for _ in range(args.warmup):
+        dv.frag_csum_batch_per_wave(descs, mode=mode, out=pw_out)
+    torch.cuda.synchronize()
+    pev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    pev[0].record(stream)
+    for i in range(args.steps):
+        dv.frag_csum_batch_per_wave(descs, mode=mode, out=pw_out)
+        pev[i + 1].record(stream)
+    torch.cuda.synchronize()
+    pw_s = sum(pev[i].elapsed_time(pev[i + 1]) for i in range(args.steps)) / args.steps / 1e3
+    pw_same = bool(torch.equal(pw_out, out))
     achieved = total / kern_avg_s / 1e9
     meta = total + 20 * lens.size  # + the 16-byte descriptor read and the 4-byte result write
     traffic = read_traffic("crc_configC") if mode == dv.CRC32 else None
@@ -610,16 +623,22 @@ def run_mixed(args):
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
                      "traffic_source": None if traffic is None else traffic.get("source"),
-                     "kernel": "crc_stream_kernel" if mode == dv.CRC32 else "sum_rows_kernel",
+                     "kernel": "crc_stream_kernel" if mode == dv.CRC32 else "crc_stream_kernel<kSum>",
                      "incl_metadata": {"bytes": meta, "achieved": round(meta / kern_avg_s / 1e9, 1),
                                        "frac": round(meta / kern_avg_s / 1e9 / HBM_PEAK_GBS, 4)},
                      "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                      "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2],
                                                                           max(kern_ms))],
                      "algorithmic_bytes_per_launch": total},
+        "one_wavefront_per_fragment": {"kernel": "crc_rows_kernel<DescSource>" if mode == dv.CRC32 else
+                                       "sum_rows_kernel<DescSource>",
+                                       "entry_point": "lampi_frag_csum_batch_per_wave",
+                                       "kernel_avg_ms": round(pw_s * 1e3, 4),
+                                       "frac": round(total / pw_s / 1e9 / HBM_PEAK_GBS, 4),
+                                       "same_checksums": pw_same},
         "parity": {"check": f"full digest vs tests/golden/fixtures.json (config C, {args.mode})",
                    ("xor" if mode == dv.CRC32 else "sum"): f"{got[0]:08x}", "wsum": f"{got[1]:08x}",
-                   "ok": got == want},
+                   "ok": got == want and pw_same},
         "cpu_baseline": None}))
 
 

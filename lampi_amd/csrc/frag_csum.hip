@@ -2591,6 +2591,22 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     return hipGetLastError();
 }
 
+// The north_star's one-wavefront-per-fragment schedule for descriptor batches (hard
+// part 3: reported beside the piece streams): crc_rows_kernel (a wave walks its fragments row by
+// row, one row prefetched) / sum_rows_kernel.
+hipError_t launch_desc_per_wave(const lampi_frag_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
+                                hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t fpw = pick_fpw(n, 1);
+    if (mode == LAMPI_CSUM_CRC32)
+        hipLaunchKernelGGL((crc_rows_kernel<DescSource>), grid_for(n, fpw), dim3(kBlock), 0, s, DescSource{d}, n, fpw,
+                           img, out);
+    else
+        hipLaunchKernelGGL(sum_rows_kernel<DescSource>, grid_for(n, fpw), dim3(kBlock), 0, s, DescSource{d}, n, fpw,
+                           out);
+    return hipGetLastError();
+}
+
 hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, size_t n,
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;

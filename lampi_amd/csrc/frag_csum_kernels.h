@@ -13,6 +13,9 @@ int crc_grid(int device);
 
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
                            hipStream_t s);
+// One wavefront per fragment (crc_rows_kernel / sum_rows_kernel), mode = lampi_csum_mode.
+hipError_t launch_desc_per_wave(const lampi_frag_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
+                                hipStream_t s);
 hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, size_t n,
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s);
 // Regular batch: frag_len % 4096 == 0, base 16-byte aligned, n full fragments.

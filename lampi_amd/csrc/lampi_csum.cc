@@ -459,6 +459,20 @@ int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_
     return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s));
 }
 
+int lampi_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode,
+                                   void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (n == 0) return 0;
+    if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_desc_per_wave(d_descs, n, d_out, mode, img, (hipStream_t)stream));
+}
+
 int lampi_frag_csum_batch_strided(const lampi_frag_desc *d_descs, size_t n, void *d_out, size_t out_stride, int mode,
                                   void *stream) {
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);

@@ -11,7 +11,7 @@ import torch
 
 from ._lib import CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
 
-__all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
+__all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
            "make_descs", "make_copy_descs", "as_u32", "chain_csum_batch", "header_csum_batch", "header_check_batch", "check_data_batch",
            "mask_bits", "make_recv_descs", "copy_to_app_batch"]
 
@@ -109,6 +109,21 @@ def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32
         raise ValueError("out is too small")
     check(lib().lampi_frag_csum_batch(descs.data_ptr(), count, out.data_ptr(), mode, _stream_handle(stream)),
           "lampi_frag_csum_batch")
+    return out
+
+
+def frag_csum_batch_per_wave(descs: torch.Tensor, n: int | None = None, mode: int = CRC32,
+                             out: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """lampi_frag_csum_batch on the one-wavefront-per-fragment schedule (same results)."""
+    _require_cuda(descs, "descs")
+    count = descs.numel() * descs.element_size() // 16 if n is None else int(n)
+    if out is None:
+        out = torch.empty(count, dtype=torch.int32, device=descs.device)
+    _require_cuda(out, "out")
+    if out.numel() < count:
+        raise ValueError("out is too small")
+    check(lib().lampi_frag_csum_batch_per_wave(descs.data_ptr(), count, out.data_ptr(), mode, _stream_handle(stream)),
+          "lampi_frag_csum_batch_per_wave")
     return out
 
 

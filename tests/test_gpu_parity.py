@@ -108,10 +108,11 @@ def test_descriptor_batch_edges_and_alignment(cuda, oracle, mode):
     parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
     parts[::3] = 0xFFFFFFFF
     descs = dv.make_descs(base, offs, lens, parts)
-    got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
     want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
-    bad = np.nonzero(got != want)[0]
-    assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+    for fn in (dv.frag_csum_batch, dv.frag_csum_batch_per_wave):  # piece streams / one wave per fragment
+        got = dv.as_u32(fn(descs, mode=mode))
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (fn.__name__, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
 
 
 def test_descriptor_batch_random(cuda, oracle):
@@ -165,10 +166,11 @@ def test_descriptor_batch_fragments_across_chains(cuda, oracle, case, mode):
     host = base.cpu().numpy()
     parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
     descs = dv.make_descs(base, offs, lens, parts)
-    got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
     want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
-    bad = np.nonzero(got != want)[0]
-    assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+    for fn in (dv.frag_csum_batch, dv.frag_csum_batch_per_wave):  # piece streams / one wave per fragment
+        got = dv.as_u32(fn(descs, mode=mode))
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (fn.__name__, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
 
 
 def test_descriptor_batch_maximum_length(cuda):
@@ -407,6 +409,9 @@ def test_config_c_mixed_sizes_full_digest(cuda, oracle):
     assert digest(crc) == (gold["crc_xor"], gold["crc_wsum"])
     s = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.SUM32))
     assert (int(np.sum(s, dtype=np.uint64) & 0xFFFFFFFF), digest(s)[1]) == (gold["sum_total"], gold["sum_wsum"])
+    # the one-wavefront-per-fragment schedule on the same batch (bench.py --config C reports both)
+    assert np.array_equal(dv.as_u32(dv.frag_csum_batch_per_wave(descs, mode=dv.CRC32)), crc)
+    assert np.array_equal(dv.as_u32(dv.frag_csum_batch_per_wave(descs, mode=dv.SUM32)), s)
     del buf
     torch.cuda.empty_cache()
 

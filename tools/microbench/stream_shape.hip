@@ -123,6 +123,31 @@ int main(int argc, char **argv) {
     }
     add("CONTIG 4wg/cu(40K lds)", 155, 0, true);
     add("SUB 4wg/cu(40K lds)", 155, 2, true);
+    // other workgroup shapes at the same rows per chain: 512 threads (8 chains) with 53 KiB
+    // (3 per CU) or 77 KiB (2 per CU); 256 threads (4 chains) with 77 KiB (2 per CU) or 26 KiB
+    auto add2 = [&](std::string nm, int nw, int ldsk, int R, int S) {
+        vs.push_back({nm + " R=" + std::to_string(R) + " S=" + std::to_string(S), [=] {
+                          const unsigned g = (unsigned)((nrows + R - 1) / R);
+                          if (nw == 8 && ldsk == 53)
+                              hipLaunchKernelGGL((rd_stream<8, 53000>), dim3(g), dim3(512), 0, 0, s, nrows, R, S, sink);
+                          else if (nw == 8)
+                              hipLaunchKernelGGL((rd_stream<8, 79000>), dim3(g), dim3(512), 0, 0, s, nrows, R, S, sink);
+                          else if (nw == 4 && ldsk == 77)
+                              hipLaunchKernelGGL((rd_stream<4, 79000>), dim3(g), dim3(256), 0, 0, s, nrows, R, S, sink);
+                          else if (nw == 4)
+                              hipLaunchKernelGGL((rd_stream<4, 26000>), dim3(g), dim3(256), 0, 0, s, nrows, R, S, sink);
+                          else
+                              hipLaunchKernelGGL((rd_stream<16, 100000>), dim3(g), dim3(1024), 0, 0, s, nrows, R, S, sink);
+                      }});
+    };
+    add2("512thr 3wg/cu(53K)", 8, 53, 104, 0);
+    add2("512thr 3wg/cu(53K)", 8, 53, 104, 2);
+    add2("512thr 2wg/cu(77K)", 8, 77, 104, 0);
+    add2("256thr 2wg/cu(77K)", 4, 77, 52, 0);
+    add2("256thr 2wg/cu(77K)", 4, 77, 52, 1);
+    add2("256thr 6wg/cu(26K)", 4, 26, 52, 0);
+    add2("256thr 6wg/cu(26K)", 4, 26, 52, 1);
+    add2("1024thr 1wg/cu(100K)", 16, 100, 208, 0);
     for (auto &v : vs) v.f();
     CK(hipGetLastError());
     CK(hipDeviceSynchronize());
