@@ -43,13 +43,10 @@ constexpr size_t kImgHorner16Cols = kImgCombine16Cols + 2048;
 //   [kImgPow2Cols, +1024)    shift by 2^b bytes, b = 0..31, NORMAL domain: word b*32 + c = column c
 //                            (chained checksums: crc(s, A || B) = shift_|B|(crc(s, A)) ^ crc(0, B))
 constexpr size_t kImgPow2Cols = kImgHorner16Cols + 32;
-//   [kImgZero, +16)          zeros: the row loads of crc_frags_kernel read chunks wholly outside a
+//   [kImgZero, +16)          zeros: the row loads of crc_stream_kernel read chunks wholly outside a
 //                            fragment from here
 constexpr size_t kImgZero = kImgPow2Cols + 1024;
 constexpr size_t kImgWords = kImgZero + 16;
-// The device allocation of the image is followed by kImgTrashBytes of writable scratch: lanes of
-// the fused copy with nothing to store write their 16 bytes there (per-lane slots, never read).
-constexpr size_t kImgTrashBytes = 1024;
 constexpr int kChunkBytes = 16;                          // coalesced layout: 16-byte chunks
 constexpr int kChunkStep = kRowBytes / 4 - kChunkBytes;  // 1008 zero bytes between a lane's chunks
 

@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <cstdint>
+#include <cstdlib>
 
 #include "crc_const.h"
 #include "crc_tables.h"
@@ -568,6 +569,38 @@ __device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *ds
     }
 }
 
+// The reverse: a row loaded coalesced (lane l holds the 16-byte chunks at 16l + 1024q) into the
+// lane-contiguous pieces the CRC runs on (lane l: bytes [64l, 64l + 64)), through the wave's 1 KiB
+// staging area one quarter row at a time (every lane writes its chunk of quarter q, the 16 lanes
+// whose pieces lie in it read them back).  One wave's LDS operations complete in order: no barrier.
+__device__ __forceinline__ void rows_to_pieces(uint32_t *stage, uint32_t d[16], int lane) {
+    u32x4 *st = (u32x4 *)stage;
+    uint32_t e[16];
+#pragma unroll
+    for (int w = 0; w < 16; ++w) e[w] = 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        st[lane] = u32x4{d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]};
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        if ((lane >> 4) == q) {
+            const int b = (lane & 15) * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const u32x4 v = st[b + k];
+                e[4 * k + 0] = v.x;
+                e[4 * k + 1] = v.y;
+                e[4 * k + 2] = v.z;
+                e[4 * k + 3] = v.w;
+            }
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int w = 0; w < 16; ++w) d[w] = e[w];
+}
+
 // d[15] of lane - 1 (lane 0 gets `carry`, the last lane's word of the previous row)
 __device__ __forceinline__ uint32_t prev_lane_top(uint32_t d15, uint32_t carry, int lane) {
     const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((lane - 1) * 4, (int)d15);
@@ -755,13 +788,36 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
         return n;
     };
 
+    // Copy sources load every row that starts inside its fragment (r > 0, or an unpadded frame)
+    // coalesced -- lane l takes the 16 bytes at 16l + 1024q, one 1 KiB run per instruction, also
+    // from sources that are not 16-byte aligned (unaligned dwordx4; a GM slot payload sits 72 bytes
+    // in) -- stores it to a dword-aligned destination straight from those registers and hands the
+    // CRC the lane-contiguous pieces through the wave's staging area (rows_to_pieces).  The other
+    // rows (a padded frame's first) keep the lane-contiguous masked loads.
+    auto coal_row = [&](const RowGeom &gg, uint32_t rr) -> bool { return Src::kCopy && (rr > 0 || gg.P == 0); };
+    auto load_row = [&](const FragInfo &fi, const RowGeom &gg, uint32_t rr, uint32_t(&dd)[16]) {
+        if (coal_row(gg, rr)) {
+            gbyte *p = fi.addr + ((long long)rr * kRowBytes - (long long)gg.P) + 16 * lane;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const u32x4 v = *(gu32x4_a1 *)(p + 1024 * q);
+                dd[4 * q + 0] = v.x;
+                dd[4 * q + 1] = v.y;
+                dd[4 * q + 2] = v.z;
+                dd[4 * q + 3] = v.w;
+            }
+        } else {
+            crc_load_row(fi, gg, rr, lane, dd);
+        }
+    };
+
     FragInfo cur;
     size_t f = next_nonempty(f0, cur);
     if (f >= n) return;
     RowGeom g = crc_geom(cur);
     uint32_t r = 0;
     uint32_t d[16];
-    crc_load_row(cur, g, 0, lane, d);
+    load_row(cur, g, 0, d);
     uint32_t C = 0;
     uint32_t carry = 0;
 
@@ -778,10 +834,23 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
         }
         const bool more = nf < n;
         uint32_t nd[16];
-        if (more) crc_load_row(nfi, ng, nr, lane, nd);
+        if (more) load_row(nfi, ng, nr, nd);
 
         if constexpr (Src::kCopy) {  // copy before the partial register is injected
-            if (cur.copylen) {
+            bool stored = false;
+            if (coal_row(g, r)) {
+                const long long row0 = (long long)r * kRowBytes - (long long)g.P;  // >= 0
+                if (cur.copylen && row0 + kRowBytes <= (long long)cur.copylen &&
+                    (((uintptr_t)cur.dst + (uint64_t)row0) & 3u) == 0) {
+                    gwbyte *q = (gwbyte *)(cur.dst + row0) + 16 * lane;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        *(gwu32x4_a4 *)(q + 1024 * c) = u32x4{d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]};
+                    stored = true;
+                }
+                rows_to_pieces(lds + (kLdsBytes + (threadIdx.x >> 6) * kArea) / 4, d, lane);
+            }
+            if (cur.copylen && !stored) {
                 const long long o = (long long)r * kRowBytes + lane * kLaneBytes - (long long)g.P;
                 const uint32_t dm = (uint32_t)((uintptr_t)cur.dst - g.P) & 15u;
                 const long long row0 = (long long)r * kRowBytes - (long long)g.P;
@@ -1067,27 +1136,15 @@ struct RowsN4 {
     RowN<4> r[K];
 };
 
-// kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way
-// kPB: piece bytes (64; 16 for the fused copy, whose rows are then 1 KiB and every load and store
-// instruction of a wave covers 1 KiB).  kCopy (SUM, 16-byte pieces, 4-byte-aligned dst; a source
-// that is not 16-byte aligned takes the two-load funnel variant):
-// each lane stores its piece to dst + 16k with one asm store per row (lanes with nothing to store
-// write a per-lane trash slot, so the ring's waits count loads and stores exactly); a piece that
-// ends past copylen is stored byte by byte in addition (compiler stores: they only make the waits
-// stricter).
-struct StreamCopy {
-    uint64_t dst;
-    uint32_t copylen, pad;
-};
-
-template <bool kMis, int kD, int kAbl, int kK, bool kSum, int kPB = 64, bool kCopy = false>
+// kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way.
+// (Round 1 also ran the SUM fused copy on 16-byte-piece streams here; round 2 moved it to
+// sum_rows_kernel, which measured faster on every layout: launch_sum_copy.)
+template <bool kMis, int kD, int kAbl, int kK, bool kSum>
 __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDesc *sdesc, const uint64_t *sstart,
                                             const uint16_t *sj, uint32_t *marks, const StreamChain *sch,
                                             uint32_t *sopen, uint32_t *shead, gbyte *zero, uint32_t *sres,
-                                            uint32_t *__restrict__ out, const StreamCopy *scopy = nullptr,
-                                            uint8_t *trash = nullptr) {
-    static_assert(kPB == 64 || (kPB == 16 && kSum && kK == 1), "16-byte pieces: SUM, one chain per wave");
-    static_assert(!kCopy || kPB == 16, "the fused copy runs on 16-byte pieces");
+                                            uint32_t *__restrict__ out) {
+    constexpr int kPB = 64;  // piece bytes
     constexpr int NL = kMis ? kPB / 16 + 1 : kPB / 16;  // loads per row
     constexpr int kW = kPB / 4;                          // words per piece
     const uint32_t lane = threadIdx.x & 63u;
@@ -1105,8 +1162,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         uint32_t fix;         // bit 0: a first piece needs byte masking, bit 1: partial injected as data,
                               // bit 2: null row
         uint32_t one;         // one-segment rows: list entry | output index << 16
-        gwbyte *dst;          // kCopy: where the lane's piece goes (the trash slot when nothing)
-        uint32_t ncp;         // kCopy: bytes of the piece to copy (0..16)
     };
     SChain cs[kK];
     uint32_t head[kK], mid[kK];
@@ -1133,10 +1188,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             t.M = 0ull;
             t.fix = 4u;
             t.one = 0u;
-            if constexpr (kCopy) {
-                t.dst = (gwbyte *)(trash + 16u * lane);
-                t.ncp = 0u;
-            }
 #pragma unroll
             for (int q = 0; q < NL; ++q) A.p[q] = zero;
             return A;
@@ -1177,13 +1228,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             const long long o0 = (long long)k0 * kPB - (long long)P;
             gbyte *pa = (gbyte *)(uintptr_t)addr + o0 + lane * (uint32_t)kPB;
             uint32_t sh = 0u;
-            if constexpr (kCopy) {
-                const StreamCopy cp = scopy[lr];
-                const uint64_t ob = (uint64_t)k0 * kPB + lane * (uint32_t)kPB;
-                const uint32_t cl = uniform(cp.copylen);
-                t.ncp = ob < cl ? (uint32_t)min<uint64_t>(cl - ob, 16u) : 0u;
-                t.dst = (gwbyte *)(uintptr_t)(uniform64(cp.dst) + ob);
-            }
             if constexpr (!kMis && kSum) {  // chunks past the fragment end read zeros
                 const long long o = o0 + (long long)lane * kPB;
 #pragma unroll
@@ -1233,12 +1277,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         const long long o = (long long)k * kPB - (long long)P;
         gbyte *pa = (gbyte *)(uintptr_t)D.addr + o;
         uint32_t sh = 0u;
-        if constexpr (kCopy) {
-            const StreamCopy cp = scopy[lr];
-            const uint64_t ob = (uint64_t)k * kPB;
-            t.ncp = (!nul && ob < cp.copylen) ? (uint32_t)min<uint64_t>(cp.copylen - ob, 16u) : 0u;
-            t.dst = nul ? (gwbyte *)(trash + 16u * lane) : (gwbyte *)(uintptr_t)(cp.dst + ob);
-        }
         if constexpr (!kMis && kSum) {
 #pragma unroll
             for (int q = 0; q < kPB / 16; ++q) A.p[q] = (!nul && o + 16 * q < (long long)D.len) ? pa + 16 * q : zero;
@@ -1395,18 +1433,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         uint32_t d[kK][kW], C[kK];
 #pragma unroll
         for (int c = 0; c < kK; ++c) prepare(raw[c], t[c], d[c]);
-        if constexpr (kCopy) {  // the piece to dst (the trash slot unless all 16 bytes are copied)
-            // (prepare masked only bytes past the fragment end, which are never copied)
-            gwbyte *sa = t[0].ncp == 16u ? t[0].dst : (gwbyte *)(trash + 16u * lane);
-            const u32x4 v = u32x4{d[0][0], d[0][1], d[0][2], d[0][3]};
-            asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(sa), "v"(v) : "memory");
-            if (t[0].ncp != 0u && t[0].ncp < 16u) {  // a piece ending past copylen: its first ncp bytes
-                const uint32_t w[4] = {d[0][0], d[0][1], d[0][2], d[0][3]};
-#pragma unroll
-                for (uint32_t b = 0; b < 15; ++b)  // constant indices: a dynamic w[] index would go to scratch
-                    if (b < t[0].ncp) t[0].dst[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3u)));
-            }
-        }
 #pragma unroll
         for (int c = 0; c < kK; ++c) {
             C[c] = t[c].sreg;
@@ -1434,26 +1460,15 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 #pragma unroll
         for (int c = 0; c < kK; ++c) finish(c, t[c], v[c], carry[c]);
     };
-    bool first_pass = true;
     auto wait_slot = [&](RowN<NL> (&r)[kK], auto S) {
-        constexpr int kS = decltype(S)::value;
-        if constexpr (kCopy) {
-            // vmcnt counts loads and stores in issue order: younger than slot S's loads are
-            // (kD - 1) loads and, after the first pass, kD - 1 stores (one per step; S on the first)
-            constexpr int A = (kD - 1) * NL + kS, B = (kD - 1) * (NL + 1);
-            if constexpr (NL == 1)
-                wait_sel<A, B, B>(first_pass ? 0u : 1u, r[0].q[0]);
-            else
-                wait_sel<A, B, B>(first_pass ? 0u : 1u, r[0].q[0], r[0].q[1]);
-        } else if constexpr (kK == 2) {
+        (void)S;
+        if constexpr (kK == 2) {
             wait_rows2<(kD - 1) * 2 * NL>(r[0], r[1]);
         } else if constexpr (NL == 4) {
             asm volatile("s_waitcnt vmcnt(%4) ; lampi-wait %0 %1 %2 %3"
                          : "+v"(r[0].q[0]), "+v"(r[0].q[1]), "+v"(r[0].q[2]), "+v"(r[0].q[3])
                          : "n"((kD - 1) * NL)
                          : "memory");
-        } else if constexpr (NL == 1) {
-            asm volatile("s_waitcnt vmcnt(%1) ; lampi-wait %0" : "+v"(r[0].q[0]) : "n"((kD - 1) * NL) : "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(%5) ; lampi-wait %0 %1 %2 %3 %4"
                          : "+v"(r[0].q[0]), "+v"(r[0].q[1]), "+v"(r[0].q[2]), "+v"(r[0].q[3]), "+v"(r[0].q[4])
@@ -1483,7 +1498,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
         LAMPI_STREAM_STEP(5)
         LAMPI_STREAM_STEP(6)
         LAMPI_STREAM_STEP(7)
-        first_pass = false;
     }
 #undef LAMPI_STREAM_STEP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the rows in flight before exit
@@ -1496,15 +1510,11 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 // kAbl (tools/microbench/frags_ablation.hip only): 1 = loads and task walk, no row work;
 // 2 = everything but the table lookups of the pieces.  kK: chains per wave, kWv: waves per
 // workgroup (kWv * kK chains); kWaveCap > 0 asks the compiler for that many waves per SIMD.
-// kPB / kCopy: see stream_body (the fused copy: SUM, 16-byte pieces; a workgroup with a fragment
-// whose dst is not 4-byte (dword) aligned does nothing -- sum_rows_kernel<..., kSkipFast> takes
-// those; dword-aligned dwordx4 stores run at the aligned rate).  trash: 1 KiB of device memory the copy's masked lanes store to.
-template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0,
-          int kPB = 64, bool kCopy = false>
+template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kWaveCap > 0 ? kWaveCap : 1)))
-crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out,
-                  uint8_t *trash) {
-    static_assert(Src::kCopy == kCopy, "copy sources run the fused-copy variant");
+crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
+    static_assert(!Src::kCopy, "fused copies run crc_rows_kernel / sum_rows_kernel");
+    constexpr int kPB = 64;  // piece bytes
     constexpr uint32_t kThreads = 64 * kWv;
     constexpr uint32_t kChains = kWv * kK;
     static_assert(kThreads >= kFragsPerWg, "one fragment per thread in the set-up");
@@ -1516,7 +1526,6 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     __shared__ StreamChain schain[kChains];
     __shared__ uint32_t chead[kChains], sopen[kChains], shead[kChains];
     __shared__ uint32_t sres[kFragsPerWg];        // the workgroup's checksums, stored at the end
-    __shared__ StreamCopy scopy[kCopy ? kFragsPerWg + 1 : 1];
     __shared__ uint64_t wpieces[kWv];
     __shared__ uint32_t wcount[kWv];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, t = threadIdx.x;
@@ -1525,12 +1534,6 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
 
     FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
     if (t < nwg) mine = src.get(base + t);
-    if constexpr (kCopy) {  // fast path only: 4-byte-aligned destinations throughout the workgroup
-        // (a piece's dwordx4 store is then dword-aligned: dst + 16k at dst % 16 = 4, 8, 12 --
-        // the GM send side's slots after a 72-byte header -- runs at the aligned rate)
-        const bool slow = t < nwg && mine.len != 0u && (((uintptr_t)mine.dst) & 3u) != 0u;
-        if (__syncthreads_or(slow)) return;
-    }
     if (t < kChains) chead[t] = 0u;
     auto nopre = [] {};
     if constexpr (kSum) {
@@ -1589,7 +1592,6 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
         sdesc[li] = StreamDesc{(uint64_t)(uintptr_t)mine.addr, mine.len, mine.partial};
         sstart[li] = ex;
         sj[li] = (uint16_t)t;
-        if constexpr (kCopy) scopy[li] = StreamCopy{(uint64_t)(uintptr_t)mine.dst, mine.copylen, 0u};
 #pragma unroll
         for (uint32_t c = 0; c < kChains; ++c) {
             const uint64_t pc = 64u * ((c * R) / kChains);
@@ -1617,23 +1619,12 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     for (uint32_t i = t; i < kChains * 64; i += kThreads) marks[i] = 0u;
     const bool anymis = __syncthreads_or(mis) != 0;
     gbyte *zero = (gbyte *)(img + kImgZero);
-    if constexpr (kPB == 64) {
-        if (anymis)  // five loads per row: a one-slot ring keeps its registers within the aligned variant's
-            stream_body<true, 1, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
-                                                 sopen + kK * wave, shead + kK * wave, zero, sres, out);
-        else
-            stream_body<false, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
-                                                   sopen + kK * wave, shead + kK * wave, zero, sres, out);
-    } else if (anymis) {  // sources not 16-byte aligned: two loads per piece, funnel-shifted (a
-        // two-slot ring keeps the registers within the budget: four slots spilled)
-        stream_body<true, 2, kAbl, kK, kSum, kPB, kCopy>(lds, sdesc, sstart, sj, marks + 64 * kK * wave,
-                                                          schain + kK * wave, sopen + kK * wave, shead + kK * wave,
-                                                          zero, sres, out, scopy, trash);
-    } else {
-        stream_body<false, kD, kAbl, kK, kSum, kPB, kCopy>(lds, sdesc, sstart, sj, marks + 64 * kK * wave,
-                                                           schain + kK * wave, sopen + kK * wave, shead + kK * wave,
-                                                           zero, sres, out, scopy, trash);
-    }
+    if (anymis)  // five loads per row: a one-slot ring keeps its registers within the aligned variant's
+        stream_body<true, 1, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+                                             sopen + kK * wave, shead + kK * wave, zero, sres, out);
+    else
+        stream_body<false, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+                                               sopen + kK * wave, shead + kK * wave, zero, sres, out);
     if (kAbl != 0) return;
     __syncthreads();
     // stream_join: fragments crossing chain starts.  Thread c owns the fragment crossing chain c's
@@ -2001,92 +1992,168 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 // MemFunctions.cc:142-516, 913-1071).  Phase (kPhase sources) is taken mod the word size.
 // kSkipFast (copy sources): the workgroup does nothing when every fragment of its 4*fpw has a
 // 4-byte-aligned dst -- crc_stream_kernel's fused copy took those (same partition).
-template <class Src, class Acc = uint32_t, bool kSkipFast = false>
-__global__ void __launch_bounds__(kBlock) sum_rows_kernel(Src src, size_t n, uint32_t fpw, Acc *__restrict__ out) {
+template <class Src, class Acc = uint32_t, bool kSkipFast = false, int kWv = kWaves>
+__global__ void __launch_bounds__(64 * kWv) sum_rows_kernel(Src src, size_t n, uint32_t fpw, Acc *__restrict__ out) {
     const int lane = threadIdx.x & 63;
-    __shared__ __attribute__((aligned(16))) uint32_t stage[Src::kCopy ? kWaves * 1024 / 4 : 1];  // per-wave copy staging
+    __shared__ __attribute__((aligned(16))) uint32_t stage[Src::kCopy ? kWv * 1024 / 4 : 1];  // per-wave copy staging
     if constexpr (kSkipFast) {
-        const size_t g = (size_t)blockIdx.x * kWaves * fpw + threadIdx.x;
+        const size_t g = (size_t)blockIdx.x * kWv * fpw + threadIdx.x;
         bool slow = false;
-        if (threadIdx.x < kWaves * fpw && g < n) {
+        if (threadIdx.x < kWv * fpw && g < n) {
             const FragInfo fi = src.get(g);
             slow = fi.len != 0u && (((uintptr_t)fi.dst) & 3u) != 0u;
         }
         if (!__syncthreads_or(slow)) return;
     }
-    const size_t f0 = wg_first(fpw);
-    const size_t fend = f0 + (size_t)kWaves * fpw;
-    for (size_t f = f0; f < n && f < fend; f += kWaves) {
-        FragInfo fi = src.get(f);
-        fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
-        fi.len = uniform(fi.len);
-        if constexpr (Src::kCopy) {
-            fi.dst = (uint8_t *)uniform64((uint64_t)(uintptr_t)fi.dst);
-            fi.copylen = uniform(fi.copylen);
-        }
-        // byte phase of the first byte in the word grid (chained pieces); the frame starts
-        // `ph` bytes early and those bytes read as zero
-        const uint32_t ph = Src::kPhase ? (uniform(fi.partial) & (uint32_t)(sizeof(Acc) - 1)) : 0u;
-        gbyte *fb = fi.addr - ph;
-        const uint32_t span = fi.len + ph;
-        const uint32_t R = (uint32_t)(((uint64_t)fi.len + ph + (kRowBytes - 1)) / kRowBytes);
-        const uint32_t s16 = (uint32_t)((uintptr_t)fb & 15u);
-        uint8_t *db = fi.dst - ph;
-        const uint32_t dm = (uint32_t)((uintptr_t)db & 15u);
-        Acc acc = 0;
-        uint32_t carry = 0;
-        for (uint32_t r = 0; r < R; ++r) {
-            const long long o = (long long)r * kRowBytes + lane * kLaneBytes;
-            // rows wholly inside the fragment load unmasked (also when misaligned: load64's
-            // unaligned path); edge rows read only the aligned chunks that hold fragment bytes
-            const bool mask = (r == 0 && ph != 0) || (r + 1 == R && span % kRowBytes != 0);
-            uint32_t d[16];
-            load64(fb, o, ph, (long long)span, mask, s16, d);
+    const size_t f0 = uniform(blockIdx.x * kWv * fpw + (threadIdx.x >> 6));
+    const size_t fend = f0 + (size_t)kWv * fpw;  // exclusive, stride kWv
+    uint32_t *area = stage + (threadIdx.x >> 6) * (1024 / 4);
+
+    // a fragment's frame: `ph` = the byte phase of its first byte in the word grid (chained
+    // pieces); the frame starts ph bytes early and those bytes read as zero
+    struct Frame {
+        FragInfo fi;
+        gbyte *fb;
+        uint8_t *db;
+        uint32_t ph, span, R, s16, dm;
+    };
+    auto open = [&](size_t x, Frame &t) -> size_t {  // next non-empty fragment (empty ones: 0)
+        for (; x < n && x < fend; x += kWv) {
+            FragInfo fi = src.get(x);
+            fi.addr = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
+            fi.len = uniform(fi.len);
             if constexpr (Src::kCopy) {
-                if (fi.copylen) {
-                    // whole rows inside the copy: staged 1 KiB-coalesced stores at the dword-aligned
-                    // db + row0 - m (as in crc_rows_kernel); edge rows: word/byte stores
-                    const long long row0 = (long long)r * kRowBytes, lo = ph, hi = (long long)fi.copylen + ph;
-                    const uint32_t m = dm & 3u;
-                    const uint32_t prev = m ? prev_lane_top(d[15], carry, lane) : 0u;
-                    if (row0 >= lo && row0 + kRowBytes <= hi) {
-                        uint32_t *area = stage + (threadIdx.x >> 6) * (1024 / 4);
-                        if (m == 0) {
-                            store_row_coalesced<1024>(area, db + row0, d, lane);
-                        } else {
-                            const uint32_t sh = 4u - m;
-                            uint32_t v[16];
-                            v[0] = __builtin_amdgcn_alignbyte(d[0], prev, sh);
+                fi.dst = (uint8_t *)uniform64((uint64_t)(uintptr_t)fi.dst);
+                fi.copylen = uniform(fi.copylen);
+            }
+            if (fi.len) {
+                t.fi = fi;
+                t.ph = Src::kPhase ? (uniform(fi.partial) & (uint32_t)(sizeof(Acc) - 1)) : 0u;
+                t.fb = fi.addr - t.ph;
+                t.span = fi.len + t.ph;
+                t.R = (uint32_t)(((uint64_t)fi.len + t.ph + (kRowBytes - 1)) / kRowBytes);
+                t.s16 = (uint32_t)((uintptr_t)t.fb & 15u);
+                t.db = fi.dst - t.ph;
+                t.dm = (uint32_t)((uintptr_t)t.db & 15u);
+                return x;
+            }
+            if (lane == 0) emit(src, out, x, (Acc)0, fi);
+        }
+        return n;
+    };
+    // interior rows load coalesced (16 bytes at 16l + 1024q, one 1 KiB run per instruction,
+    // unaligned sources included): every chunk starts on the fragment's word grid and the sum is
+    // order-free, so only a copy to a destination that is not dword aligned needs the lane-contiguous
+    // pieces (rows_to_pieces).  Edge rows (a phase in front, a partial last row) load lane-contiguous
+    // and masked.  Returns whether the row was loaded coalesced.
+    auto load = [&](const Frame &t, uint32_t r, uint32_t(&d)[16]) -> bool {
+        const bool mask = (r == 0 && t.ph != 0) || (r + 1 == t.R && t.span % kRowBytes != 0);
+        if (mask) {
+            load64(t.fb, (long long)r * kRowBytes + lane * kLaneBytes, t.ph, (long long)t.span, true, t.s16, d);
+            return false;
+        }
+        gbyte *p = t.fb + (uint64_t)r * kRowBytes + 16 * lane;
 #pragma unroll
-                            for (int w = 1; w < 16; ++w) v[w] = __builtin_amdgcn_alignbyte(d[w], d[w - 1], sh);
-                            const bool skip0 = row0 < lo + 4;
-                            store_row_coalesced<1024>(area, db + row0 - m, v, lane, skip0);
-                            if (skip0 && lane == 0) store_word(db, row0 - (long long)m, v[0], lo, hi);
-                            if (lane == 63 && r + 1 == R)
-                                store_word(db, row0 - (long long)m + kRowBytes, __builtin_amdgcn_alignbyte(0u, d[15], sh),
-                                           lo, hi);
-                        }
-                    } else {
-                        store64(db, o, d, ph, hi, m, dm == 0, prev, lane == 63 && r + 1 == R);
-                    }
-                    carry = __builtin_amdgcn_readlane(d[15], 63);
+        for (int q = 0; q < 4; ++q) {
+            const u32x4 v = *(gu32x4_a1 *)(p + 1024 * q);
+            d[4 * q + 0] = v.x;
+            d[4 * q + 1] = v.y;
+            d[4 * q + 2] = v.z;
+            d[4 * q + 3] = v.w;
+        }
+        return true;
+    };
+
+    Frame cur;
+    size_t f = open(f0, cur);
+    if (f >= n) return;
+    uint32_t r = 0;
+    uint32_t d[16];
+    bool coal = load(cur, 0, d);
+    Acc acc = 0;
+    uint32_t carry = 0;
+    for (;;) {
+        // prefetch the next row (of this fragment, or the first of the wave's next one)
+        Frame nt = cur;
+        size_t nf = f;
+        uint32_t nr = r + 1;
+        if (nr >= cur.R) {
+            nf = open(f + kWv, nt);
+            nr = 0;
+        }
+        const bool more = nf < n;
+        uint32_t nd[16];
+        bool ncoal = false;
+        if (more) ncoal = load(nt, nr, nd);
+
+        if constexpr (Src::kCopy) {
+            const FragInfo &fi = cur.fi;
+            const long long row0 = (long long)r * kRowBytes, lo = cur.ph, hi = (long long)fi.copylen + cur.ph;
+            bool stored = false;
+            if (coal && fi.copylen) {
+                if (row0 >= lo && row0 + kRowBytes <= hi && (cur.dm & 3u) == 0) {
+                    gwbyte *q = (gwbyte *)(cur.db + row0) + 16 * lane;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        *(gwu32x4_a4 *)(q + 1024 * c) = u32x4{d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]};
+                    stored = true;
+                } else {
+                    rows_to_pieces(area, d, lane);
                 }
             }
-            if constexpr (sizeof(Acc) == 4) {
+            if (fi.copylen && !stored) {
+                // whole rows inside the copy: staged 1 KiB-coalesced stores at the dword-aligned
+                // db + row0 - m (as in crc_rows_kernel); edge rows: word/byte stores
+                const long long o = row0 + lane * kLaneBytes;
+                const uint32_t m = cur.dm & 3u;
+                if (r == 0) carry = 0;
+                const uint32_t prev = m ? prev_lane_top(d[15], carry, lane) : 0u;
+                if (row0 >= lo && row0 + kRowBytes <= hi) {
+                    if (m == 0) {
+                        store_row_coalesced<1024>(area, cur.db + row0, d, lane);
+                    } else {
+                        const uint32_t sh = 4u - m;
+                        uint32_t v[16];
+                        v[0] = __builtin_amdgcn_alignbyte(d[0], prev, sh);
 #pragma unroll
-                for (int w = 0; w < 16; ++w) acc += d[w];
-            } else {  // 64-bit words: the frame is 8-byte aligned to the fragment's word grid
-#pragma unroll
-                for (int w = 0; w < 16; w += 2) acc += (uint64_t)d[w] | ((uint64_t)d[w + 1] << 32);
+                        for (int w = 1; w < 16; ++w) v[w] = __builtin_amdgcn_alignbyte(d[w], d[w - 1], sh);
+                        const bool skip0 = row0 < lo + 4;
+                        store_row_coalesced<1024>(area, cur.db + row0 - m, v, lane, skip0);
+                        if (skip0 && lane == 0) store_word(cur.db, row0 - (long long)m, v[0], lo, hi);
+                        if (lane == 63 && r + 1 == cur.R)
+                            store_word(cur.db, row0 - (long long)m + kRowBytes, __builtin_amdgcn_alignbyte(0u, d[15], sh),
+                                       lo, hi);
+                    }
+                } else {
+                    store64(cur.db, o, d, cur.ph, hi, m, cur.dm == 0, prev, lane == 63 && r + 1 == cur.R);
+                }
+                carry = __builtin_amdgcn_readlane(d[15], 63);
             }
         }
         if constexpr (sizeof(Acc) == 4) {
-            acc = wave_add(acc);
-        } else {
 #pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+            for (int w = 0; w < 16; ++w) acc += d[w];
+        } else {  // 64-bit words: the frame is 8-byte aligned to the fragment's word grid
+#pragma unroll
+            for (int w = 0; w < 16; w += 2) acc += (uint64_t)d[w] | ((uint64_t)d[w + 1] << 32);
         }
-        if (lane == 0) emit(src, out, f, acc, fi);
+        if (r + 1 == cur.R) {
+            if constexpr (sizeof(Acc) == 4) {
+                acc = wave_add(acc);
+            } else {
+#pragma unroll
+                for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+            }
+            if (lane == 0) emit(src, out, f, acc, cur.fi);
+            acc = 0;
+        }
+        if (!more) break;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) d[w] = nd[w];
+        coal = ncoal;
+        cur = nt;
+        f = nf;
+        r = nr;
     }
 }
 
@@ -2575,7 +2642,6 @@ static uint32_t frags_per_wg(size_t n) {
 
 // crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_ablation.hip)
 constexpr int kStreamD = 2, kStreamK = 1, kStreamWv = 12, kStreamCap = 6;
-constexpr int kCopyD = 4;  // fused copy: 1 KiB rows, three in flight per wave (6 slots spilled at 80 VGPRs)
 
 static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg - 1) / fpg)); }
 
@@ -2587,7 +2653,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg,
-                       img, out, nullptr);
+                       img, out);
     return hipGetLastError();
 }
 
@@ -2613,7 +2679,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
-                       MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out, nullptr);
+                       MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
     return hipGetLastError();
 }
 
@@ -2671,40 +2737,30 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
     return hipGetLastError();
 }
 
-// Fused-copy SUM launches pair crc_stream_kernel (workgroups whose destinations are all 4-byte
-// aligned) with sum_rows_kernel<..., kSkipFast> (the others) over the SAME partition: fpg fragments
-// per crc_stream_kernel workgroup = kWaves * fpw fragments per sum_rows_kernel workgroup.  One
-// helper picks fpg for every such pair, so the two kernels can never split a batch differently.
-static uint32_t bcopy_frags_per_wg(size_t n) {
-    uint32_t fpg = 96;
-    while (fpg > 4 && n / fpg < 2048) fpg = fpg > 12 ? fpg / 2 : 4;
-    return fpg;
-}
-static_assert(96 % kWaves == 0 && 48 % kWaves == 0 && 24 % kWaves == 0 && 12 % kWaves == 0 && 4 % kWaves == 0,
-              "every fpg bcopy_frags_per_wg can return is a multiple of kWaves");
-
-// SUM: crc_stream_kernel's fused copy (16-byte pieces, coalesced loads and stores) for workgroups
-// whose fragments all have 4-byte-aligned destinations, then sum_rows_kernel for the others.
-// img must be an allocation of the table image followed by kImgTrashBytes of device memory
-// (device_tables()).
+// Fused-copy SUM (bcopy_uicsum, LA-MPI's default mode): sum_rows_kernel in 8-wave workgroups, one
+// fragment per wave with the next row prefetched, interior rows loaded and (to dword-aligned
+// destinations) stored coalesced straight from registers.  Measured against the previous pair
+// (crc_stream_kernel's 16-byte-piece streams for workgroups with dword-aligned destinations +
+// sum_rows_kernel for the rest) on one box, 4M x 4 KiB (profiles/r02_sum_copy_ab.txt): descriptors
+// 68.4 -> 70.0%, sources at +8 68.5 -> 69.8%, destinations at +8 66.2 -> 68.2%, at +1 62.8 -> 68.0%,
+// the receive step in GM slots 65.0 -> 68.4% of read + write.
 template <class Src>
-static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, const uint32_t *img, hipStream_t s) {
-    const uint32_t fpg = bcopy_frags_per_wg(n);
-    uint8_t *trash = (uint8_t *)(uintptr_t)(img + kImgWords);
-    hipLaunchKernelGGL((crc_stream_kernel<Src, kCopyD, 0, 1, true, kStreamWv, kStreamCap, 16, true>), frags_grid(n, fpg),
-                       dim3(64 * kStreamWv), 0, s, src, n, fpg, img, out, trash);
-    hipLaunchKernelGGL((sum_rows_kernel<Src, uint32_t, true>), frags_grid(n, fpg), dim3(kBlock), 0, s, src, n,
-                       fpg / kWaves, out);
+static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t s) {
+    constexpr int kWv = 8;
+    const uint32_t fpw = std::max(1u, pick_fpw(n, 1) / 2);  // the 4-wave schedule's span per workgroup
+    hipLaunchKernelGGL((sum_rows_kernel<Src, uint32_t, false, kWv>), dim3((unsigned)((n + (size_t)kWv * fpw - 1) /
+                                                                                      ((size_t)kWv * fpw))),
+                       dim3(64 * kWv), 0, s, src, n, fpw, out);
 }
 
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                              hipStream_t s) {
     if (n == 0) return hipSuccess;
-    if (!img) return hipErrorInvalidValue;  // the tables (CRC) / zero chunk and trash slots (SUM)
+    if (!img) return hipErrorInvalidValue;  // the tables (CRC)
     if (mode == LAMPI_CSUM_CRC32)
         launch_crc_rows_copy(CopySource{d}, n, 1, img, out, s);
     else
-        launch_sum_copy(CopySource{d}, n, out, img, s);
+        launch_sum_copy(CopySource{d}, n, out, s);
     return hipGetLastError();
 }
 
@@ -2720,7 +2776,7 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
     if (crc)
         launch_crc_rows_copy(src, n, 1, img, csum, s);
     else
-        launch_sum_copy(src, n, csum, img, s);
+        launch_sum_copy(src, n, csum, s);
     return hipGetLastError();
 }
 
@@ -2749,7 +2805,7 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     if (img) {  // piece streams (img: the zero chunk)
         const uint32_t fpg = frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, true, kStreamWv, kStreamCap>),
-                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
+                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
@@ -2768,7 +2824,7 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (img) {
         const uint32_t fpg = frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, true, kStreamWv, kStreamCap>),
-                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out, nullptr);
+                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
@@ -2794,10 +2850,8 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                            base, (uint32_t)n, frag_len, out, dst, dst_stride);
         return hipGetLastError();
     }
-    // ragged or unaligned: the fused-copy piece streams as for descriptor batches (4-byte-aligned
-    // destinations), sum_rows_kernel for the workgroups with byte-misaligned ones
-    if (!img) return hipErrorInvalidValue;
-    launch_sum_copy(MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, out, img, s);
+    // ragged or unaligned: the fused copy of descriptor batches
+    launch_sum_copy(MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, out, s);
     return hipGetLastError();
 }
 

@@ -50,7 +50,7 @@ hipError_t device_tables(int dev, const uint32_t **out) {
     std::call_once(t.once, [&] {
         const std::vector<uint32_t> &h = host_image();
         uint32_t *p = nullptr;
-        t.err = hipMalloc(&p, h.size() * sizeof(uint32_t) + kImgTrashBytes);  // + the copy's trash slots
+        t.err = hipMalloc(&p, h.size() * sizeof(uint32_t));
         if (t.err == hipSuccess) t.err = hipMemcpy(p, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
         if (t.err == hipSuccess) t.img = p;
     });
@@ -497,7 +497,7 @@ int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d
     int dev = 0;
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
-    const uint32_t *img = nullptr;  // both modes: SUM's fused copy reads its zero chunk and trash slots
+    const uint32_t *img = nullptr;  // CRC: the tables
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
     return to_int(launch_bcopy_desc(d_descs, n, d_out, mode, img, (hipStream_t)stream));
@@ -513,7 +513,7 @@ int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void
     int dev = 0;
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
-    const uint32_t *img = nullptr;  // CRC: the tables; SUM: the zero chunk and trash slots of the streams
+    const uint32_t *img = nullptr;  // CRC: the tables
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
     return to_int(launch_copy_to_app(d_descs, n, (const uint8_t *)d_expected, expected_stride, d_copied, d_csum, d_mask,
@@ -552,7 +552,7 @@ int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_
     int dev = 0;
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
-    const uint32_t *img = nullptr;  // CRC: the tables; SUM: the zero chunk and trash slots of the streams
+    const uint32_t *img = nullptr;  // CRC: the tables
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
     return to_int(launch_msg_bcopy((const uint8_t *)d_msg, msg_len, frag_len, partial, (uint8_t *)d_dst, dst_stride, n,
