@@ -12,22 +12,25 @@ import torch  # noqa: E402
 
 from lampi_amd import device as dv  # noqa: E402
 
-L, n, stride, off = 4096, 1 << 20, 4096 + 80, 72
-msg = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-dv.fill_stream(msg, seed=13)
-dst = torch.zeros(off + n * stride, dtype=torch.uint8, device="cuda")
-out = torch.empty(n, dtype=torch.int32, device="cuda")
-for mode, name in ((dv.CRC32, "crc"), (dv.SUM32, "sum")):
-    run = lambda: dv.msg_bcopy(msg, L, dst[off:], stride, mode=mode, out=out)  # noqa: E731
-    for _ in range(5):
-        run()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(20):
-        run()
-    e1.record()
-    torch.cuda.synchronize()
-    s = e0.elapsed_time(e1) / 20 / 1e3
-    ok = torch.equal(dst[off:off + n * stride].view(n, stride)[:, :L], msg.view(n, L))
-    print(f"{name}: {2 * n * L / s / 1e9:.1f} GB/s = {2 * n * L / s / 8e12:.3f} of 8 TB/s, copy ok {ok}")
+for L, n, stride, off in ((4096, 1 << 20, 4096 + 80, 72),   # 4 KiB payloads in 4,176-byte slots
+                          (65456, 1 << 14, 65536, 72)):      # GM's own: 65,456-byte payloads in 64 KiB slots
+    msg = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    dv.fill_stream(msg, seed=13)
+    dst = torch.zeros(off + n * stride, dtype=torch.uint8, device="cuda")
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    for mode, name in ((dv.CRC32, "crc"), (dv.SUM32, "sum")):
+        run = lambda: dv.msg_bcopy(msg, L, dst[off:], stride, mode=mode, out=out)  # noqa: E731
+        for _ in range(5):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        s = e0.elapsed_time(e1) / 20 / 1e3
+        ok = torch.equal(dst[off:off + n * stride].view(n, stride)[:, :L], msg.view(n, L))
+        print(f"L={L} slot={stride} {name}: {2 * n * L / s / 1e9:.1f} GB/s = {2 * n * L / s / 8e12:.3f} of 8 TB/s, "
+              f"copy ok {ok}", flush=True)
+    del msg, dst, out
