@@ -569,6 +569,39 @@ __device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *ds
     }
 }
 
+// A row only partly inside the copy [lo, hi) (offsets relative to dst; the row's byte 0 at row0,
+// dst + row0 dword-aligned): the same 1 KiB-coalesced staging as store_row_coalesced; a lane's
+// 16-byte chunk goes out whole when it lies inside, word by word (store_word: whole words, bytes
+// at an edge) when it straddles an edge, not at all outside.  Edge rows written lane by lane with
+// dword stores (16 instructions touching 64 lines each) ran GM's 65,456-byte slot copies at
+// about 51% of read + write.
+__device__ __forceinline__ void store_row_coalesced_masked(uint32_t *stage, uint8_t *dst, long long row0,
+                                                           const uint32_t d[16], int lane, long long lo, long long hi) {
+    u32x4 *st = (u32x4 *)stage;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        if (lane / 16 == h) {
+            const int b = (lane % 16) * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) st[b + q] = u32x4{d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]};
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        const u32x4 v = st[lane];
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const long long c = row0 + h * 1024 + 16 * lane;
+        if (c >= lo && c + 16 <= hi) {
+            *(gwu32x4_a4 *)(dst + c) = v;
+        } else if (c + 16 > lo && c < hi) {
+            store_word(dst, c, v.x, lo, hi);
+            store_word(dst, c + 4, v.y, lo, hi);
+            store_word(dst, c + 8, v.z, lo, hi);
+            store_word(dst, c + 12, v.w, lo, hi);
+        }
+    }
+}
+
 // The reverse: a row loaded coalesced (lane l holds the 16-byte chunks at 16l + 1024q) into the
 // lane-contiguous pieces the CRC runs on (lane l: bytes [64l, 64l + 64)), through the wave's 1 KiB
 // staging area one quarter row at a time (every lane writes its chunk of quarter q, the 16 lanes
@@ -876,10 +909,12 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                     if (lane == 63 && r + 1 == g.R)
                         store_word(cur.dst, row0 - (long long)m + kRowBytes, __builtin_amdgcn_alignbyte(0u, d[15], sh), 0,
                                    (long long)cur.copylen);
+                } else if ((dm & 3u) == 0) {
+                    store_row_coalesced_masked(area, cur.dst, row0, d, lane, 0, (long long)cur.copylen);
                 } else {
                     if (r == 0) carry = 0;
-                    const uint32_t prev = (dm & 3u) ? prev_lane_top(d[15], carry, lane) : 0u;
-                    store64(cur.dst, o, d, 0, (long long)cur.copylen, dm & 3u, dm == 0, prev,
+                    const uint32_t prev = prev_lane_top(d[15], carry, lane);
+                    store64(cur.dst, o, d, 0, (long long)cur.copylen, dm & 3u, false, prev,
                             lane == 63 && r + 1 == g.R);
                 }
                 carry = __builtin_amdgcn_readlane(d[15], 63);
@@ -2124,8 +2159,10 @@ __global__ void __launch_bounds__(64 * kWv) sum_rows_kernel(Src src, size_t n, u
                             store_word(cur.db, row0 - (long long)m + kRowBytes, __builtin_amdgcn_alignbyte(0u, d[15], sh),
                                        lo, hi);
                     }
+                } else if (m == 0) {
+                    store_row_coalesced_masked(area, cur.db, row0, d, lane, lo, hi);
                 } else {
-                    store64(cur.db, o, d, cur.ph, hi, m, cur.dm == 0, prev, lane == 63 && r + 1 == cur.R);
+                    store64(cur.db, o, d, cur.ph, hi, m, false, prev, lane == 63 && r + 1 == cur.R);
                 }
                 carry = __builtin_amdgcn_readlane(d[15], 63);
             }
