@@ -99,7 +99,7 @@ def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC3
 
 def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
                     stream: torch.cuda.Stream | None = None) -> torch.Tensor:
-    """out[i] = checksum of fragment descs[i]; one wavefront per fragment."""
+    """out[i] = checksum of fragment descs[i] (piece streams: fragments of any size share rows)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 16 if n is None else int(n)
     if out is None:

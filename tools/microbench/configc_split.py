@@ -2,7 +2,7 @@
 batch and on its size classes alone (fragments < 4 KiB / >= 4 KiB, and < 1 KiB / >= 16 KiB),
 same buffer and descriptors.  Prints each subset's bytes, kernel time and fraction of 8 TB/s.
 
-python tools/microbench/configc_split.py
+python tools/microbench/configc_split.py [--quick]   (--quick: the whole batch and the prologue only)
 """
 import os
 import sys
@@ -36,14 +36,21 @@ def timed(descs, n, reps=30):
     return e0.elapsed_time(e1) / reps / 1e3
 
 
-for name, sel in (("all", np.ones(lens.size, bool)), ("<4KiB", lens < 4096), (">=4KiB", lens >= 4096),
-                  ("<1KiB", lens < 1024), (">=16KiB", lens >= 16384)):
+QUICK = "--quick" in sys.argv
+for name, sel in (("all", np.ones(lens.size, bool)),) + (() if QUICK else (
+        ("<4KiB", lens < 4096), (">=4KiB", lens >= 4096), ("<1KiB", lens < 1024), (">=16KiB", lens >= 16384))):
     idx = np.nonzero(sel)[0]
     d = dv.make_descs(buf, offs[idx], lens[idx])
     b = int(lens[idx].sum(dtype=np.uint64))
     t = timed(d, idx.size)
     print(f"{name:8s} {idx.size:7d} fragments {b / 2**30:6.3f} GiB  {t * 1e3:7.3f} ms  "
           f"{b / t / 8e12:.3f} of 8 TB/s", flush=True)
+
+if QUICK:
+    zl = np.zeros(lens.size, dtype=lens.dtype)
+    t = timed(dv.make_descs(buf, offs, zl), lens.size)
+    print(f"empty fragments: {t * 1e3:7.3f} ms", flush=True)
+    sys.exit(0)
 
 # the two size classes at once, on two streams (the small fragments' latency-bound work
 # overlapping the large fragments' streaming)
