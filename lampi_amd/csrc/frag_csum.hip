@@ -298,8 +298,8 @@ __device__ __forceinline__ void store_row(gwbyte *p, const Row &r) {
 // memory wait.  Only the per-lane combine tables come from the basis image (64 lanes x 32
 // columns, 8 KiB, L2-resident): two dwordx4 loads per thread, issued before anything else so
 // their latency overlaps the rows the workgroup issues next (`pre`) and the constant builds.
-// kParts (diagnostics only, tools/microbench/crc_ablation.hip): bit 0 slicing, bit 1 combine,
-// bit 2 Horner tables; the product always builds all three.
+// kParts: bit 0 slicing, bit 1 combine, bit 2 Horner tables (the piece streams need no Horner
+// tables).
 constexpr cx::SliceBasis kSliceBasis = cx::slice_basis();
 constexpr cx::Mat kHornerMat = cx::swapped(cx::shift(kRowBytes - kLaneBytes));  // 4032 bytes
 constexpr cx::Mat kHorner16Mat = cx::swapped(cx::shift(kChunkStep));           // 1008 bytes
@@ -1174,7 +1174,7 @@ struct RowsN4 {
 // kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way.
 // (Round 1 also ran the SUM fused copy on 16-byte-piece streams here; round 2 moved it to
 // sum_rows_kernel, which measured faster on every layout: launch_sum_copy.)
-template <bool kMis, int kD, int kAbl, int kK, bool kSum>
+template <bool kMis, int kD, int kK, bool kSum>
 __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDesc *sdesc, const uint64_t *sstart,
                                             const uint16_t *sj, uint32_t *marks, const StreamChain *sch,
                                             uint32_t *sopen, uint32_t *shead, gbyte *zero, uint32_t *sres,
@@ -1457,14 +1457,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     for (int c = 0; c < kK; ++c) carry[c] = 0u;
     uint32_t step = 0u;
     auto process = [&](RowN<NL> (&raw)[kK], const STask (&t)[kK]) {
-        if constexpr (kAbl == 1) {  // keep the loaded data and the tasks live, nothing else
-            uint32_t x = t[0].info ^ t[kK - 1].sreg ^ (uint32_t)t[0].M ^ t[kK - 1].fix;
-#pragma unroll
-            for (int q = 0; q < NL; ++q) x ^= raw[0].q[q].x ^ raw[kK - 1].q[q].w;
-            carry[0] ^= x;
-            if (carry[0] == 0x9E3779B9u && lane == 64u) out[0] = carry[kK - 1];
-            return;
-        }
         uint32_t d[kK][kW], C[kK];
 #pragma unroll
         for (int c = 0; c < kK; ++c) prepare(raw[c], t[c], d[c]);
@@ -1478,11 +1470,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
             for (int c = 0; c < kK; ++c)
 #pragma unroll
                 for (int w = 0; w < kW; w += 2) C[c] = C[c] + d[c][w] + d[c][w + 1];
-        } else if constexpr (kAbl == 2) {
-#pragma unroll
-            for (int c = 0; c < kK; ++c)
-#pragma unroll
-                for (int w = 0; w < 16; ++w) C[c] ^= d[c][w];
         } else if constexpr (kK == 2) {
             crc_piece2(lds, kl, C[0], d[0], C[1], d[1]);
         } else {
@@ -1542,10 +1529,11 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     }
 }
 
-// kAbl (tools/microbench/frags_ablation.hip only): 1 = loads and task walk, no row work;
-// 2 = everything but the table lookups of the pieces.  kK: chains per wave, kWv: waves per
-// workgroup (kWv * kK chains); kWaveCap > 0 asks the compiler for that many waves per SIMD.
-template <class Src, int kD = 3, int kAbl = 0, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0>
+// kK: chains per wave, kWv: waves per workgroup (kWv * kK chains); kWaveCap > 0 asks the
+// compiler for that many waves per SIMD.  (Round 1's ablated variants -- loads and task walk
+// only, no piece lookups -- ran as a template switch here until commit d95cfff:
+// profiles/r01_stream_ablation.txt.)
+template <class Src, int kD = 3, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kWaveCap > 0 ? kWaveCap : 1)))
 crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
     static_assert(!Src::kCopy, "fused copies run crc_rows_kernel / sum_rows_kernel");
@@ -1655,12 +1643,11 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     const bool anymis = __syncthreads_or(mis) != 0;
     gbyte *zero = (gbyte *)(img + kImgZero);
     if (anymis)  // five loads per row: a one-slot ring keeps its registers within the aligned variant's
-        stream_body<true, 1, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+        stream_body<true, 1, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                              sopen + kK * wave, shead + kK * wave, zero, sres, out);
     else
-        stream_body<false, kD, kAbl, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+        stream_body<false, kD, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                                sopen + kK * wave, shead + kK * wave, zero, sres, out);
-    if (kAbl != 0) return;
     __syncthreads();
     // stream_join: fragments crossing chain starts.  Thread c owns the fragment crossing chain c's
     // start when that is the first chain start inside it; the part before is chain c-1's open
@@ -1818,8 +1805,8 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
     }
 }
 
-// kAblate (tools/microbench/crc_ablation.hip only; the product launches 0):
-//   1 = loads only (words XOR-folded, no table lookups), 2 = lookups only (no global loads)
+// (Round 1's ablated variants -- loads only, lookups only -- ran as a template switch here until
+// commit d95cfff: profiles/r01_ablation.txt.)
 // kCopy: fused bcopy -- each row is also stored to dst + f*dst_stride (dst and dst_stride 4-byte
 // aligned: asm global_store_dwordx4 at dword-aligned addresses, launch_msg_bcopy's gate) as soon
 // as it arrives; per step the ring then carries 4K stores beside 4K loads, and the waits count
@@ -1833,7 +1820,7 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // kernel keeps the two-workgroups-per-CU occupancy the schedule was measured at).
 // kWv: waves per workgroup (the table builders use the first 256 threads); kCap > 0 asks the
 // compiler for that many waves per SIMD.
-template <int kAblate, int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
+template <int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
           bool kSum = false, int kWv = kWaves, int kCap = 0>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kCap > 0 ? kCap : 1)))
 crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, size_t frag_len, uint32_t partial,
@@ -1885,17 +1872,15 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     if constexpr (kSum) {
         issue_all();
         asm volatile("" ::"v"(lds) : "memory");  // the LDS array escapes: it stays allocated
-    } else if (kAblate != 2 && kWv == kWaves) {
+    } else if (kWv == kWaves) {
         // every ring slot is in flight while the workgroup builds its tables
         stage_tables<4 * K * D, decltype(issue_all), 7, kCoal>(lds, img, issue_all);
-    } else if (kAblate != 2) {
+    } else {
         if (threadIdx.x < 64 * kWaves)
             stage_tables<4 * K * D, decltype(issue_all), 7, kCoal, false>(lds, img, issue_all);
         else
             issue_all();
         lds_barrier();
-    } else {
-        stage_tables<0>(lds, img, [] {});
     }
     if (nfr == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1934,21 +1919,6 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
             }
             return;
         }
-        if (kAblate == 1) {
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                uint32_t y = C[c];
-#pragma unroll
-                for (int w = 0; w < 16; ++w) y ^= row_word(b.x[c], w);
-                C[c] = y;
-            }
-            if (t.r + 1 == R && lane == 0) {
-#pragma unroll
-                for (int c = 0; c < K; ++c)
-                    if (K * t.i + c < nfr) out[frag(t.i, c)] = C[c];
-            }
-            return;
-        }
         if constexpr (kCoal) {
             crc_chunks<K>(lds, k, C, b, t.r == 0, (lane == 0) ? vinit : 0u);
         } else {
@@ -1974,19 +1944,6 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
             }
         }
     };
-    if (kAblate == 2) {  // same lookups on register data, no HBM traffic
-        RowsK<K> &A = ring[0];
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-            for (int w = 0; w < 4; ++w) A.x[c].q[w] = u32x4{lane_off + w + 7u * c, lane_off ^ 0x5A5Au, 7u * w, f0 + c};
-        for (GroupTask u = t[0];; u = advance(u)) {
-            process(A, u);
-#pragma unroll
-            for (int c = 0; c < K; ++c) A.x[c].q[0].x ^= C[c];
-            if (is_last(u)) break;
-        }
-        return;
-    }
     // steady state: slot S is waited for, checksummed (and stored) and refilled with the task
     // after the most recently issued one.  vmcnt counts loads and stores in issue order: the
     // operations younger than slot S's loads are (D-1)*kL loads, plus with kCopy the stores
@@ -2664,7 +2621,7 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
     hipLaunchKernelGGL((crc_rows_kernel<Src, kWv>), grid, dim3(64 * kWv), 0, s, src, n, fpw, img, out);
 }
 
-// fragments per workgroup of crc_stream_kernel: 96 (measured: tools/microbench/frags_ablation.hip,
+// fragments per workgroup of crc_stream_kernel: 96 (measured: tools/microbench/frags_sweep.hip,
 // 12-wave workgroups -- 96 beat 64/128/192/256 on config C and on 4 KiB descriptors: shorter
 // workgroups shrink the end-of-kernel tail, and 96 uniform 4 KiB fragments are 8 rows per chain),
 // halved for small batches until they give one workgroup per CU (a 16 MiB chunk of 65,456-byte
@@ -2677,7 +2634,7 @@ static uint32_t frags_per_wg(size_t n) {
     return fpg;
 }
 
-// crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_ablation.hip)
+// crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_sweep.hip)
 constexpr int kStreamD = 2, kStreamK = 1, kStreamWv = 12, kStreamCap = 6;
 
 static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg - 1) / fpg)); }
@@ -2689,7 +2646,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg,
+    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg,
                        img, out);
     return hipGetLastError();
 }
@@ -2715,7 +2672,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     (void)grid;
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
+    hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
                        MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
     return hipGetLastError();
 }
@@ -2744,7 +2701,7 @@ static hipError_t launch_regular(const uint8_t *base, size_t n, size_t frag_len,
     if (frag_len == (size_t)kRowBytes && n >= (size_t)kV) {
         const size_t nv = n / kV;
         const uint32_t fpw = pick_regular_fpw(nv, kV * frag_len);
-        hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains, false, false, 3, kV, kSum>), grid_for(nv, fpw),
+        hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, kV, kSum>), grid_for(nv, fpw),
                            dim3(kBlock), 0, s, base, (uint32_t)nv, fpw, kV * frag_len, partial, img, out, nullptr,
                            (size_t)0);
         done = nv * kV;
@@ -2752,7 +2709,7 @@ static hipError_t launch_regular(const uint8_t *base, size_t n, size_t frag_len,
     }
     const size_t m = n - done;  // fragment-order schedule (and the last n % kV fragments of a 4 KiB batch)
     const uint32_t fpw = pick_regular_fpw(m, frag_len);
-    hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains, false, false, 3, 1, kSum>), grid_for(m, fpw),
+    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 1, kSum>), grid_for(m, fpw),
                        dim3(kBlock), 0, s, base + done * frag_len, (uint32_t)m, fpw, frag_len, partial, img, out + done,
                        nullptr, (size_t)0);
     return hipGetLastError();
@@ -2769,7 +2726,7 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
     if (n == 0) return hipSuccess;
     if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
     const uint32_t fpw = pick_fpw(n, (uint32_t)(frag_len / kRowBytes));
-    hipLaunchKernelGGL((crc_regular_kernel<0, kRegularChains, true>), grid_for(n, fpw), dim3(kBlock), 0, s, base,
+    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, true>), grid_for(n, fpw), dim3(kBlock), 0, s, base,
                        (uint32_t)n, fpw, frag_len, partial, img, out, dst, dst_stride);
     return hipGetLastError();
 }
@@ -2841,7 +2798,7 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     if (n == 0) return hipSuccess;
     if (img) {  // piece streams (img: the zero chunk)
         const uint32_t fpg = frags_per_wg(n);
-        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, 0, kStreamK, true, kStreamWv, kStreamCap>),
+        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, true, kStreamWv, kStreamCap>),
                            frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out);
         return hipGetLastError();
     }
@@ -2860,7 +2817,7 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     }
     if (img) {
         const uint32_t fpg = frags_per_wg(n);
-        hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, 0, kStreamK, true, kStreamWv, kStreamCap>),
+        hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, true, kStreamWv, kStreamCap>),
                            frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
         return hipGetLastError();
     }

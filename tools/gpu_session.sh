@@ -55,7 +55,7 @@ for step in "$@"; do
     tests_chain) run pytest_chain 600 python -m pytest tests/test_gpu_chain.py -m gpu -x -q ;;
     tests_csum64) run pytest_csum64 600 python -m pytest tests/test_gpu_csum64.py -m gpu -x -q ;;
     tests_verify) run pytest_verify 600 python -m pytest tests/test_gpu_verify.py -m gpu -x -q ;;
-    ablation) run ablation 500 tools/microbench/crc_ablation ;;
+    sweep) run sweep 500 tools/microbench/frags_sweep ;;
     microbench) run microbench 300 tools/microbench/readbw ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -43,7 +43,7 @@ static Cfg make_copy(uint32_t L, uint32_t fpw) {
     c.fpw = fpw;
     c.go = [](const uint8_t *buf, uint32_t n, uint32_t fpw, uint32_t L, const uint32_t *img, uint32_t *out) {
         const dim3 grid((n + kWaves * fpw - 1) / (kWaves * fpw));
-        hipLaunchKernelGGL((crc_regular_kernel<0, K, true, true, D, 1, kSum>), grid, dim3(kBlock), 0, 0, buf, n, fpw,
+        hipLaunchKernelGGL((crc_regular_kernel<K, true, true, D, 1, kSum>), grid, dim3(kBlock), 0, 0, buf, n, fpw,
                            (size_t)L, 0xFFFFFFFFu, img, out, g_dst, (size_t)L);
     };
     return c;
@@ -60,7 +60,7 @@ static Cfg make(uint32_t L, uint32_t fpw) {
     c.go = [](const uint8_t *buf, uint32_t n, uint32_t fpw, uint32_t L, const uint32_t *img, uint32_t *out) {
         const uint32_t nv = n / V;  // V > 1: the rows of V*4096-byte virtual fragments are 4 KiB fragments
         const dim3 grid((nv + kWaves * fpw - 1) / (kWaves * fpw));
-        hipLaunchKernelGGL((crc_regular_kernel<0, K, false, false, D, V>), grid, dim3(kBlock), 0, 0, buf, nv, fpw,
+        hipLaunchKernelGGL((crc_regular_kernel<K, false, false, D, V>), grid, dim3(kBlock), 0, 0, buf, nv, fpw,
                            (size_t)L * V, 0xFFFFFFFFu, img, out, nullptr, (size_t)0);
     };
     return c;

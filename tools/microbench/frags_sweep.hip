@@ -1,10 +1,11 @@
-// frags_ablation.hip -- crc_stream_kernel (the general-fragment product kernel) on config C
+// frags_sweep.hip -- crc_stream_kernel (the general-fragment product kernel) on config C
 // (659,114 Zipf-sized fragments, 4 GiB) and on 4M x 4 KiB descriptors (config B through
-// descriptors): ablated variants (loads + task walk only; no table lookups), ring depth, chains
-// per wave, fragments per workgroup and the occupancy sweep; the regular kernel on the uniform
-// batch for comparison.  Checksums of the product variant are compared with the regular
-// kernel's on the uniform batch.
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 frags_ablation.hip -o frags_ablation
+// descriptors): ring depth, chains per wave, fragments per workgroup and the occupancy sweep;
+// the regular kernel on the uniform batch for comparison.  Checksums of the product variant are
+// compared with the regular kernel's on the uniform batch.  (Until commit d95cfff this was
+// frags_ablation.hip and also ran ablated kernel variants -- loads + task walk only, no table
+// lookups -- through a template switch of the product kernel: profiles/r01_stream_ablation.txt.)
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 frags_sweep.hip -o frags_sweep
 #include "../../lampi_amd/csrc/crc_tables.cc"
 #include "../../lampi_amd/csrc/frag_csum.hip"
 
@@ -54,18 +55,18 @@ static std::vector<uint32_t> zipf_lengths(uint64_t min_total) {  // SURVEY.md 8(
     return out;
 }
 
-template <int kAbl, int kD = 2, int kK = 1, int kWv = 12, int kCap = 6>
+template <int kD = 2, int kK = 1, int kWv = 12, int kCap = 6>
 static void launch_stream(const lampi_frag_desc *d, size_t n, const uint32_t *img, uint32_t *out, uint32_t fpg = 0,
                           size_t pad_lds = 0) {
     if (fpg == 0) fpg = frags_per_wg(n);
-    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kD, kAbl, kK, false, kWv, kCap>), frags_grid(n, fpg),
+    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kD, kK, false, kWv, kCap>), frags_grid(n, fpg),
                        dim3(64 * kWv), pad_lds, 0, DescSource{d}, n, fpg, img, out);
 }
 
 template <int kD, int kK, int kWv, int kCap>
 static int stream_vgprs() {
     hipFuncAttributes a;
-    CK(hipFuncGetAttributes(&a, (const void *)crc_stream_kernel<DescSource, kD, 0, kK, false, kWv, kCap>));
+    CK(hipFuncGetAttributes(&a, (const void *)crc_stream_kernel<DescSource, kD, kK, false, kWv, kCap>));
     return a.numRegs;
 }
 
@@ -141,15 +142,13 @@ int main() {
         struct V {
             const char *name;
             std::function<void()> go;
-        } vs[] = {{"product (12 waves/WG, fpg 96)", [&] { launch_stream<0>(d, n, dimg, out); }},
-                  {"no lookups", [&] { launch_stream<2>(d, n, dimg, out); }},
-                  {"loads + tasks", [&] { launch_stream<1>(d, n, dimg, out); }},
-                  {"12 waves/WG fpg 256", [&] { launch_stream<0>(d, n, dimg, out, 256); }},
-                  {"12 waves/WG fpg 128", [&] { launch_stream<0>(d, n, dimg, out, 128); }},
-                  {"12 waves/WG fpg 48", [&] { launch_stream<0>(d, n, dimg, out, 48); }},
-                  {"8 waves/WG K1 kD2 fpg 96", [&] { launch_stream<0, 2, 1, 8, 0>(d, n, dimg, out, 96); }},
-                  {"8 waves/WG K1 kD2 fpg 256", [&] { launch_stream<0, 2, 1, 8, 0>(d, n, dimg, out, 256); }},
-                  {"4 waves/WG K2 kD2", [&] { launch_stream<0, 2, 2, 4, 0>(d, n, dimg, out); }}};
+        } vs[] = {{"product (12 waves/WG, fpg 96)", [&] { launch_stream<>(d, n, dimg, out); }},
+                  {"12 waves/WG fpg 256", [&] { launch_stream<>(d, n, dimg, out, 256); }},
+                  {"12 waves/WG fpg 128", [&] { launch_stream<>(d, n, dimg, out, 128); }},
+                  {"12 waves/WG fpg 48", [&] { launch_stream<>(d, n, dimg, out, 48); }},
+                  {"8 waves/WG K1 kD2 fpg 96", [&] { launch_stream<2, 1, 8, 0>(d, n, dimg, out, 96); }},
+                  {"8 waves/WG K1 kD2 fpg 256", [&] { launch_stream<2, 1, 8, 0>(d, n, dimg, out, 256); }},
+                  {"4 waves/WG K2 kD2", [&] { launch_stream<2, 2, 4, 0>(d, n, dimg, out); }}};
         // three interleaved rounds, back-to-back launches (as bench.py times them): run-to-run clock
         // and box drift are larger than most differences measured here
         const size_t nv = sizeof(vs) / sizeof(vs[0]);
@@ -170,12 +169,12 @@ int main() {
             int waves;
             const char *how;
             std::function<void()> go;
-        } occ[] = {{4, "K2, 4 waves/WG, 1 WG/CU", [&] { launch_stream<0, 2, 2, 4, 0>(d, n, dimg, out, 0, 16u << 10); }},
-                   {8, "K2, 4 waves/WG, 2 WG/CU", [&] { launch_stream<0, 2, 2, 4, 0>(d, n, dimg, out); }},
-                   {8, "K1, 8 waves/WG, 1 WG/CU", [&] { launch_stream<0, 2, 1, 8, 0>(d, n, dimg, out, 0, 16u << 10); }},
-                   {12, "K1, 12 waves/WG, 1 WG/CU", [&] { launch_stream<0>(d, n, dimg, out, 0, 16u << 10); }},
-                   {16, "K1, 8 waves/WG, 2 WG/CU", [&] { launch_stream<0, 2, 1, 8, 0>(d, n, dimg, out); }},
-                   {24, "K1, 12 waves/WG, 2 WG/CU", [&] { launch_stream<0>(d, n, dimg, out); }}};
+        } occ[] = {{4, "K2, 4 waves/WG, 1 WG/CU", [&] { launch_stream<2, 2, 4, 0>(d, n, dimg, out, 0, 16u << 10); }},
+                   {8, "K2, 4 waves/WG, 2 WG/CU", [&] { launch_stream<2, 2, 4, 0>(d, n, dimg, out); }},
+                   {8, "K1, 8 waves/WG, 1 WG/CU", [&] { launch_stream<2, 1, 8, 0>(d, n, dimg, out, 0, 16u << 10); }},
+                   {12, "K1, 12 waves/WG, 1 WG/CU", [&] { launch_stream<>(d, n, dimg, out, 0, 16u << 10); }},
+                   {16, "K1, 8 waves/WG, 2 WG/CU", [&] { launch_stream<2, 1, 8, 0>(d, n, dimg, out); }},
+                   {24, "K1, 12 waves/WG, 2 WG/CU", [&] { launch_stream<>(d, n, dimg, out); }}};
         for (auto &o : occ) {
             const double ms = time_ms(o.go, 9);
             printf("%-24s occupancy %2d waves/CU (%s): %6.1f%% of 8 TB/s\n", cname, o.waves, o.how,
@@ -184,7 +183,7 @@ int main() {
         if (cfg == 1) {
             const double ms = time_ms([&] { launch_crc_regular(buf, n, 4096, 0xFFFFFFFFu, ref, dimg, 512, 0); }, 15);
             printf("%-24s %-18s %8.3f ms  %6.1f%% of 8 TB/s\n", cname, "regular kernel", ms, total / (ms * 1e-3) / 8e12 * 100);
-            launch_stream<0>(d, n, dimg, out);
+            launch_stream<>(d, n, dimg, out);
             CK(hipDeviceSynchronize());
             std::vector<uint32_t> a(n), b(n);
             CK(hipMemcpy(a.data(), out, n * 4, hipMemcpyDeviceToHost));

@@ -38,11 +38,11 @@ static Cfg make(const char *nm, size_t n, uint32_t L, uint32_t fpw, const uint32
     c.go = [=](const uint8_t *buf, uint32_t *out) {
         const size_t nv = n / kV;
         const dim3 grid((unsigned)((nv + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw)));
-        hipLaunchKernelGGL((crc_regular_kernel<0, K, false, false, D, kV, false, kWv, kCap>), grid, dim3(64 * kWv), 0,
+        hipLaunchKernelGGL((crc_regular_kernel<K, false, false, D, kV, false, kWv, kCap>), grid, dim3(64 * kWv), 0,
                            0, buf, (uint32_t)nv, fpw, (size_t)kV * L, 0xFFFFFFFFu, img, out, nullptr, (size_t)0);
     };
     hipFuncAttributes a;
-    CK(hipFuncGetAttributes(&a, (const void *)crc_regular_kernel<0, K, false, false, D, kV, false, kWv, kCap>));
+    CK(hipFuncGetAttributes(&a, (const void *)crc_regular_kernel<K, false, false, D, kV, false, kWv, kCap>));
     c.vgprs = a.numRegs;
     return c;
 }
