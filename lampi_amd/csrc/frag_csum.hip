@@ -2607,16 +2607,27 @@ static uint32_t pick_fpw(size_t n, uint32_t R) {
     return fpw;
 }
 
+// Large fragments of a known length (messages; descriptor batches pass frag_len 0): halve the
+// fragments per wave while the grid has fewer than 2048 workgroups (4 per resident slot) and a
+// workgroup of kWv waves would carry more than 512 KiB -- a 1 GiB message of 65,456-byte
+// fragments otherwise runs as ~500 workgroups of 2-3 MiB, most of the chip idle in the tail.
+static uint32_t spread_fpw(uint32_t fpw, size_t n, int kWv, size_t frag_len) {
+    while (frag_len > 0 && fpw > 1 && (n + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw) < 2048 &&
+           (size_t)kWv * fpw * frag_len > (512u << 10))
+        fpw >>= 1;
+    return fpw;
+}
+
 constexpr int kRegularChains = 2;
 
 // crc_rows_kernel with a fused copy: 8-wave workgroups (16 waves/CU, one row in flight each),
 // half the fragments per wave of the 4-wave schedule so a workgroup covers the same span
 template <class Src>
 static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uint32_t *img, uint32_t *out,
-                                 hipStream_t s) {
+                                 hipStream_t s, size_t frag_len = 0) {
     static_assert(Src::kCopy, "the staging area is for the fused copy");
     constexpr int kWv = 2 * kWaves;  // 10-wave workgroups (20 waves/CU): 61% against 69% (4M x 4 KiB)
-    const uint32_t fpw = std::max(1u, pick_fpw(n, R) / 2);
+    const uint32_t fpw = spread_fpw(std::max(1u, pick_fpw(n, R) / 2), n, kWv, frag_len);
     const dim3 grid((unsigned)((n + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw)));
     hipLaunchKernelGGL((crc_rows_kernel<Src, kWv>), grid, dim3(64 * kWv), 0, s, src, n, fpw, img, out);
 }
@@ -2628,10 +2639,13 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
 // fragments is only 256 fragments).  Every workgroup stages ~77 KiB of LDS tables, so more
 // workgroups than CUs only repeat that prologue: 4,096 x 4 KiB took 21.9 us at >= 2048
 // workgroups, 14.6 us at >= 512, 9.95 us at >= 256 (bench.py --latency); config C unchanged.
-static uint32_t frags_per_wg(size_t n) {
+// With the fragment length known (messages), large fragments are spread as in spread_fpw
+// (16,404 x 65,456 bytes: 6 fragments per workgroup, not 48: CRC 55 -> 62%, SUM 62 -> 74%;
+// profiles/r02_bigfrag_ab.txt).
+static uint32_t frags_per_wg(size_t n, size_t frag_len = 0) {
     uint32_t fpg = 96;
     while (fpg > 3 && n / fpg < 256) fpg >>= 1;
-    return fpg;
+    return spread_fpw(fpg, n, 1, frag_len);
 }
 
 // crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_sweep.hip)
@@ -2671,7 +2685,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
-    const uint32_t fpg = frags_per_wg(n);
+    const uint32_t fpg = frags_per_wg(n, frag_len);
     hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
                        MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
     return hipGetLastError();
@@ -2739,9 +2753,9 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 // 68.4 -> 70.0%, sources at +8 68.5 -> 69.8%, destinations at +8 66.2 -> 68.2%, at +1 62.8 -> 68.0%,
 // the receive step in GM slots 65.0 -> 68.4% of read + write.
 template <class Src>
-static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t s) {
+static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t s, size_t frag_len = 0) {
     constexpr int kWv = 8;
-    const uint32_t fpw = std::max(1u, pick_fpw(n, 1) / 2);  // the 4-wave schedule's span per workgroup
+    const uint32_t fpw = spread_fpw(std::max(1u, pick_fpw(n, 1) / 2), n, kWv, frag_len);  // the 4-wave schedule's span per workgroup
     hipLaunchKernelGGL((sum_rows_kernel<Src, uint32_t, false, kWv>), dim3((unsigned)((n + (size_t)kWv * fpw - 1) /
                                                                                       ((size_t)kWv * fpw))),
                        dim3(64 * kWv), 0, s, src, n, fpw, out);
@@ -2811,12 +2825,12 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
                           const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
-    if (msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 && ((uintptr_t)base & 15u) == 0 &&
-        n <= 0xFFFFFFFFull) {
+    if (msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 && regular_msg_frag(frag_len, true) &&
+        ((uintptr_t)base & 15u) == 0 && n <= 0xFFFFFFFFull) {
         return launch_regular<true>(base, n, frag_len, 0u, out, nullptr, s);
     }
     if (img) {
-        const uint32_t fpg = frags_per_wg(n);
+        const uint32_t fpg = frags_per_wg(n, frag_len);
         hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, true, kStreamWv, kStreamCap>),
                            frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
         return hipGetLastError();
@@ -2836,7 +2850,7 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
     if (mode == LAMPI_CSUM_CRC32) {
         if (regular) return launch_crc_regular_copy(base, n, frag_len, partial, dst, dst_stride, out, img, s);
         launch_crc_rows_copy(MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n,
-                             (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes), img, out, s);
+                             (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes), img, out, s, frag_len);
         return hipGetLastError();
     }
     if (regular) {
@@ -2845,7 +2859,7 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
         return hipGetLastError();
     }
     // ragged or unaligned: the fused copy of descriptor batches
-    launch_sum_copy(MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, out, s);
+    launch_sum_copy(MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, out, s, frag_len);
     return hipGetLastError();
 }
 

@@ -8,6 +8,16 @@
 
 namespace lampi {
 
+// Uniform message fragments of whole 4 KiB rows take the regular kernels (read-only checksums),
+// except where the piece streams measured faster (tools/microbench/bigfrag_scan.py,
+// profiles/r02_bigfrag_ab.txt, 1 and 16 GiB batches, A/B on one box): 64 KiB fragments in CRC
+// (regular 61-71% of the HBM roofline -- its concurrent chains sit 64 KiB apart; 48, 96, 128,
+// 256 KiB and 1 MiB run at 77-79% -- against 67-76%) and 33-64 KiB fragments in SUM (68-76%
+// against 74-78%; from 128 KiB on the two are within a point).
+inline bool regular_msg_frag(size_t frag_len, bool sum) {
+    return sum ? (frag_len <= (32u << 10) || frag_len > (64u << 10)) : frag_len != (64u << 10);
+}
+
 // Workgroups for the persistent CRC kernel on `device` (one 1024-thread WG per CU).
 int crc_grid(int device);
 

@@ -538,7 +538,7 @@ int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t 
     if (e != hipSuccess) return to_int(e);
     if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_msg(base, msg_len, frag_len, n, d_out, img, grid, s));
     const bool regular = msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 &&
-                         ((uintptr_t)base & 15u) == 0;
+                         regular_msg_frag(frag_len, false) && ((uintptr_t)base & 15u) == 0;
     if (regular) return to_int(launch_crc_regular(base, n, frag_len, partial, d_out, img, grid, s));
     return to_int(launch_crc_msg(base, msg_len, frag_len, partial, n, d_out, img, grid, s));
 }
