@@ -3,7 +3,7 @@ header offset 72 (dst % 16 = 8) against the same copy into slots at offset 80 / 
 aligned) and into a contiguous destination, and lampi_msg_csum alone (no copy); 64 KiB fragments
 (a whole number of 4 KiB rows: the regular kernel's copy) for comparison.  1 GiB messages.
 
-python tools/microbench/gm_send_shapes.py
+python tools/microbench/gm_send_shapes.py [--gib G]   (message size, default 1 GiB)
 """
 import os
 import sys
@@ -28,8 +28,9 @@ def timed(run, reps=20):
     return e0.elapsed_time(e1) / reps / 1e3
 
 
+GIB = int(sys.argv[sys.argv.index("--gib") + 1]) if "--gib" in sys.argv else 1
 for L in (65456, 65536):
-    n = (1 << 30) // L
+    n = (GIB << 30) // L
     msg = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     dv.fill_stream(msg, seed=13)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
