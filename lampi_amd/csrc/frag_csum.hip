@@ -154,6 +154,31 @@ struct MsgCopySource {
     }
 };
 
+// The 4 KiB rows of a message's large fragments as items (SUM fused copies, launch_msg_bcopy):
+// item v is row v % rpf of fragment v / rpf, so a workgroup's waves take consecutive rows of
+// one fragment instead of eight fragments 64 KiB apart (plain copies in that shape:
+// tools/microbench/copy4.hip, 64 KiB fragments 67% against 63-65%).  A row starts at a multiple
+// of 4096 bytes into its fragment, on the fragment's word grid, so the fragment's uicsum is the
+// sum of its rows' sums: emit adds them into out (zeroed first).  Rows past a short last
+// fragment are empty.
+struct MsgRowCopySource {
+    static constexpr bool kCopy = true;
+    static constexpr bool kPhase = false;
+    const uint8_t *base;
+    size_t msg_len;
+    size_t frag_len;
+    uint8_t *dst;
+    size_t dst_stride;
+    uint32_t rpf;  // rows per fragment, ceil(frag_len / 4096)
+    __device__ FragInfo get(size_t v) const {
+        const size_t f = v / rpf, r = v - f * rpf;
+        const size_t off = f * frag_len + r * kRowBytes;
+        const size_t fend = min(msg_len, (f + 1) * frag_len);
+        const uint32_t len = off < fend ? (uint32_t)min((size_t)kRowBytes, fend - off) : 0u;
+        return {(gbyte *)(base + off), len, 0u, dst + f * dst_stride + r * kRowBytes, len};
+    }
+};
+
 // Typemap pieces of chained checksums (lampi_chain_csum_batch): pieces longer than `small`
 // bytes; the others read as empty here and are done one thread per piece.  CRC values start
 // from a zero register (the chain fold threads the caller's register); SUM values are taken at
@@ -216,6 +241,10 @@ struct IsRecv<RecvSource> : std::true_type {};
 // every kernel stores a fragment's checksum through this: receive sources also decide it
 template <class Src, class Acc>
 __device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v, const FragInfo &fi) {
+    if constexpr (std::is_same<Src, MsgRowCopySource>::value) {  // a row's part of its fragment's sum
+        if (v != 0) atomicAdd(out + f / src.rpf, v);
+        return;
+    }
     out[f] = v;
     if constexpr (IsRecv<Src>::value) src.verdict(f, v, fi);
 }
@@ -2856,6 +2885,13 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
     if (regular) {
         hipLaunchKernelGGL(sum_regular_kernel<true>, dim3((unsigned)((n + kWaves - 1) / kWaves)), dim3(kBlock), 0, s,
                            base, (uint32_t)n, frag_len, out, dst, dst_stride);
+        return hipGetLastError();
+    }
+    if (frag_len >= 4 * (size_t)kRowBytes && msg_len != 0) {  // large fragments: row items (MsgRowCopySource)
+        const hipError_t e = hipMemsetAsync(out, 0, n * sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+        const uint32_t rpf = (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes);
+        launch_sum_copy(MsgRowCopySource{base, msg_len, frag_len, dst, dst_stride, rpf}, n * rpf, out, s, kRowBytes);
         return hipGetLastError();
     }
     // ragged or unaligned: the fused copy of descriptor batches

@@ -202,6 +202,11 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     (4096 * 20001, 4096, 4096 + 80, 72),    # regular kernel into 72-byte-header slots (dst % 16 = 8)
     (16384 * 3001, 16384, 16384 + 76, 4),   # regular, 16 KiB, slot stride and base only 4-byte aligned
     (5, 4096, 4096, 1),                     # one short fragment
+    # SUM: fragments of 16 KiB and more that are not whole rows go through row items
+    # (MsgRowCopySource: one 4 KiB row per item, sums added per fragment)
+    (16385 * 2000 + 3, 16385, 16385 + 7, 1),  # 5 rows, the last 1 byte; byte-misaligned destinations
+    (40000 * 1500 + 12345, 40000, 40000, 0),  # a short last fragment with fewer rows
+    (20001 * 777, 20001, 20480, 8),           # odd length, destinations at +8
 ])
 def test_msg_bcopy(cuda, oracle, mode, msg_len, frag_len, stride, dst_off):
     """lampi_msg_bcopy: fragment k -> dst + k*stride with its checksum fused; gap bytes untouched."""
