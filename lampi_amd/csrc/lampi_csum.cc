@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -91,7 +92,8 @@ struct HostCtx {
     hipStream_t stream = nullptr;
     hipEvent_t half_free[2] = {nullptr, nullptr};  // the last transfer through each bounce half
     uint8_t *pin = nullptr;                       // 2 x kBounceHalf pinned bytes
-    uint64_t *pres = nullptr;                     // pinned, host-coherent result words (4 x u64)
+    uint64_t *pres = nullptr;                     // pinned, host-coherent result words (4 x u64) + signal word
+    uint64_t seq = 0;                             // the last signal value asked for (wait_done)
     uint8_t *zpin = nullptr;                      // pinned, host-coherent staging of small calls
     uint8_t *zpin_d = nullptr;                    // ... and the device's view of it,
     uint64_t *pres_d = nullptr;                   //     of pres
@@ -134,6 +136,7 @@ struct HostCtx {
         if (stream) (void)hipStreamDestroy(stream);
         if (have_cur && cur != dev) (void)hipSetDevice(cur);
         dev = -1;
+        seq = 0;
         stream = nullptr;
         half_free[0] = half_free[1] = nullptr;
         pin = nullptr;
@@ -153,6 +156,8 @@ struct HostCtx {
 
 thread_local HostCtx t_ctx;
 
+constexpr int kSignalWord = 7;  // pres[7]: the sequence number wait_done polls for
+
 HostCtx &host_ctx() {
     HostCtx &ctx = t_ctx;
     int dev = 0;
@@ -164,7 +169,8 @@ HostCtx &host_ctx() {
         for (hipEvent_t &e : ctx.half_free) LAMPI_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         LAMPI_CHECK(hipHostMalloc((void **)&ctx.pin, 2 * kBounceHalf, hipHostMallocDefault));
         constexpr unsigned kCoherent = hipHostMallocMapped | hipHostMallocCoherent;
-        LAMPI_CHECK(hipHostMalloc((void **)&ctx.pres, 4 * sizeof(uint64_t), kCoherent));
+        LAMPI_CHECK(hipHostMalloc((void **)&ctx.pres, 8 * sizeof(uint64_t), kCoherent));
+        ctx.pres[kSignalWord] = ctx.seq = 0;
         LAMPI_CHECK(hipHostMalloc((void **)&ctx.hdesc, kMaxPieces * sizeof(lampi_frag_desc), kCoherent));
         LAMPI_CHECK(hipHostMalloc((void **)&ctx.zpin, kZeroCopy, kCoherent));
         LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.zpin_d, ctx.zpin, 0));
@@ -229,6 +235,28 @@ const lampi_frag_desc *upload_descs(HostCtx &c, uint32_t n, bool zero_copy) {
     return c.ddesc;
 }
 
+// Wait for the call's kernels.  A zero-copy call (at most 256 KiB, a few microseconds of device
+// work) has the stream write the next sequence number into host-coherent pinned memory after
+// them and polls for it: a tiny kernel's round trip is 8.7 us that way against 10.9 us through
+// hipStreamSynchronize's wake-up (tools/microbench/sync_latency.hip, profiles/r02_sync_latency.txt).
+// Larger calls, a stream that cannot write the value, or no signal within 5 ms fall back to
+// hipStreamSynchronize, which also reports errors.
+void wait_done(HostCtx &c, bool poll) {
+    if (poll) {
+        const uint64_t seq = ++c.seq;
+        uint64_t *sig = c.pres + kSignalWord;
+        if (hipStreamWriteValue64(c.stream, c.pres_d + kSignalWord, seq, 0) == hipSuccess) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t i = 0; __atomic_load_n(sig, __ATOMIC_ACQUIRE) != seq; ++i) {
+                __builtin_ia32_pause();
+                if ((i & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
+            }
+            if (__atomic_load_n(sig, __ATOMIC_ACQUIRE) == seq) return;
+        }
+    }
+    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+}
+
 // CRC of the staged bytes [0, len) from register `partial`, computed on the GPU; the result is
 // written by the last kernel straight into pinned host memory.
 uint32_t device_crc(HostCtx &c, const Staged &st, uint64_t len, uint32_t partial) {
@@ -254,7 +282,7 @@ uint32_t device_crc(HostCtx &c, const Staged &st, uint64_t len, uint32_t partial
         LAMPI_CHECK(launch_crc_desc(d, n, c.dvals, img, grid, c.stream));
         LAMPI_CHECK(launch_crc_combine(c.dvals, n, combine_tables(c, B), next_pow2(n), res, c.stream));
     }
-    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    wait_done(c, st.zero_copy);
     return ((const volatile uint32_t *)c.pres)[0];
 }
 
@@ -278,7 +306,7 @@ uint32_t device_sum(HostCtx &c, const Staged &st, uint64_t len, unsigned int *pi
     }
     uint32_t *out3 = (uint32_t *)c.pres_d;
     LAMPI_CHECK(launch_sum_finish(c.dvals, n, st.base, len, *pint, *plen, out3, c.stream));
-    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    wait_done(c, st.zero_copy);
     const volatile uint32_t *h = (const volatile uint32_t *)c.pres;
     *pint = h[1];
     *plen = h[2];
@@ -302,7 +330,7 @@ uint64_t device_sum64(HostCtx &c, const Staged &st, uint64_t len, unsigned long 
     LAMPI_CHECK(launch_sum64_desc(d, n, c.dvals64, true, c.stream));
     uint64_t *out3 = c.pres_d;
     LAMPI_CHECK(launch_sum64_finish(c.dvals64, n, st.base, len, k ? (uint64_t)*plong : 0u, k, out3, c.stream));
-    LAMPI_CHECK(hipStreamSynchronize(c.stream));
+    wait_done(c, st.zero_copy);
     const volatile uint64_t *h = (const volatile uint64_t *)c.pres;
     *plong = (unsigned long)h[1];
     *plen = (unsigned long)h[2];
