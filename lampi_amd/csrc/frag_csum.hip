@@ -179,6 +179,26 @@ struct MsgRowCopySource {
     }
 };
 
+// One piece of a host call (lampi_uicrc / lampi_uicsum on at most kZeroCopy bytes) by value, so
+// no descriptor is read back over PCIe; its result is followed by the host signal (emit).
+struct HostOneSource {
+    static constexpr bool kCopy = false;
+    static constexpr bool kPhase = false;
+    uint64_t addr;
+    uint32_t len, partial;
+    uint64_t *sig;  // host-coherent word the host polls (HostCtx::wait_done); seq is stored there
+    uint64_t seq;
+    __device__ FragInfo get(size_t) const { return {(gbyte *)(uintptr_t)addr, len, partial, nullptr, 0u}; }
+};
+
+// Tell a polling host that this kernel's results (already stored) are complete: a system-scope
+// fence, then the sequence number with a system-scope release store (vector store).
+__device__ __forceinline__ void signal_host(uint64_t *sig, uint64_t seq) {
+    if (sig == nullptr) return;
+    __threadfence_system();
+    __hip_atomic_store(sig, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Typemap pieces of chained checksums (lampi_chain_csum_batch): pieces longer than `small`
 // bytes; the others read as empty here and are done one thread per piece.  CRC values start
 // from a zero register (the chain fold threads the caller's register); SUM values are taken at
@@ -241,6 +261,11 @@ struct IsRecv<RecvSource> : std::true_type {};
 // every kernel stores a fragment's checksum through this: receive sources also decide it
 template <class Src, class Acc>
 __device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v, const FragInfo &fi) {
+    if constexpr (std::is_same<Src, HostOneSource>::value) {  // the host call's one result, then the signal
+        out[f] = v;
+        signal_host(src.sig, src.seq);
+        return;
+    }
     if constexpr (std::is_same<Src, MsgRowCopySource>::value) {  // a row's part of its fragment's sum
         if (v != 0) atomicAdd(out + f / src.rpf, v);
         return;
@@ -2457,7 +2482,8 @@ __global__ void __launch_bounds__(256) chain_fold_kernel(const lampi_copy_desc *
 // new (lastPartialLong, lastPartialLength) is the trailing partial word of the virtual stream
 // [old partial bytes | the len new bytes].  out3 = {sum, plong, plen}.
 __global__ void sum64_finish_kernel(const uint64_t *__restrict__ vals, uint32_t nv, const uint8_t *__restrict__ src,
-                                    uint64_t len, uint64_t plong, uint64_t plen, uint64_t *__restrict__ out3) {
+                                    uint64_t len, uint64_t plong, uint64_t plen, uint64_t *__restrict__ out3,
+                                    uint64_t *sig, uint64_t seq) {
     uint64_t acc = 0;
     for (uint32_t i = threadIdx.x; i < nv; i += blockDim.x) acc += vals[i];
 #pragma unroll
@@ -2478,6 +2504,7 @@ __global__ void sum64_finish_kernel(const uint64_t *__restrict__ vals, uint32_t 
     out3[0] = total;
     out3[1] = np;
     out3[2] = nl;
+    signal_host(sig, seq);
 }
 
 // ---- synthetic stream fill ----------------------------------------------------------------
@@ -2531,7 +2558,7 @@ __global__ void __launch_bounds__(256) fill_stream_kernel(uint8_t *dst, size_t n
 // tabs[lvl*128 + p*16 + v]: normal-domain nibble tables of shift by B * 2^lvl.
 __global__ void __launch_bounds__(1024) crc_combine_kernel(const uint32_t *__restrict__ vals, uint32_t n,
                                                            const uint32_t *__restrict__ tabs, uint32_t npow,
-                                                           uint32_t *__restrict__ out) {
+                                                           uint32_t *__restrict__ out, uint64_t *sig, uint64_t seq) {
     extern __shared__ __attribute__((aligned(16))) uint32_t v[];  // 2 * npow words: ping-pong
     const uint32_t pad = npow - n;
     for (uint32_t i = threadIdx.x; i < npow; i += blockDim.x) v[i] = (i < pad) ? 0u : vals[i - pad];
@@ -2552,7 +2579,10 @@ __global__ void __launch_bounds__(1024) crc_combine_kernel(const uint32_t *__res
         src = dst;
         dst = tmp;
     }
-    if (threadIdx.x == 0) out[0] = src[0];
+    if (threadIdx.x == 0) {
+        out[0] = src[0];
+        signal_host(sig, seq);
+    }
 }
 
 // ---- SUM over a chained stream ------------------------------------------------------------
@@ -2561,7 +2591,7 @@ __global__ void __launch_bounds__(1024) crc_combine_kernel(const uint32_t *__res
 // produces the new (pint, plen) state.  out3 = {sum, pint, plen}.
 __global__ void sum_stream_finish_kernel(const uint32_t *__restrict__ partials, uint32_t npart,
                                          const uint8_t *__restrict__ src, uint64_t len, uint32_t pint,
-                                         uint32_t plen, uint32_t *__restrict__ out3) {
+                                         uint32_t plen, uint32_t *__restrict__ out3, uint64_t *sig, uint64_t seq) {
     __shared__ uint32_t red[256];
     uint32_t acc = 0;
     for (uint32_t i = threadIdx.x; i < npart; i += blockDim.x) acc += partials[i];
@@ -2589,6 +2619,7 @@ __global__ void sum_stream_finish_kernel(const uint32_t *__restrict__ partials, 
             out3[0] = sum;
             out3[1] = w;
             out3[2] = k + (uint32_t)take;
+            signal_host(sig, seq);
             return;
         }
     }
@@ -2599,6 +2630,7 @@ __global__ void sum_stream_finish_kernel(const uint32_t *__restrict__ partials, 
     out3[0] = sum + tail;
     out3[1] = tail;
     out3[2] = (uint32_t)r;
+    signal_host(sig, seq);
 }
 
 // Fragment-strided stream: fragment i of dst (frag_len bytes, frag_len % 8 == 0) holds stream
@@ -2830,8 +2862,8 @@ hipError_t launch_sum64_desc(const lampi_frag_desc *d, size_t n, uint64_t *out, 
 }
 
 hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t *src, uint64_t len, uint64_t plong,
-                               uint64_t plen, uint64_t *out3, hipStream_t s) {
-    hipLaunchKernelGGL(sum64_finish_kernel, dim3(1), dim3(256), 0, s, vals, nv, src, len, plong, plen, out3);
+                               uint64_t plen, uint64_t *out3, hipStream_t s, uint64_t *sig, uint64_t seq) {
+    hipLaunchKernelGGL(sum64_finish_kernel, dim3(1), dim3(256), 0, s, vals, nv, src, len, plong, plen, out3, sig, seq);
     return hipGetLastError();
 }
 
@@ -2958,16 +2990,30 @@ hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t
 }
 
 hipError_t launch_crc_combine(const uint32_t *vals, uint32_t n, const uint32_t *tabs, uint32_t npow,
-                              uint32_t *out, hipStream_t s) {
+                              uint32_t *out, hipStream_t s, uint64_t *sig, uint64_t seq) {
     hipLaunchKernelGGL(crc_combine_kernel, dim3(1), dim3(1024), 2 * npow * sizeof(uint32_t), s, vals, n, tabs, npow,
-                       out);
+                       out, sig, seq);
+    return hipGetLastError();
+}
+
+// One host-call piece by value (HostOneSource): the piece-stream kernel on a single fragment,
+// its result stored to out and followed by the host signal.
+hipError_t launch_host_one(const uint8_t *addr, uint32_t len, uint32_t partial, uint32_t *out, int mode,
+                           const uint32_t *img, hipStream_t s, uint64_t *sig, uint64_t seq) {
+    const HostOneSource src{(uint64_t)(uintptr_t)addr, len, partial, sig, seq};
+    if (mode == LAMPI_CSUM_CRC32)
+        hipLaunchKernelGGL((crc_stream_kernel<HostOneSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), dim3(1),
+                           dim3(64 * kStreamWv), 0, s, src, (size_t)1, 1u, img, out);
+    else
+        hipLaunchKernelGGL((crc_stream_kernel<HostOneSource, kStreamD, kStreamK, true, kStreamWv, kStreamCap>), dim3(1),
+                           dim3(64 * kStreamWv), 0, s, src, (size_t)1, 1u, img, out);
     return hipGetLastError();
 }
 
 hipError_t launch_sum_finish(const uint32_t *partials, uint32_t npart, const uint8_t *src, uint64_t len,
-                             uint32_t pint, uint32_t plen, uint32_t *out3, hipStream_t s) {
+                             uint32_t pint, uint32_t plen, uint32_t *out3, hipStream_t s, uint64_t *sig, uint64_t seq) {
     hipLaunchKernelGGL(sum_stream_finish_kernel, dim3(1), dim3(256), 0, s, partials, npart, src, len, pint, plen,
-                       out3);
+                       out3, sig, seq);
     return hipGetLastError();
 }
 

@@ -59,8 +59,11 @@ hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t
                         int mode, const uint32_t *img, uint32_t *vals, uint32_t *phase, hipStream_t s);
 // 64-bit csum: per-descriptor sums (phased: desc.partial = byte phase 0..7) and the chained finish.
 hipError_t launch_sum64_desc(const lampi_frag_desc *d, size_t n, uint64_t *out, bool phased, hipStream_t s);
+// The host path's last kernels (combine / finish / a single piece) store their result, then, when
+// sig is given, seq into *sig at system scope: the host polls it (lampi_csum.cc wait_done).
 hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t *src, uint64_t len, uint64_t plong,
-                               uint64_t plen, uint64_t *out3, hipStream_t s);
+                               uint64_t plen, uint64_t *out3, hipStream_t s, uint64_t *sig = nullptr,
+                               uint64_t seq = 0);
 // SUM per descriptor / per fragment of a message: piece streams when img (the table image, for its
 // zero chunk) is given, one wavefront per fragment (sum_rows_kernel) otherwise.
 hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
@@ -68,9 +71,12 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
 hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out,
                           const uint32_t *img, int grid, hipStream_t s);
 hipError_t launch_crc_combine(const uint32_t *vals, uint32_t n, const uint32_t *tabs, uint32_t npow,
-                              uint32_t *out, hipStream_t s);
+                              uint32_t *out, hipStream_t s, uint64_t *sig = nullptr, uint64_t seq = 0);
 hipError_t launch_sum_finish(const uint32_t *partials, uint32_t npart, const uint8_t *src, uint64_t len,
-                             uint32_t pint, uint32_t plen, uint32_t *out3, hipStream_t s);
+                             uint32_t pint, uint32_t plen, uint32_t *out3, hipStream_t s, uint64_t *sig = nullptr,
+                             uint64_t seq = 0);
+hipError_t launch_host_one(const uint8_t *addr, uint32_t len, uint32_t partial, uint32_t *out, int mode,
+                           const uint32_t *img, hipStream_t s, uint64_t *sig, uint64_t seq);
 hipError_t launch_fill_frags(uint64_t *dst, size_t n, uint64_t frag_words, uint64_t seed, uint64_t k0,
                              uint64_t kstep, int grid, hipStream_t s);
 hipError_t launch_fill_stream(uint8_t *dst, size_t nbytes, uint64_t seed, uint64_t byte_off, int grid,

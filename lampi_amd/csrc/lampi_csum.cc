@@ -236,23 +236,23 @@ const lampi_frag_desc *upload_descs(HostCtx &c, uint32_t n, bool zero_copy) {
 }
 
 // Wait for the call's kernels.  A zero-copy call (at most 256 KiB, a few microseconds of device
-// work) has the stream write the next sequence number into host-coherent pinned memory after
-// them and polls for it: a tiny kernel's round trip is 8.7 us that way against 10.9 us through
-// hipStreamSynchronize's wake-up (tools/microbench/sync_latency.hip, profiles/r02_sync_latency.txt).
-// Larger calls, a stream that cannot write the value, or no signal within 5 ms fall back to
-// hipStreamSynchronize, which also reports errors.
-void wait_done(HostCtx &c, bool poll) {
-    if (poll) {
-        const uint64_t seq = ++c.seq;
-        uint64_t *sig = c.pres + kSignalWord;
-        if (hipStreamWriteValue64(c.stream, c.pres_d + kSignalWord, seq, 0) == hipSuccess) {
-            const auto t0 = std::chrono::steady_clock::now();
-            for (uint32_t i = 0; __atomic_load_n(sig, __ATOMIC_ACQUIRE) != seq; ++i) {
-                __builtin_ia32_pause();
-                if ((i & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
-            }
-            if (__atomic_load_n(sig, __ATOMIC_ACQUIRE) == seq) return;
+// work) gets a sequence number that its last kernel stores into host-coherent pinned memory once
+// the results are out (signal_host, system scope), and the host polls for it: a tiny kernel's
+// round trip is 6.4 us that way against 10.9 us through hipStreamSynchronize's wake-up
+// (tools/microbench/sync_latency.hip, profiles/r02_sync_latency.txt).  No signal within 5 ms, or
+// a larger call (seq 0), waits in hipStreamSynchronize, which also reports errors.
+uint64_t next_signal(HostCtx &c, const Staged &st) { return st.zero_copy ? ++c.seq : 0u; }
+uint64_t *signal_word(HostCtx &c, uint64_t seq) { return seq ? c.pres_d + kSignalWord : nullptr; }
+
+void wait_done(HostCtx &c, uint64_t seq) {
+    if (seq) {
+        const uint64_t *sig = c.pres + kSignalWord;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t i = 0; __atomic_load_n(sig, __ATOMIC_ACQUIRE) != seq; ++i) {
+            __builtin_ia32_pause();
+            if ((i & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
         }
+        if (__atomic_load_n(sig, __ATOMIC_ACQUIRE) == seq) return;
     }
     LAMPI_CHECK(hipStreamSynchronize(c.stream));
 }
@@ -273,16 +273,20 @@ uint32_t device_crc(HostCtx &c, const Staged &st, uint64_t len, uint32_t partial
         c.hdesc[k].length = (uint32_t)(k == 0 ? first : B);
         c.hdesc[k].partial = k == 0 ? partial : 0u;
     }
-    const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
     uint32_t *res = (uint32_t *)c.pres_d;
-    if (n == 1) {
-        LAMPI_CHECK(launch_crc_desc(d, 1, res, img, grid, c.stream));
+    const uint64_t seq = next_signal(c, st);
+    if (n == 1 && st.zero_copy) {  // the piece by value; its kernel signals
+        LAMPI_CHECK(launch_host_one(st.base, (uint32_t)len, partial, res, LAMPI_CSUM_CRC32, img, c.stream,
+                                    signal_word(c, seq), seq));
+    } else if (n == 1) {
+        LAMPI_CHECK(launch_crc_desc(upload_descs(c, 1, false), 1, res, img, grid, c.stream));
     } else {
         ensure(c.dvals, c.vcap, (size_t)n + 4);
-        LAMPI_CHECK(launch_crc_desc(d, n, c.dvals, img, grid, c.stream));
-        LAMPI_CHECK(launch_crc_combine(c.dvals, n, combine_tables(c, B), next_pow2(n), res, c.stream));
+        LAMPI_CHECK(launch_crc_desc(upload_descs(c, n, st.zero_copy), n, c.dvals, img, grid, c.stream));
+        LAMPI_CHECK(launch_crc_combine(c.dvals, n, combine_tables(c, B), next_pow2(n), res, c.stream,
+                                       signal_word(c, seq), seq));
     }
-    wait_done(c, st.zero_copy);
+    wait_done(c, seq);
     return ((const volatile uint32_t *)c.pres)[0];
 }
 
@@ -300,13 +304,19 @@ uint32_t device_sum(HostCtx &c, const Staged &st, uint64_t len, unsigned int *pi
         c.hdesc[i].partial = 0;
     }
     ensure(c.dvals, c.vcap, (size_t)n + 4);
-    if (n) {
+    if (n == 1 && st.zero_copy) {  // the piece by value
+        const uint32_t *img = nullptr;
+        LAMPI_CHECK(device_tables(c.dev, &img));
+        LAMPI_CHECK(launch_host_one((const uint8_t *)(uintptr_t)c.hdesc[0].addr, c.hdesc[0].length, 0u, c.dvals,
+                                    LAMPI_CSUM_SUM32, img, c.stream, nullptr, 0u));
+    } else if (n) {
         const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
         LAMPI_CHECK(launch_sum_desc(d, n, c.dvals, nullptr, grid, c.stream));
     }
     uint32_t *out3 = (uint32_t *)c.pres_d;
-    LAMPI_CHECK(launch_sum_finish(c.dvals, n, st.base, len, *pint, *plen, out3, c.stream));
-    wait_done(c, st.zero_copy);
+    const uint64_t seq = next_signal(c, st);
+    LAMPI_CHECK(launch_sum_finish(c.dvals, n, st.base, len, *pint, *plen, out3, c.stream, signal_word(c, seq), seq));
+    wait_done(c, seq);
     const volatile uint32_t *h = (const volatile uint32_t *)c.pres;
     *pint = h[1];
     *plen = h[2];
@@ -329,8 +339,10 @@ uint64_t device_sum64(HostCtx &c, const Staged &st, uint64_t len, unsigned long 
     const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
     LAMPI_CHECK(launch_sum64_desc(d, n, c.dvals64, true, c.stream));
     uint64_t *out3 = c.pres_d;
-    LAMPI_CHECK(launch_sum64_finish(c.dvals64, n, st.base, len, k ? (uint64_t)*plong : 0u, k, out3, c.stream));
-    wait_done(c, st.zero_copy);
+    const uint64_t seq = next_signal(c, st);
+    LAMPI_CHECK(launch_sum64_finish(c.dvals64, n, st.base, len, k ? (uint64_t)*plong : 0u, k, out3, c.stream,
+                                    signal_word(c, seq), seq));
+    wait_done(c, seq);
     const volatile uint64_t *h = (const volatile uint64_t *)c.pres;
     *plong = (unsigned long)h[1];
     *plen = (unsigned long)h[2];
