@@ -897,7 +897,7 @@ def run_recv(args):
                      "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}"),
                      "traffic_source": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}", "source"),
                      "kernel": "crc_rows_kernel<RecvSource, 8>" if mode == dv.CRC32 else
-                               "crc_stream_kernel<RecvSource, kPB = 16, kCopy> (+ sum_rows_kernel fallback)",
+                               "sum_rows_kernel<RecvSource, uint32_t, false, 8>",
                      "kernel_avg_ms": round(kern * 1e3, 4), "algorithmic_bytes_per_launch": int(moved),
                      "note": "algorithmic bytes = payload read + payload written; the 4-byte expected value and "
                              "32-byte descriptor per fragment excluded"},
