@@ -485,7 +485,8 @@ def run_device(args):
                     "GiB_per_s": round(r[1] / GIB / r[0], 2),
                     "roofline_frac": round(r[1] / r[0] / 1e9 / HBM_PEAK_GBS, 4),
                     "parity_ok": r[2] == 0} for i, r in enumerate(rows)]
-        cfg_key = f"{'crc' if crc else 'sum'}_{n}x{L}"
+        # PMC traffic is recorded per kernel: the descriptor runs have no entry of their own
+        cfg_key = f"{'crc' if crc else 'sum'}_{'desc_' if args.desc else ''}{n}x{L}"
         traffic = None if args.dry_run else read_traffic(cfg_key)
         kernel = ("none (dry run)" if args.dry_run else
                   "crc_stream_kernel (descriptors)" if args.desc and crc else
@@ -494,7 +495,8 @@ def run_device(args):
         workload = (f"config D shard {args.shard} of 8: {n} x {L} B fragments k = {args.shard} (mod 8), seed 3"
                     if args.shard is not None else
                     f"{n} x {L} B fragments per GPU, device-resident, "
-                    f"{'CRC-32/MPEG-2 (uicrc)' if crc else 'uicsum'}, one wavefront per fragment")
+                    f"{'CRC-32/MPEG-2 (uicrc)' if crc else 'uicsum'}, "
+                    f"{'one descriptor per fragment (piece streams)' if args.desc else 'one wavefront per fragment'}")
         result = {
             "metric": METRIC,
             "value": round(value, 2),
