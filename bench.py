@@ -35,6 +35,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--frags F] [--frag-b
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -1005,8 +1006,15 @@ def run_latency(args):
             t0 = time.perf_counter()
             _clib().lampi_bcopy_uicrc(hb.ctypes.data, hd.ctypes.data, nb, nb, 0xFFFFFFFF)
             tc.append(time.perf_counter() - t0)
+        ts = []
+        pint, plen = ctypes.c_uint(0), ctypes.c_uint(0)
+        for i in range(220):
+            t0 = time.perf_counter()
+            _clib().lampi_uicsum(hb.ctypes.data, nb, ctypes.byref(pint), ctypes.byref(plen))
+            ts.append(time.perf_counter() - t0)
         host_rows.append({"bytes": nb, "uicrc_us_median": round(float(np.median(t[20:])) * 1e6, 2),
-                          "bcopy_uicrc_us_median": round(float(np.median(tc[20:])) * 1e6, 2)})
+                          "bcopy_uicrc_us_median": round(float(np.median(tc[20:])) * 1e6, 2),
+                          "uicsum_us_median": round(float(np.median(ts[20:])) * 1e6, 2)})
     rows.append({"host_entry_points": host_rows})
     dv.frag_csum_batch(descs, n=nmax, out=out)
     got = dv.as_u32(out[:nmax])

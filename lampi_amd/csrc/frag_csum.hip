@@ -2588,13 +2588,37 @@ __global__ void __launch_bounds__(1024) crc_combine_kernel(const uint32_t *__res
 // ---- SUM over a chained stream ------------------------------------------------------------
 // The body [t, t + 4*nb) was summed by sum_rows_kernel in word-aligned pieces (partials);
 // this adds the head (completing the caller's partial word) and the tail partial word and
-// produces the new (pint, plen) state.  out3 = {sum, pint, plen}.
+// produces the new (pint, plen) state.  out3 = {sum, pint, plen}.  partials == nullptr (small
+// host calls, one kernel in all): the workgroup sums the body words of src itself -- aligned
+// dwords funnel-shifted by the body's byte offset, consecutive lanes on consecutive words, eight
+// loads in flight per thread (host memory: each load is a PCIe round trip).
 __global__ void sum_stream_finish_kernel(const uint32_t *__restrict__ partials, uint32_t npart,
                                          const uint8_t *__restrict__ src, uint64_t len, uint32_t pint,
                                          uint32_t plen, uint32_t *__restrict__ out3, uint64_t *sig, uint64_t seq) {
-    __shared__ uint32_t red[256];
+    __shared__ uint32_t red[1024];
     uint32_t acc = 0;
-    for (uint32_t i = threadIdx.x; i < npart; i += blockDim.x) acc += partials[i];
+    if (partials != nullptr) {
+        for (uint32_t i = threadIdx.x; i < npart; i += blockDim.x) acc += partials[i];
+    } else {
+        const uint32_t k0 = plen >= 4 ? 0u : plen;
+        const uint64_t take = k0 ? (4u - k0 < len ? 4u - k0 : len) : 0u;
+        if (!(k0 && k0 + take < 4)) {  // otherwise every byte completes the partial word
+            const uint64_t nw = (len - take) >> 2;  // body words
+            const uintptr_t b0 = (uintptr_t)(src + take);
+            const uint32_t sh = (uint32_t)(b0 & 3u);
+            const uint32_t *a = (const uint32_t *)(b0 - sh);
+            for (uint64_t i0 = threadIdx.x; i0 < nw; i0 += 8ull * blockDim.x) {
+                uint32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+                    v[u] = i < nw ? (sh ? __builtin_amdgcn_alignbyte(a[i + 1], a[i], sh) : a[i]) : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += v[u];
+            }
+        }
+    }
     red[threadIdx.x] = acc;
     __syncthreads();
     for (uint32_t s = blockDim.x / 2; s > 0; s >>= 1) {
@@ -3012,8 +3036,8 @@ hipError_t launch_host_one(const uint8_t *addr, uint32_t len, uint32_t partial, 
 
 hipError_t launch_sum_finish(const uint32_t *partials, uint32_t npart, const uint8_t *src, uint64_t len,
                              uint32_t pint, uint32_t plen, uint32_t *out3, hipStream_t s, uint64_t *sig, uint64_t seq) {
-    hipLaunchKernelGGL(sum_stream_finish_kernel, dim3(1), dim3(256), 0, s, partials, npart, src, len, pint, plen,
-                       out3, sig, seq);
+    hipLaunchKernelGGL(sum_stream_finish_kernel, dim3(1), dim3(partials ? 256 : 1024), 0, s, partials, npart, src, len,
+                       pint, plen, out3, sig, seq);
     return hipGetLastError();
 }
 

@@ -263,7 +263,10 @@ uint32_t device_crc(HostCtx &c, const Staged &st, uint64_t len, uint32_t partial
     const uint32_t *img = nullptr;
     LAMPI_CHECK(device_tables(c.dev, &img));
     const int grid = crc_grid(c.dev);
-    const uint64_t B = piece_size(len);
+    // zero-copy calls above 8 KiB: 4 KiB pieces folded by the combine kernel (one piece per row:
+    // the piece-stream kernel then joins no fragment across its chains, whose serial join of a
+    // 64 KiB piece cost ~20 us); otherwise pieces of piece_size
+    const uint64_t B = (st.zero_copy && len > 8192) ? 4096 : piece_size(len);
     const uint32_t n = (uint32_t)((len + B - 1) / B);
     // pieces of the front-padded message: piece 0 holds the first len - (n-1)*B bytes
     const uint64_t first = len - (uint64_t)(n - 1) * B;
@@ -304,17 +307,20 @@ uint32_t device_sum(HostCtx &c, const Staged &st, uint64_t len, unsigned int *pi
         c.hdesc[i].partial = 0;
     }
     ensure(c.dvals, c.vcap, (size_t)n + 4);
-    if (n == 1 && st.zero_copy) {  // the piece by value
-        const uint32_t *img = nullptr;
-        LAMPI_CHECK(device_tables(c.dev, &img));
-        LAMPI_CHECK(launch_host_one((const uint8_t *)(uintptr_t)c.hdesc[0].addr, c.hdesc[0].length, 0u, c.dvals,
-                                    LAMPI_CSUM_SUM32, img, c.stream, nullptr, 0u));
-    } else if (n) {
+    uint32_t *out3 = (uint32_t *)c.pres_d;
+    const uint64_t seq = next_signal(c, st);
+    if (st.zero_copy) {  // one kernel sums the body, completes the state and signals
+        LAMPI_CHECK(launch_sum_finish(nullptr, 0, st.base, len, *pint, *plen, out3, c.stream, signal_word(c, seq), seq));
+        wait_done(c, seq);
+        const volatile uint32_t *h = (const volatile uint32_t *)c.pres;
+        *pint = h[1];
+        *plen = h[2];
+        return h[0];
+    }
+    if (n) {
         const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
         LAMPI_CHECK(launch_sum_desc(d, n, c.dvals, nullptr, grid, c.stream));
     }
-    uint32_t *out3 = (uint32_t *)c.pres_d;
-    const uint64_t seq = next_signal(c, st);
     LAMPI_CHECK(launch_sum_finish(c.dvals, n, st.base, len, *pint, *plen, out3, c.stream, signal_word(c, seq), seq));
     wait_done(c, seq);
     const volatile uint32_t *h = (const volatile uint32_t *)c.pres;
