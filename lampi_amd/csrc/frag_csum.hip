@@ -1197,24 +1197,48 @@ struct StreamChain {
     uint32_t mid;      // 1: the chain starts inside fragment `head`
 };
 
+// a * b mod P (CRC-32/MPEG-2, normal MSB-first register domain), Horner over b's bits
+__host__ __device__ constexpr uint32_t gf_mulmod(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+    for (int i = 31; i >= 0; --i) {
+        r = (r << 1) ^ ((r >> 31) ? 0x04C11DB7u : 0u);
+        r ^= ((b >> i) & 1u) ? a : 0u;
+    }
+    return r;
+}
+// kRowShift[j] = x^(8 * 4096 * 2^j) mod P: the shift of a register past 2^j rows of zero bytes
+struct RowShifts {
+    uint32_t k[20];
+};
+constexpr RowShifts row_shifts() {
+    RowShifts t{};
+    uint32_t x = 2u;                                  // x^1
+    for (int i = 0; i < 15; ++i) x = gf_mulmod(x, x);  // x^(2^15) = x^(8 * 4096)
+    for (int j = 0; j < 20; ++j) {
+        t.k[j] = x;
+        x = gf_mulmod(x, x);
+    }
+    return t;
+}
+constexpr RowShifts kRowShift = row_shifts();
+static_assert(gf_mulmod(0x80000000u, 2u) == 0x04C11DB7u, "x^31 * x = x^32 = P - x^32");
+
 // C (swapped domain) after 64*m zero bytes, m < 2^26: the low six bits of m through lane
-// (63 - (m & 63))'s combine column in LDS, the rows (4096 bytes = 2^12) through the image's
-// shift-by-2^e columns (normal domain, e = 12..31)
+// (63 - (m & 63))'s combine column in LDS, the rows (h = m >> 6, 4096 bytes each) as products
+// with compile-time constants x^(8 * 4096 * 2^j) mod P -- no memory traffic (the shift-by-2^e
+// columns of the table image took one dependent round of 32 global loads per bit of h, and a
+// fragment spanning all chains of a workgroup joined that way serially: 65,456-byte host calls
+// spent ~20 us there)
 __device__ uint32_t shift_pieces(const uint32_t *lds, const uint32_t *__restrict__ img, uint32_t C, uint64_t m) {
+    (void)img;
     const uint32_t l = (uint32_t)(m & 63u);
     if (l) C = combine_at(lds, comb_col(63u - l), C);
-    uint32_t h = (uint32_t)(m >> 6);
+    const uint32_t h = (uint32_t)(m >> 6);
     if (h) {
         uint32_t c = __builtin_bswap32(C);
-        while (h) {
-            const uint32_t e = 12u + (uint32_t)__builtin_ctz(h);
-            h &= h - 1u;
-            const uint32_t *col = img + kImgPow2Cols + e * 32u;
-            uint32_t r = 0;
 #pragma unroll
-            for (int b = 0; b < 32; ++b) r ^= ((c >> b) & 1u) ? col[b] : 0u;
-            c = r;
-        }
+        for (int j = 0; j < 20; ++j)
+            if ((h >> j) & 1u) c = gf_mulmod(c, kRowShift.k[j]);
         C = __builtin_bswap32(c);
     }
     return C;
