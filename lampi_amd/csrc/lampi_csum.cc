@@ -172,7 +172,7 @@ HostCtx &host_ctx() {
         LAMPI_CHECK(hipHostMalloc((void **)&ctx.pres, 8 * sizeof(uint64_t), kCoherent));
         ctx.pres[kSignalWord] = ctx.seq = 0;
         LAMPI_CHECK(hipHostMalloc((void **)&ctx.hdesc, kMaxPieces * sizeof(lampi_frag_desc), kCoherent));
-        LAMPI_CHECK(hipHostMalloc((void **)&ctx.zpin, kZeroCopy, kCoherent));
+        LAMPI_CHECK(hipHostMalloc((void **)&ctx.zpin, kZeroCopy + 64, kCoherent));  // + slack: aligned word reads past a body (uicsum)
         LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.zpin_d, ctx.zpin, 0));
         LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.pres_d, ctx.pres, 0));
         LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.hdesc_d, ctx.hdesc, 0));

@@ -325,7 +325,9 @@ def test_host_api_matches_reference_semantics(cuda, oracle):
 
     rng = np.random.default_rng(7)
     data = rng.integers(0, 256, size=3 << 20, dtype=np.uint8)
-    for n in [0, 1, 3, 4, 5, 100, 4096, 65456, 65537, 1 << 20, (3 << 20) - 5]:
+    # 8 KiB..256 KiB: the zero-copy sizes (CRC in 4 KiB pieces, SUM in one kernel reading aligned
+    # words past the body's end: 262,144 is the largest zero-copy call)
+    for n in [0, 1, 3, 4, 5, 100, 4096, 8192, 8193, 65456, 65537, 262143, 262144, 262145, 1 << 20, (3 << 20) - 5]:
         for off in (0, 1, 3):
             src = data[off:off + n]
             p = int(rng.integers(0, 2**32))
