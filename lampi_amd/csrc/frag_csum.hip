@@ -1626,6 +1626,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     __shared__ uint32_t marks[kChains * 64];      // boundary scratch, 64 words per chain
     __shared__ StreamChain schain[kChains];
     __shared__ uint32_t chead[kChains], sopen[kChains], shead[kChains];
+    __shared__ uint32_t sjoin[kChains];           // stream_join: the parts of the fragment chain c starts
     __shared__ uint32_t sres[kFragsPerWg];        // the workgroup's checksums, stored at the end
     __shared__ uint64_t wpieces[kWv];
     __shared__ uint32_t wcount[kWv];
@@ -1635,7 +1636,10 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
 
     FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
     if (t < nwg) mine = src.get(base + t);
-    if (t < kChains) chead[t] = 0u;
+    if (t < kChains) {
+        chead[t] = 0u;
+        sjoin[t] = 0u;  // read after the rows
+    }
     auto nopre = [] {};
     if constexpr (kSum) {
         __syncthreads();
@@ -1727,26 +1731,43 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
         stream_body<false, kD, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                                sopen + kK * wave, shead + kK * wave, zero, sres, out);
     __syncthreads();
-    // stream_join: fragments crossing chain starts.  Thread c owns the fragment crossing chain c's
-    // start when that is the first chain start inside it; the part before is chain c-1's open
-    // value, every later part is shifted in by its length.
-    if (t >= 1 && t < kChains && schain[t].mid) {
-        const uint32_t f = schain[t].head;
-        if (schain[t - 1].rs <= sstart[f]) {
-            const uint64_t ef = sstart[f + 1];
-            uint32_t C = sopen[t - 1];
-            for (uint32_t c = t; c < kChains; ++c) {
-                const uint64_t lo = schain[c].rs, hi = schain[c].end;
-                if (hi == lo) continue;
-                if (ef <= hi) {
-                    C = kSum ? C + shead[c] : shift_pieces(lds, img, C, ef - lo) ^ shead[c];
-                    break;
-                }
-                C = kSum ? C + sopen[c] : shift_pieces(lds, img, C, hi - lo) ^ sopen[c];
+    // stream_join: fragments crossing chain starts, every chain's part at once.  A fragment f
+    // crossing chains a (where it starts) .. b (where it ends) is the XOR (SUM: sum) of each
+    // chain's part shifted past the rest of f: chains a..b-1 leave their open value (sopen),
+    // chain b its final part (shead).  Thread c adds chain c's part of the fragment it starts
+    // inside (head, mid) and of the fragment it starts that crosses its end into sjoin[start
+    // chain]; the start chain's thread then stores the result.  (Round 1 joined the parts one
+    // after another in one thread: a fragment spanning all twelve chains took eleven dependent
+    // shifts, 256 KiB fragments one per workgroup ran at 47%.)
+    uint32_t gown = ~0u;  // the crossing fragment this thread's chain starts (its result is stored here)
+    if (t < kChains && schain[t].rs < schain[t].end) {
+        const uint64_t rs = schain[t].rs, end = schain[t].end;
+        if (schain[t].mid) {  // part of the fragment this chain starts inside
+            const uint32_t h = schain[t].head;
+            const uint64_t sf = sstart[h], ef = sstart[h + 1];
+            uint32_t a = t;
+            while (a > 0 && schain[a - 1].rs > sf) --a;  // a - 1: the chain holding h's first piece
+            const uint32_t v = ef <= end ? shead[t] : (kSum ? sopen[t] : shift_pieces(lds, img, sopen[t], ef - end));
+            if (kSum)
+                atomicAdd(&sjoin[a - 1], v);
+            else
+                atomicXor(&sjoin[a - 1], v);
+        }
+        if (t + 1 < kChains) {  // the fragment open at this chain's end, when it starts here
+            const uint32_t g = schain[t + 1].head;
+            const uint64_t sg = sstart[g], eg = sstart[g + 1];
+            if (sg >= rs && sg < end && eg > end) {
+                const uint32_t v = kSum ? sopen[t] : shift_pieces(lds, img, sopen[t], eg - end);
+                if (kSum)
+                    atomicAdd(&sjoin[t], v);
+                else
+                    atomicXor(&sjoin[t], v);
+                gown = g;
             }
-            sres[sj[f]] = kSum ? C : __builtin_bswap32(C);
         }
     }
+    __syncthreads();
+    if (gown != ~0u) sres[sj[gown]] = kSum ? sjoin[t] : __builtin_bswap32(sjoin[t]);
     __syncthreads();
     if (t < nwg) emit(src, out, base + t, sres[t], mine);
 }
