@@ -791,7 +791,7 @@ def run_bcopy(args):
     _, kern_copy = timed(lambda: dst.copy_(src))
     moved = 2.0 * n * L
     achieved = moved / kern / 1e9
-    kname = ("crc_regular_kernel<copy>" if mode == dv.CRC32 else "sum_regular_kernel<copy>")
+    kname = ("crc_regular_kernel<copy>" if mode == dv.CRC32 else "sum_copy_row_kernel")
     print(json.dumps({
         "metric": "device-resident fused copy+checksum GiB/s of payload (bcopy); % of HBM roofline",
         "value": round(n * L / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,

@@ -77,6 +77,25 @@ typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
 typedef __attribute__((address_space(1))) const u32x4_a1 gu32x4_a1;  // unaligned 16-byte loads
 typedef __attribute__((address_space(1))) u32x4_a4 gwu32x4_a4;
 
+// Copy destinations are written with non-temporal stores (the `nt` bit: streamed past the caches
+// the payload is not re-read from): +1.3 to +2 points of read + write bandwidth in the copy shapes
+// measured (tools/microbench/copy5.hip, profiles/r02_copy5.txt).  -DLAMPI_NT_STORES=0 for A/B runs.
+#ifndef LAMPI_NT_STORES
+#define LAMPI_NT_STORES 1
+#endif
+#if LAMPI_NT_STORES
+#define LAMPI_ST_NT " nt"
+#else
+#define LAMPI_ST_NT ""
+#endif
+__device__ __forceinline__ void st16(gwu32x4_a4 *p, const u32x4 &v) {
+#if LAMPI_NT_STORES
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 struct FragInfo {
     gbyte *addr;
     uint32_t len;      // bytes checksummed
@@ -337,10 +356,10 @@ __device__ __forceinline__ void row_words(const Row &r, uint32_t d[16]) {
 template <int kS = 16>
 __device__ __forceinline__ void store_row(gwbyte *p, const Row &r) {
     asm volatile(
-        "global_store_dwordx4 %0, %1, off\n\t"
-        "global_store_dwordx4 %0, %2, off offset:%5\n\t"
-        "global_store_dwordx4 %0, %3, off offset:%6\n\t"
-        "global_store_dwordx4 %0, %4, off offset:%7\n\t"
+        "global_store_dwordx4 %0, %1, off" LAMPI_ST_NT "\n\t"
+        "global_store_dwordx4 %0, %2, off offset:%5" LAMPI_ST_NT "\n\t"
+        "global_store_dwordx4 %0, %3, off offset:%6" LAMPI_ST_NT "\n\t"
+        "global_store_dwordx4 %0, %4, off offset:%7" LAMPI_ST_NT "\n\t"
         "s_nop 1"
         :
         : "v"(p), "v"(r.q[0]), "v"(r.q[1]), "v"(r.q[2]), "v"(r.q[3]), "n"(kS), "n"(2 * kS), "n"(3 * kS)
@@ -564,7 +583,7 @@ __device__ __forceinline__ void store64(uint8_t *dst, long long o, const uint32_
         if (a16 && o >= lo && o + 64 <= hi) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                *(gwu32x4 *)(dst + o + 16 * k) = u32x4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]};
+                st16((gwu32x4_a4 *)(dst + o + 16 * k), u32x4{d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]});
             return;
         }
 #pragma unroll
@@ -617,7 +636,7 @@ __device__ __forceinline__ void store_row_coalesced(uint32_t *stage, uint8_t *ds
                 *(gwuint *)(c + 8) = v[i].z;
                 *(gwuint *)(c + 12) = v[i].w;
             } else {
-                *(gwu32x4_a4 *)c = v[i];  // dst is 4-byte aligned (dword-aligned dwordx4 store)
+                st16((gwu32x4_a4 *)c, v[i]);  // dst is 4-byte aligned (dword-aligned dwordx4 store)
             }
         }
     }
@@ -646,7 +665,7 @@ __device__ __forceinline__ void store_row_coalesced_masked(uint32_t *stage, uint
         __builtin_amdgcn_wave_barrier();
         const long long c = row0 + h * 1024 + 16 * lane;
         if (c >= lo && c + 16 <= hi) {
-            *(gwu32x4_a4 *)(dst + c) = v;
+            st16((gwu32x4_a4 *)(dst + c), v);
         } else if (c + 16 > lo && c < hi) {
             store_word(dst, c, v.x, lo, hi);
             store_word(dst, c + 4, v.y, lo, hi);
@@ -932,7 +951,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
                     gwbyte *q = (gwbyte *)(cur.dst + row0) + 16 * lane;
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        *(gwu32x4_a4 *)(q + 1024 * c) = u32x4{d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]};
+                        st16((gwu32x4_a4 *)(q + 1024 * c), u32x4{d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]});
                     stored = true;
                 }
                 rows_to_pieces(lds + (kLdsBytes + (threadIdx.x >> 6) * kArea) / 4, d, lane);
@@ -2186,7 +2205,7 @@ __global__ void __launch_bounds__(64 * kWv) sum_rows_kernel(Src src, size_t n, u
                     gwbyte *q = (gwbyte *)(cur.db + row0) + 16 * lane;
 #pragma unroll
                     for (int c = 0; c < 4; ++c)
-                        *(gwu32x4_a4 *)(q + 1024 * c) = u32x4{d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]};
+                        st16((gwu32x4_a4 *)(q + 1024 * c), u32x4{d[4 * c], d[4 * c + 1], d[4 * c + 2], d[4 * c + 3]});
                     stored = true;
                 } else {
                     rows_to_pieces(area, d, lane);
@@ -2250,51 +2269,35 @@ __global__ void __launch_bounds__(64 * kWv) sum_rows_kernel(Src src, size_t n, u
     }
 }
 
-// SUM fast path for regular batches (frag_len % 4096 == 0, 16-byte aligned base): no tables,
-// hence no staging, so it uses the fastest measured read shape -- one fragment per wave,
-// short-lived 256-thread workgroups in address order, up to four rows (16 x dwordx4 per
-// lane) in flight at once.
-template <bool kCopy = false>
-__global__ void __launch_bounds__(kBlock) sum_regular_kernel(const uint8_t *__restrict__ base, uint32_t n,
-                                                             size_t frag_len, uint32_t *__restrict__ out,
-                                                             uint8_t *__restrict__ dst = nullptr,
-                                                             size_t dst_stride = 0) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t f = uniform(blockIdx.x * kWaves + (threadIdx.x >> 6));
-    if (f >= n) return;
-    const uint32_t R = (uint32_t)(frag_len / kRowBytes);
-    // the sum is order-free: the copy moves rows in the coalesced layout (1 KiB per store
-    // instruction), the read-only sum keeps lane-contiguous 64-byte pieces
-    constexpr int kS = kCopy ? kRowBytes / 4 : 16;
-    const uint64_t lo = (uint64_t)lane * (kCopy ? kChunkBytes : kLaneBytes);
-    gbyte *p = (gbyte *)(base + (uint64_t)f * frag_len + lo);
-    gwbyte *q = kCopy ? (gwbyte *)(dst + (uint64_t)f * dst_stride + lo) : nullptr;
-    uint32_t acc = 0;
-    uint32_t r = 0;
-    for (; r + 4 <= R; r += 4) {
-        u32x4 v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)(r + k / 4) * kRowBytes + kS * (k & 3));
-        if constexpr (kCopy) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) *(gwu32x4_a4 *)(q + (uint64_t)(r + k / 4) * kRowBytes + kS * (k & 3)) = v[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+// SUM fused copy (bcopy_uicsum) of messages whose fragments are >= 4 KiB and a multiple of 16
+// bytes long, from a 16-byte-aligned base to dword-aligned destinations: the textbook copy shape --
+// one short-lived 256-thread workgroup per 4 KiB row, one 16-byte chunk per thread, non-temporal
+// stores -- which copies at 78-81% of read + write against 72-74% for one fragment per wave
+// (tools/microbench/copy5.hip, profiles/r02_copy5.txt).  The row's sum goes to out[f] (a one-row
+// fragment) or is added atomically into out[f], zeroed beforehand (the sum is order-free and a row
+// starts on the fragment's word grid).  Fragment f spans [f*frag_len, min(.., msg_len)).
+__global__ void __launch_bounds__(kBlock) sum_copy_row_kernel(const uint8_t *__restrict__ base, size_t msg_len,
+                                                              size_t frag_len, uint32_t rpf, uint32_t *__restrict__ out,
+                                                              uint8_t *__restrict__ dst, size_t dst_stride) {
+    __shared__ uint32_t part[kWaves];
+    const uint32_t f = uniform(blockIdx.x / rpf), r = uniform(blockIdx.x - f * rpf);
+    const uint64_t fo = (uint64_t)f * frag_len, o = (uint64_t)r * kRowBytes + 16u * threadIdx.x;
+    const uint64_t flen = msg_len - fo < frag_len ? msg_len - fo : frag_len;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (o < flen) {  // flen % 16 == 0: a chunk is wholly inside or wholly outside
+        v = *(gu32x4 *)(base + fo + o);
+        st16((gwu32x4_a4 *)(dst + (uint64_t)f * dst_stride + o), v);
     }
-    for (; r < R; ++r) {
-        u32x4 v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = *(gu32x4 *)(p + (uint64_t)r * kRowBytes + kS * k);
-        if constexpr (kCopy) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) *(gwu32x4_a4 *)(q + (uint64_t)r * kRowBytes + kS * k) = v[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc += v[k].x + v[k].y + v[k].z + v[k].w;
+    const uint32_t a = wave_add(v.x + v.y + v.z + v.w);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t s = part[0] + part[1] + part[2] + part[3];
+        if (rpf == 1)
+            out[f] = s;
+        else
+            atomicAdd(out + f, s);
     }
-    acc = wave_add(acc);
-    if (lane == 0) out[f] = acc;
 }
 
 // ---- headers and receive-side verification -----------------------------------------------
@@ -2983,9 +2986,16 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                              (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes), img, out, s, frag_len);
         return hipGetLastError();
     }
-    if (regular) {
-        hipLaunchKernelGGL(sum_regular_kernel<true>, dim3((unsigned)((n + kWaves - 1) / kWaves)), dim3(kBlock), 0, s,
-                           base, (uint32_t)n, frag_len, out, dst, dst_stride);
+    const uint64_t rpf = (frag_len + kRowBytes - 1) / kRowBytes;
+    if (msg_len != 0 && frag_len >= kRowBytes && frag_len % 16 == 0 && msg_len % 16 == 0 &&
+        ((uintptr_t)base & 15u) == 0 && ((uintptr_t)dst & 3u) == 0 && dst_stride % 4 == 0 &&
+        n * rpf <= 0xFFFFFFFFull) {  // one workgroup per 4 KiB row (sum_copy_row_kernel)
+        if (rpf > 1) {
+            const hipError_t e = hipMemsetAsync(out, 0, n * sizeof(uint32_t), s);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(sum_copy_row_kernel, dim3((unsigned)(n * rpf)), dim3(kBlock), 0, s, base, msg_len, frag_len,
+                           (uint32_t)rpf, out, dst, dst_stride);
         return hipGetLastError();
     }
     if (frag_len >= 4 * (size_t)kRowBytes && msg_len != 0) {  // large fragments: row items (MsgRowCopySource)

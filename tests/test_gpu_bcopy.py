@@ -207,6 +207,12 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     (16385 * 2000 + 3, 16385, 16385 + 7, 1),  # 5 rows, the last 1 byte; byte-misaligned destinations
     (40000 * 1500 + 12345, 40000, 40000, 0),  # a short last fragment with fewer rows
     (20001 * 777, 20001, 20480, 8),           # odd length, destinations at +8
+    # SUM: 16-byte-multiple fragments of 4 KiB and more go one workgroup per 4 KiB row
+    # (sum_copy_row_kernel): partial last rows, short last fragments, dword-aligned slots
+    (65456 * 300, 65456, 65536, 72),          # GM send: 65,456-byte payloads after the 72-byte header
+    (65456 * 200 + 4000, 65456, 65536 + 4, 4),  # a last fragment of 4,000 bytes (one partial row)
+    (4112 * 3000, 4112, 4112 + 12, 12),       # a second row of 16 bytes per fragment
+    (49152 * 100 + 4096 * 5, 49152, 49152, 0),  # a last fragment of 5 of its 12 rows
 ])
 def test_msg_bcopy(cuda, oracle, mode, msg_len, frag_len, stride, dst_off):
     """lampi_msg_bcopy: fragment k -> dst + k*stride with its checksum fused; gap bytes untouched."""
