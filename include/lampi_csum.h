@@ -228,7 +228,8 @@ typedef struct lampi_recv_desc {
  *                      initial register or 0, CheckData passes a zero length).
  * d_copied[i] = lengthToCopy, or -1 when the checksum differs (CopyToApp's return value);
  * d_csum[i] = the calculated checksum (what the reference logs as "calculated=");
- * the expected checksum of fragment i is the 32-bit value at d_expected + i*expected_stride --
+ * the expected checksum of fragment i is the 32-bit value at d_expected + i*expected_stride (read
+ * for every i, whatever its descriptor says) --
  * e.g. dataChecksum (@64) of an array of 72-byte gmHeaderData records (expected_stride 72).
  * d_mask: bit (i % 32) of word i / 32 set iff fragment i is corrupt (zeroed by the call);
  * *d_nbad: number of corrupt fragments.  One wavefront per fragment (CRC) / 16-byte-piece
