@@ -2873,6 +2873,27 @@ static uint32_t frags_per_wg(size_t n, size_t frag_len = 0) {
 
 // crc_stream_kernel: ring depth and chains per wave (measured, tools/microbench/frags_sweep.hip)
 constexpr int kStreamD = 2, kStreamK = 1, kStreamWv = 12, kStreamCap = 6;
+// the SUM piece streams (no tables, so no per-workgroup staging to amortise): waves per
+// workgroup, waves per SIMD and fragments per workgroup.  Same-box A/B (profiles/r02_sum_stream/,
+// two rounds): 48 fragments per 768-thread workgroup config C SUM 74.2-76.8 -> 78.1-78.3%, 4 KiB
+// descriptors 78.9 -> 79.1-80.3%; 24 / 32 / 64 fragments 71 / 76.5 / 77.5%; 8-wave workgroups 76.6%;
+// 256-thread workgroups of 8 / 16 / 32 fragments 78.2-78.9 / 77.5-77.9 / 76.4% (4 KiB descriptors
+// 74 / 80 / 77%); 8 waves per SIMD spills (scratch next to the asm load ring: not run).
+#ifndef LAMPI_SUM_WV
+#define LAMPI_SUM_WV 12
+#endif
+#ifndef LAMPI_SUM_CAP
+#define LAMPI_SUM_CAP 6
+#endif
+#ifndef LAMPI_SUM_FPG
+#define LAMPI_SUM_FPG 48
+#endif
+constexpr int kSumWv = LAMPI_SUM_WV, kSumCap = LAMPI_SUM_CAP;
+static uint32_t sum_frags_per_wg(size_t n, size_t frag_len = 0) {
+    uint32_t fpg = LAMPI_SUM_FPG;
+    while (fpg > 3 && n / fpg < 256) fpg >>= 1;
+    return spread_fpw(fpg, n, 1, frag_len);
+}
 
 static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg - 1) / fpg)); }
 
@@ -3037,9 +3058,9 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (img) {  // piece streams (img: the zero chunk)
-        const uint32_t fpg = frags_per_wg(n);
-        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, true, kStreamWv, kStreamCap>),
-                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out);
+        const uint32_t fpg = sum_frags_per_wg(n);
+        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, true, kSumWv, kSumCap>),
+                           frags_grid(n, fpg), dim3(64 * kSumWv), 0, s, DescSource{d}, n, fpg, img, out);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
@@ -3056,9 +3077,9 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
         return launch_regular<true>(base, n, frag_len, 0u, out, nullptr, s);
     }
     if (img) {
-        const uint32_t fpg = frags_per_wg(n, frag_len);
-        hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, true, kStreamWv, kStreamCap>),
-                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
+        const uint32_t fpg = sum_frags_per_wg(n, frag_len);
+        hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, true, kSumWv, kSumCap>),
+                           frags_grid(n, fpg), dim3(64 * kSumWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
