@@ -2865,8 +2865,11 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
 // With the fragment length known (messages), large fragments are spread as in spread_fpw
 // (16,404 x 65,456 bytes: 6 fragments per workgroup, not 48: CRC 55 -> 62%, SUM 62 -> 74%;
 // profiles/r02_bigfrag_ab.txt).
+#ifndef LAMPI_CRC_FPG
+#define LAMPI_CRC_FPG 96
+#endif
 static uint32_t frags_per_wg(size_t n, size_t frag_len = 0) {
-    uint32_t fpg = 96;
+    uint32_t fpg = LAMPI_CRC_FPG;
     while (fpg > 3 && n / fpg < 256) fpg >>= 1;
     return spread_fpw(fpg, n, 1, frag_len);
 }

@@ -122,12 +122,12 @@ def test_bcopy_batch_random(cuda, oracle):
 @pytest.mark.parametrize("n,layout", [(40, "aligned"), (40, "src8"), (3000, "mixed"), (30000, "mixed"),
                                       (30000, "src8")])
 def test_bcopy_batch_sum_streams(cuda, oracle, n, layout):
-    """SUM through the fused-copy piece streams (16-byte pieces, coalesced stores, trash slots for
-    masked lanes, byte stores for a piece ending past copylen).  Random lengths incl. 0 and odd
-    ones, copylen =/</> csumlen.  "src8": every source at +8 (payload after a 72-byte GM header:
-    the two-load funnel variant); "mixed": some sources misaligned (funnel workgroups) and some
-    destinations misaligned (byte-misaligned ones send their workgroups to sum_rows_kernel,
-    4/8/12 stay on the streams), interleaved in one batch.  Small batches make fragments span chains."""
+    """SUM fused copies of descriptor batches (sum_copy_wg_kernel: one workgroup per fragment,
+    unaligned 16-byte loads and stores, the last 1-15 bytes and the chunk a short copy ends in
+    handled after the loop).  Random lengths incl. 0 and odd ones, copylen =/</> csumlen.
+    "src8": every source at +8 (payload after a 72-byte GM header); "mixed": some sources and
+    some destinations byte-misaligned, interleaved in one batch.  (The names are round 1's, when
+    these batches ran on 16-byte-piece streams.)"""
     rng = np.random.default_rng(n + len(layout))
     big = rng.random(n) < (0.5 if n == 40 else 0.05)
     cl = np.where(big, rng.integers(0, 300000, size=n), rng.integers(0, 5000, size=n))
@@ -238,3 +238,41 @@ def test_msg_bcopy(cuda, oracle, mode, msg_len, frag_len, stride, dst_off):
     got = dv.as_u32(dv.msg_bcopy(msg, frag_len, dst[dst_off:], stride, partial=0x0BADF00D, mode=mode))
     want = oracle.desc_batch(host, offs, lens, np.full(n, 0x0BADF00D, np.uint32) if mode == 0 else None, mode)
     _assert_same(got, want, dst.cpu().numpy(), want_dst, lambda i: (i, int(lens[i])))
+
+
+def test_sum_copy_grid_loop(cuda):
+    """SUM copies beyond one grid (2^22 workgroups): the workgroups of sum_copy_wg_kernel (descriptor
+    items) and sum_copy_row_kernel (message rows) take several items each.  Checked against the
+    read-only SUM kernels (lampi_frag_csum_batch / lampi_msg_csum, parity-tested against the
+    oracle elsewhere) and the copied bytes against the source."""
+    import torch
+
+    dv = _dv()
+    n = (1 << 22) + 4099  # descriptor items: 64-byte fragments, every 3rd copied only in part
+    L = 64
+    src = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(src, seed=31)
+    dst = torch.zeros(n * L + 64, dtype=torch.uint8, device=cuda)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    copylens = np.where(np.arange(n) % 3 == 0, 37, L).astype(np.int64)
+    descs = dv.make_copy_descs(src, offs, dst, offs + np.uint64(4), copylens, np.full(n, L))
+    got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=dv.SUM32))
+    want = dv.as_u32(dv.frag_csum_batch(dv.make_descs(src, offs, np.full(n, L)), mode=dv.SUM32))
+    assert np.array_equal(got, want)
+    d = dst[4:4 + n * L].view(n, L)
+    s = src.view(n, L)
+    full = torch.from_numpy(np.arange(n) % 3 != 0).to(cuda)
+    assert torch.equal(d[full], s[full])
+    assert torch.equal(d[~full][:, :37], s[~full][:, :37])
+    assert not bool(d[~full][:, 37:].any())  # the residue is checksummed, not copied
+    del src, dst, descs, d, s
+
+    nf = (1 << 20) + 3  # message rows: 4 rows per 16 KiB fragment, 2^22 + 12 rows
+    F = 16384
+    msg = torch.empty(nf * F, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(msg, seed=32)
+    out = torch.empty(nf * F + 16, dtype=torch.uint8, device=cuda)
+    got = dv.as_u32(dv.msg_bcopy(msg, F, out[16:], F, mode=dv.SUM32))
+    want = dv.as_u32(dv.msg_csum(msg, F, mode=dv.SUM32))
+    assert np.array_equal(got, want)
+    assert torch.equal(out[16:16 + nf * F], msg)
