@@ -1946,7 +1946,9 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // kV*4096-byte fragment (launch with frag_len = kV*4096, n = fragments / kV): chain c of a wave
 // reads kV consecutive fragments one after the other instead of one.
 // kSum: the same schedule computes uicsum instead (no tables; the LDS stays allocated so the
-// kernel keeps the two-workgroups-per-CU occupancy the schedule was measured at).
+// kernel keeps the two-workgroups-per-CU occupancy the schedule was measured at: without it, five
+// workgroups per CU, config B SUM 78.7-80.4 -> 79.4-79.5%, with half the fragments per wave too
+// 79.6-79.7%, 16 KiB fragments 79.1-79.2 -> 78.5%; profiles/r02_sum_regular/).
 // kWv: waves per workgroup (the table builders use the first 256 threads); kCap > 0 asks the
 // compiler for that many waves per SIMD.
 template <int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
