@@ -5,6 +5,8 @@
 // property by striding over the grid: iteration k of workgroup b copies 4 KiB block b + k*G, one
 // float4 per thread (1 KiB per wave-instruction), with D blocks in flight per thread.
 //   GS T=256 lds=L D=d G=g : g workgroups (g = CUs x resident workgroups per CU), L bytes of LDS
+//   GS+lookups ... N=n : the same with n data-dependent LDS lookups per 16-byte chunk (a proxy for
+//                        the CRC's table lookups: 18 ~ the product's 1.1 per byte, 28 ~ 1.75 per byte)
 // Payload random.  Three interleaved rounds x 4 launches, 8 GiB (16 GiB moved).
 // Build: hipcc --offload-arch=gfx950 -O3 copy6.hip -o copy6
 #include <hip/hip_runtime.h>
@@ -76,6 +78,48 @@ done:
     if (lds[(t + 1) % T] == 0xFFFFFFFFu) sink[0] = 1;
 }
 
+
+// cp_gs plus a CRC-like load: N data-dependent ds_read_b32 per 16-byte chunk (addresses formed
+// from the chunk's bytes, XOR-accumulated), tables of LDS bytes (filled once), result to a sink
+template <int T, int LDS, int D, int N>
+__global__ void __launch_bounds__(T) cp_gs_lk(const u32x4 *__restrict__ s, u32x4 *__restrict__ d, size_t nblk,
+                                              unsigned *sink) {
+    __shared__ unsigned lds[LDS / 4];
+    for (unsigned i = threadIdx.x; i < LDS / 4; i += T) lds[i] = i * 0x9E3779B9u;
+    __syncthreads();
+    constexpr unsigned kMask = (LDS / 4 >= 8192 ? 8192 : 4096) - 1;  // index range (32 / 16 KiB)
+    constexpr int kPer = T / 256;
+    const size_t G = gridDim.x;
+    const size_t b0 = blockIdx.x;
+    const unsigned t = threadIdx.x;
+    u32x4 v[D];
+    unsigned x = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const size_t blk = b0 + (size_t)j * G;
+        if (blk * kPer < nblk) v[j] = s[blk * 256 * kPer + t];
+    }
+    for (size_t k = 0;; k += D) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const size_t blk = b0 + (k + j) * G;
+            if (blk * kPer >= nblk) goto done;
+            __builtin_nontemporal_store(v[j], d + blk * 256 * kPer + t);
+            unsigned w = v[j].x ^ x;
+#pragma unroll
+            for (int q = 0; q < N; ++q) {
+                const unsigned src = q % 4 == 0 ? v[j].x : q % 4 == 1 ? v[j].y : q % 4 == 2 ? v[j].z : v[j].w;
+                w = lds[((w >> (q & 7)) ^ src ^ (t << 3)) & kMask] ^ (w << 1);
+            }
+            x ^= w;
+            const size_t nb = b0 + (k + j + D) * G;
+            if (nb * kPer < nblk) v[j] = s[nb * 256 * kPer + t];
+        }
+    }
+done:
+    if (x == 0x12345678u) sink[0] = x;
+}
+
 int main(int argc, char **argv) {
     const size_t bytes = argc > 1 ? strtoull(argv[1], 0, 0) : (8ull << 30);
     unsigned char *s, *d;
@@ -116,6 +160,16 @@ int main(int argc, char **argv) {
     GS(256, 40000, 8, 1024, true)
     GS(256, 30000, 4, 1280, true)
     GS(256, 30000, 8, 1280, true)
+#define GSL(L, DD, G, NN)                                                                                          \
+    add("GS+lookups T=256 lds=" #L " D=" #DD " G=" #G " N=" #NN,                                                  \
+        [=] { hipLaunchKernelGGL((cp_gs_lk<256, L, DD, NN>), dim3(G), dim3(256), 0, 0, S, D, nblk, sink); });
+    GSL(65536, 8, 512, 0)
+    GSL(65536, 8, 512, 18)
+    GSL(65536, 8, 512, 28)
+    GSL(30000, 8, 1280, 0)
+    GSL(30000, 8, 1280, 18)
+    GSL(30000, 8, 1280, 28)
+    GSL(30000, 4, 1280, 28)
     for (auto &v : vs) {  // warm
         v.f();
         CK(hipGetLastError());
