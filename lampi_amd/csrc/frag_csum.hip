@@ -2111,9 +2111,9 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 }
 
 // ---- SUM -------------------------------------------------------------------------------
-// SUM fused copies (bcopy_uicsum descriptors, the receive step, message fragments from 2 KiB and
-// the rows of longer ones) in the textbook copy shape: one short-lived 256-thread workgroup per
-// fragment, thread t the 16-byte chunk at 16t of each 4 KiB row (unaligned loads and stores, any
+// SUM fused copies (bcopy_uicsum descriptors, the receive step, ragged message fragments and the
+// rows of longer ones) in the textbook copy shape: one short-lived 128-thread workgroup per
+// fragment, thread t the 16-byte chunk at 16t of each 2 KiB row (unaligned loads and stores, any
 // alignment: the memory pipeline splits them at line boundaries; 1 KiB per wave-instruction both
 // ways), non-temporal stores, the next row loaded before this one is stored.  The sum is
 // order-free and every chunk starts on the fragment's word grid.  Copy shape: 4 KiB rows 78-81% of
@@ -2152,10 +2152,20 @@ __device__ __forceinline__ void store_head16(gwbyte *q, const u32x4 &v, uint32_t
     }
 }
 
-template <class Src>
-__global__ void __launch_bounds__(kBlock) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
+// Threads per workgroup (one fragment each), same-box A/B (profiles/r02_sumcopy/ab_wgT/, ab_row/):
+// 128 against 256: 4 KiB descriptors 74.4 -> 79.1-79.2%, +8 sources 74 -> 79.6%, the receive step
+// 72 -> 75-77%, fragments of 64 B-2 KiB 1.5-2x faster (1 GiB of 1,976-byte fragments 0.80 ->
+// 0.53 ms, now ahead of sum_rows_kernel's 0.61 at every size), 16 KiB / 65,456-byte descriptors
+// 71.5 / 61.4 -> 69.9 / 58.1%; 64 threads: small fragments faster still (64 B 3.4x) but +8 and +1
+// destinations 66%; 192: 75.7%.  The row kernel keeps 256 (128 / 64: GM slots 75 -> 71 / 64%).
+#ifndef LAMPI_SUMWG_T
+#define LAMPI_SUMWG_T 128
+#endif
+template <class Src, int kT = LAMPI_SUMWG_T>
+__global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
     static_assert(Src::kCopy && !Src::kPhase, "word-grid copy sources only");
-    __shared__ uint32_t part[2][kWaves];  // by iteration parity: one barrier per fragment
+    constexpr uint32_t kW = kT / 64;
+    __shared__ uint32_t part[2][kW];  // by iteration parity: one barrier per fragment
     const uint32_t t = threadIdx.x;
     uint32_t it = 0;
     // a grid has at most 2^32 - 1 threads: beyond kMaxWgGrid fragments a workgroup takes several
@@ -2165,16 +2175,16 @@ __global__ void __launch_bounds__(kBlock) sum_copy_wg_kernel(Src src, size_t n, 
         gwbyte *q = (gwbyte *)uniform64((uint64_t)(uintptr_t)fi.dst);
         const uint32_t len = uniform(fi.len), clen = uniform(fi.copylen);  // clen <= len
         const uint32_t nfull = len / 16u, cfull = clen / 16u;  // whole 16-byte chunks
-        const uint32_t R = (nfull + 255u) / 256u;
-        // the loop moves whole chunks only (chunk c = 256 r + t); the chunk the copy ends inside
+        const uint32_t R = (nfull + kT - 1) / kT;
+        // the loop moves whole chunks only (chunk c = kT r + t); the chunk the copy ends inside
         // is kept (vc) and the fragment's partial last chunk is read after the loop
         uint32_t acc = 0;
         u32x4 v = {0u, 0u, 0u, 0u}, vc = {0u, 0u, 0u, 0u};
         if (t < nfull) v = *(gu32x4_a1 *)(p + 16u * t);
         for (uint32_t r = 0; r < R; ++r) {
-            const uint32_t c = 256u * r + t;
+            const uint32_t c = kT * r + t;
             u32x4 nv = {0u, 0u, 0u, 0u};
-            if (c + 256u < nfull) nv = *(gu32x4_a1 *)(p + 16u * (c + 256u));
+            if (c + kT < nfull) nv = *(gu32x4_a1 *)(p + 16u * (c + kT));
             if (c < cfull)
                 st16u((gwu32x4_a1 *)(q + 16u * c), v);
             else if (c == cfull)
@@ -2182,16 +2192,25 @@ __global__ void __launch_bounds__(kBlock) sum_copy_wg_kernel(Src src, size_t n, 
             acc += v.x + v.y + v.z + v.w;
             v = nv;
         }
-        if ((len & 15u) && t == (nfull & 255u)) {  // the fragment's last 1-15 bytes
+        if ((len & 15u) && t == nfull % kT) {  // the fragment's last 1-15 bytes
             const u32x4 w = load_tail16(p + 16u * nfull, len & 15u);
             acc += w.x + w.y + w.z + w.w;
             if (cfull == nfull) vc = w;
         }
-        if ((clen & 15u) && t == (cfull & 255u)) store_head16(q + 16u * cfull, vc, clen & 15u);
+        if ((clen & 15u) && t == cfull % kT) store_head16(q + 16u * cfull, vc, clen & 15u);
         acc = wave_add(acc);
-        if ((t & 63) == 0) part[it][t >> 6] = acc;
-        __syncthreads();
-        if (t == 0) emit(src, out, f, part[it][0] + part[it][1] + part[it][2] + part[it][3], fi);
+        if constexpr (kW == 1) {
+            if (t == 0) emit(src, out, f, acc, fi);
+        } else {
+            if ((t & 63) == 0) part[it][t >> 6] = acc;
+            __syncthreads();
+            if (t == 0) {
+                uint32_t sm = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < kW; ++w) sm += part[it][w];
+                emit(src, out, f, sm, fi);
+            }
+        }
     }
 }
 
@@ -2364,26 +2383,45 @@ __global__ void __launch_bounds__(64 * kWv) sum_rows_kernel(Src src, size_t n, u
 // added atomically into out[f], zeroed beforehand (the sum is order-free and a row starts on the
 // fragment's word grid).  Fragment f spans [f*frag_len, min(.., msg_len)); a workgroup takes rows
 // blockIdx.x + k*gridDim.x (one, unless there are more than kMaxWgGrid).
-__global__ void __launch_bounds__(kBlock) sum_copy_row_kernel(const uint8_t *__restrict__ base, size_t msg_len,
-                                                              size_t frag_len, uint32_t rpf, uint32_t nrows,
-                                                              uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
-                                                              size_t dst_stride) {
-    __shared__ uint32_t part[2][kWaves];  // by iteration parity: one barrier per row
+#ifndef LAMPI_SUMROW_T
+#define LAMPI_SUMROW_T 256
+#endif
+template <int kT = LAMPI_SUMROW_T>
+__global__ void __launch_bounds__(kT) sum_copy_row_kernel(const uint8_t *__restrict__ base, size_t msg_len,
+                                                          size_t frag_len, uint32_t rpf, uint32_t nrows,
+                                                          uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
+                                                          size_t dst_stride) {
+    constexpr int kS = kRowBytes / 16 / kT;  // chunks per thread per row
+    constexpr uint32_t kW = kT / 64;
+    __shared__ uint32_t part[2][kW];  // by iteration parity: one barrier per row
     uint32_t it = 0;
     for (uint32_t i = blockIdx.x; i < nrows; i += gridDim.x, it ^= 1u) {
         const uint32_t f = uniform(i / rpf), r = uniform(i - f * rpf);
-        const uint64_t fo = (uint64_t)f * frag_len, o = (uint64_t)r * kRowBytes + 16u * threadIdx.x;
+        const uint64_t fo = (uint64_t)f * frag_len;
         const uint64_t flen = msg_len - fo < frag_len ? msg_len - fo : frag_len;
-        u32x4 v = {0u, 0u, 0u, 0u};
-        if (o < flen) {  // flen % 16 == 0: a chunk is wholly inside or wholly outside
-            v = *(gu32x4 *)(base + fo + o);
-            st16((gwu32x4_a4 *)(dst + (uint64_t)f * dst_stride + o), v);
+        u32x4 v[kS];
+#pragma unroll
+        for (int k = 0; k < kS; ++k) {  // flen % 16 == 0: a chunk is wholly inside or wholly outside
+            const uint64_t o = (uint64_t)r * kRowBytes + 16u * (threadIdx.x + k * kT);
+            v[k] = o < flen ? *(gu32x4 *)(base + fo + o) : u32x4{0u, 0u, 0u, 0u};
         }
-        const uint32_t a = wave_add(v.x + v.y + v.z + v.w);
-        if ((threadIdx.x & 63) == 0) part[it][threadIdx.x >> 6] = a;
-        __syncthreads();
+        uint32_t a = 0;
+#pragma unroll
+        for (int k = 0; k < kS; ++k) {
+            const uint64_t o = (uint64_t)r * kRowBytes + 16u * (threadIdx.x + k * kT);
+            if (o < flen) st16((gwu32x4_a4 *)(dst + (uint64_t)f * dst_stride + o), v[k]);
+            a += v[k].x + v[k].y + v[k].z + v[k].w;
+        }
+        a = wave_add(a);
+        uint32_t sm = a;
+        if constexpr (kW > 1) {
+            if ((threadIdx.x & 63) == 0) part[it][threadIdx.x >> 6] = a;
+            __syncthreads();
+            sm = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kW; ++w) sm += part[it][w];
+        }
         if (threadIdx.x == 0) {
-            const uint32_t sm = part[it][0] + part[it][1] + part[it][2] + part[it][3];
             if (rpf == 1)
                 out[f] = sm;
             else
@@ -2996,20 +3034,9 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 
 // Fused-copy SUM (bcopy_uicsum, LA-MPI's default mode): sum_copy_wg_kernel, one short-lived
 // workgroup per fragment (the textbook copy shape).
-// Message fragments known to be shorter than kSumCopySmall take sum_rows_kernel instead (8-wave
-// workgroups, one fragment per wave, the next prefetched): a workgroup per fragment is latency-bound
-// there (1 GiB of 1,976-byte fragments 0.6 -> 0.9 ms, tools/microbench/sum_copy_sizes.py).
-constexpr size_t kSumCopySmall = 2048;
 template <class Src>
-static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t s, size_t frag_len = 0) {
-    if (frag_len != 0 && frag_len < kSumCopySmall) {
-        constexpr int kWv = 8;
-        const uint32_t fpw = spread_fpw(std::max(1u, pick_fpw(n, 1) / 2), n, kWv, frag_len);
-        hipLaunchKernelGGL((sum_rows_kernel<Src, uint32_t, kWv>), dim3((unsigned)((n + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw))),
-                           dim3(64 * kWv), 0, s, src, n, fpw, out);
-        return;
-    }
-    hipLaunchKernelGGL(sum_copy_wg_kernel<Src>, dim3((unsigned)std::min<size_t>(n, kMaxWgGrid)), dim3(kBlock), 0, s, src,
+static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(sum_copy_wg_kernel<Src>, dim3((unsigned)std::min<size_t>(n, kMaxWgGrid)), dim3(LAMPI_SUMWG_T), 0, s, src,
                        n, out);
 }
 
@@ -3113,7 +3140,7 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
             const hipError_t e = hipMemsetAsync(out, 0, n * sizeof(uint32_t), s);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(sum_copy_row_kernel, dim3((unsigned)std::min<size_t>(n * rpf, kMaxWgGrid)), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL(sum_copy_row_kernel<>, dim3((unsigned)std::min<size_t>(n * rpf, kMaxWgGrid)), dim3(LAMPI_SUMROW_T), 0, s,
                            base, msg_len, frag_len, (uint32_t)rpf, (uint32_t)(n * rpf), out, dst, dst_stride);
         return hipGetLastError();
     }
@@ -3123,12 +3150,11 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
     if (frag_len > kRowBytes && msg_len != 0) {  // fragments of several rows: row items (MsgRowCopySource)
         const hipError_t e = hipMemsetAsync(out, 0, n * sizeof(uint32_t), s);
         if (e != hipSuccess) return e;
-        launch_sum_copy(MsgRowCopySource{base, msg_len, frag_len, dst, dst_stride, (uint32_t)rpf}, n * rpf, out, s,
-                        kRowBytes);
+        launch_sum_copy(MsgRowCopySource{base, msg_len, frag_len, dst, dst_stride, (uint32_t)rpf}, n * rpf, out, s);
         return hipGetLastError();
     }
     // fragments of at most one row: one workgroup each
-    launch_sum_copy(MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, out, s, frag_len);
+    launch_sum_copy(MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, out, s);
     return hipGetLastError();
 }
 

@@ -213,7 +213,7 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     (65456 * 200 + 4000, 65456, 65536 + 4, 4),  # a last fragment of 4,000 bytes (one partial row)
     (4112 * 3000, 4112, 4112 + 12, 12),       # a second row of 16 bytes per fragment
     (49152 * 100 + 4096 * 5, 49152, 49152, 0),  # a last fragment of 5 of its 12 rows
-    # fragments under 2 KiB: one fragment per wave (sum_rows_kernel) for SUM
+    # fragments under 2 KiB (SUM: one 128-thread workgroup each, ragged tails)
     (1976 * 5000 + 3, 1976, 2048 + 4, 4),     # shared-memory-sized fragments, ragged tail
     (100 * 3000, 100, 128, 1),                # tiny fragments, byte-misaligned destinations
 ])
