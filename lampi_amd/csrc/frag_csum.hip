@@ -84,6 +84,8 @@ typedef __attribute__((address_space(1))) u32x4_a4 gwu32x4_a4;
 #ifndef LAMPI_NT_STORES
 #define LAMPI_NT_STORES 1
 #endif
+// (The asm-issued row loads stay cached: with the nt bit, read-only CRC fell from 80.6% to 42.3%
+// and config C from 73.6% to 44.1%; profiles/r02_sumcopy/ab_ntal/.)
 #if LAMPI_NT_STORES
 #define LAMPI_ST_NT " nt"
 #else
@@ -347,7 +349,7 @@ __device__ __forceinline__ void wait_row(Row &r) {
 
 __device__ __forceinline__ u32x4 issue_b128(gbyte *p) {
     u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(v) : "v"(p) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(v) : "v"(p) : "memory");  // the L2-resident basis
     return v;
 }
 
@@ -2118,6 +2120,18 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 // ways), non-temporal stores, the next row loaded before this one is stored.  The sum is
 // order-free and every chunk starts on the fragment's word grid.  Copy shape: 4 KiB rows 78-81% of
 // read + write against 72-74% for one fragment per wave (tools/microbench/copy5.hip).
+// source loads of the SUM copy kernels: non-temporal (read once; same-box A/B, profiles/r02_sumcopy/
+// ab_ntl/: descriptors +1 to +2.5 points, messages, slots and +1 destinations +0.5 to +1.4)
+#ifndef LAMPI_NT_LOADS
+#define LAMPI_NT_LOADS 1
+#endif
+__device__ __forceinline__ u32x4 ld16u(gu32x4_a1 *p) {
+#if LAMPI_NT_LOADS
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
 typedef __attribute__((address_space(1))) const uint32_t __attribute__((aligned(1))) gu32_a1;
 typedef __attribute__((address_space(1))) uint32_t __attribute__((aligned(1))) gwu32_a1;
 
@@ -2180,11 +2194,11 @@ __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint
         // is kept (vc) and the fragment's partial last chunk is read after the loop
         uint32_t acc = 0;
         u32x4 v = {0u, 0u, 0u, 0u}, vc = {0u, 0u, 0u, 0u};
-        if (t < nfull) v = *(gu32x4_a1 *)(p + 16u * t);
+        if (t < nfull) v = ld16u((gu32x4_a1 *)(p + 16u * t));
         for (uint32_t r = 0; r < R; ++r) {
             const uint32_t c = kT * r + t;
             u32x4 nv = {0u, 0u, 0u, 0u};
-            if (c + kT < nfull) nv = *(gu32x4_a1 *)(p + 16u * (c + kT));
+            if (c + kT < nfull) nv = ld16u((gu32x4_a1 *)(p + 16u * (c + kT)));
             if (c < cfull)
                 st16u((gwu32x4_a1 *)(q + 16u * c), v);
             else if (c == cfull)
@@ -2403,7 +2417,7 @@ __global__ void __launch_bounds__(kT) sum_copy_row_kernel(const uint8_t *__restr
 #pragma unroll
         for (int k = 0; k < kS; ++k) {  // flen % 16 == 0: a chunk is wholly inside or wholly outside
             const uint64_t o = (uint64_t)r * kRowBytes + 16u * (threadIdx.x + k * kT);
-            v[k] = o < flen ? *(gu32x4 *)(base + fo + o) : u32x4{0u, 0u, 0u, 0u};
+            v[k] = o < flen ? ld16u((gu32x4_a1 *)(base + fo + o)) : u32x4{0u, 0u, 0u, 0u};
         }
         uint32_t a = 0;
 #pragma unroll
