@@ -98,6 +98,23 @@ __device__ __forceinline__ void st16(gwu32x4_a4 *p, const u32x4 &v) {
     *p = v;
 #endif
 }
+// source loads of the SUM copy kernels: non-temporal (read once; same-box A/B, profiles/r02_sumcopy/
+// ab_ntl/: descriptors +1 to +2.5 points, messages, slots and +1 destinations +0.5 to +1.4)
+#ifndef LAMPI_NT_LOADS
+#define LAMPI_NT_LOADS 1
+#endif
+__device__ __forceinline__ u32x4 ld16u(gu32x4_a1 *p) {
+#if LAMPI_NT_LOADS
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+// coalesced row loads of crc_rows_kernel (fused CRC copies of descriptors, the receive step,
+// ragged messages): non-temporal, same-box A/B (profiles/r02_sumcopy/ab_cntl/) descriptors, +1
+// destinations, the receive step and GM 65,456-byte slots +0.5 to +1 point.  The same bit on
+// crc_regular_kernel<copy>'s asm loads cost 1.6-2.2 points there (not used).
+__device__ __forceinline__ u32x4 ld16c(gu32x4_a1 *p) { return __builtin_nontemporal_load(p); }
 typedef __attribute__((address_space(1))) u32x4_a1 gwu32x4_a1;  // unaligned 16-byte stores
 __device__ __forceinline__ void st16u(gwu32x4_a1 *p, const u32x4 &v) {
 #if LAMPI_NT_STORES
@@ -919,7 +936,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_rows_kernel(Src src, size_t n, u
             gbyte *p = fi.addr + ((long long)rr * kRowBytes - (long long)gg.P) + 16 * lane;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const u32x4 v = *(gu32x4_a1 *)(p + 1024 * q);
+                const u32x4 v = ld16c((gu32x4_a1 *)(p + 1024 * q));
                 dd[4 * q + 0] = v.x;
                 dd[4 * q + 1] = v.y;
                 dd[4 * q + 2] = v.z;
@@ -2120,18 +2137,6 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 // ways), non-temporal stores, the next row loaded before this one is stored.  The sum is
 // order-free and every chunk starts on the fragment's word grid.  Copy shape: 4 KiB rows 78-81% of
 // read + write against 72-74% for one fragment per wave (tools/microbench/copy5.hip).
-// source loads of the SUM copy kernels: non-temporal (read once; same-box A/B, profiles/r02_sumcopy/
-// ab_ntl/: descriptors +1 to +2.5 points, messages, slots and +1 destinations +0.5 to +1.4)
-#ifndef LAMPI_NT_LOADS
-#define LAMPI_NT_LOADS 1
-#endif
-__device__ __forceinline__ u32x4 ld16u(gu32x4_a1 *p) {
-#if LAMPI_NT_LOADS
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
 typedef __attribute__((address_space(1))) const uint32_t __attribute__((aligned(1))) gu32_a1;
 typedef __attribute__((address_space(1))) uint32_t __attribute__((aligned(1))) gwu32_a1;
 
