@@ -2909,7 +2909,10 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
                                  hipStream_t s, size_t frag_len = 0) {
     static_assert(Src::kCopy, "the staging area is for the fused copy");
     constexpr int kWv = 2 * kWaves;  // 10-wave workgroups (20 waves/CU): 61% against 69% (4M x 4 KiB)
-    const uint32_t fpw = spread_fpw(std::max(1u, pick_fpw(n, R) / 2), n, kWv, frag_len);
+#ifndef LAMPI_RCOPY_FPW_MUL
+#define LAMPI_RCOPY_FPW_MUL 2  // in quarters (see LAMPI_CCOPY_FPW_MUL)
+#endif
+    const uint32_t fpw = spread_fpw(std::max(1u, pick_fpw(n, R) / 2 * LAMPI_RCOPY_FPW_MUL / 4), n, kWv, frag_len);
     const dim3 grid((unsigned)((n + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw)));
     hipLaunchKernelGGL((crc_rows_kernel<Src, kWv>), grid, dim3(64 * kWv), 0, s, src, n, fpw, img, out);
 }
@@ -3045,7 +3048,14 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
                                    size_t dst_stride, uint32_t *out, const uint32_t *img, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t fpw = pick_fpw(n, (uint32_t)(frag_len / kRowBytes));
+// fused CRC copies: half the read-only kernels' fragments per wave (same-box A/B,
+// profiles/r02_crc_copy_fpw/: message 69.8 -> 72.2%, descriptors 72.1 -> 74.4%, +8 sources
+// 71.8 -> 74.2%, +8 destinations 67.4 -> 69.5-70.4%, the receive step 71.2 -> 72%; a quarter:
+// about the same, +1 destinations 2 points lower; twice: no change; 3/4: 2 points lower)
+#ifndef LAMPI_CCOPY_FPW_MUL
+#define LAMPI_CCOPY_FPW_MUL 2  // in quarters of pick_fpw
+#endif
+    const uint32_t fpw = std::max(1u, pick_fpw(n, (uint32_t)(frag_len / kRowBytes)) * LAMPI_CCOPY_FPW_MUL / 4);
     hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, true>), grid_for(n, fpw), dim3(kBlock), 0, s, base,
                        (uint32_t)n, fpw, frag_len, partial, img, out, dst, dst_stride);
     return hipGetLastError();
