@@ -2908,7 +2908,9 @@ template <class Src>
 static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uint32_t *img, uint32_t *out,
                                  hipStream_t s, size_t frag_len = 0) {
     static_assert(Src::kCopy, "the staging area is for the fused copy");
-    constexpr int kWv = 2 * kWaves;  // 10-wave workgroups (20 waves/CU): 61% against 69% (4M x 4 KiB)
+    // 10-wave workgroups (20 waves/CU): 61% against 69% (4M x 4 KiB); with half the fragments per
+    // wave, 4 / 6 waves: descriptors 62-64 / 52% against 74-75% (profiles/r02_crc_copy_fpw/waves/)
+    constexpr int kWv = 2 * kWaves;
 #ifndef LAMPI_RCOPY_FPW_MUL
 #define LAMPI_RCOPY_FPW_MUL 2  // in quarters (see LAMPI_CCOPY_FPW_MUL)
 #endif
