@@ -3058,6 +3058,7 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 #define LAMPI_CCOPY_FPW_MUL 2  // in quarters of pick_fpw
 #endif
     const uint32_t fpw = std::max(1u, pick_fpw(n, (uint32_t)(frag_len / kRowBytes)) * LAMPI_CCOPY_FPW_MUL / 4);
+    // (one chain per wave and / or a two-deep ring: within a point of this, profiles/r02_crc_copy_fpw/chains/)
     hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, true>), grid_for(n, fpw), dim3(kBlock), 0, s, base,
                        (uint32_t)n, fpw, frag_len, partial, img, out, dst, dst_stride);
     return hipGetLastError();
