@@ -646,78 +646,91 @@ def run_mixed(args):
 
 
 def run_e2e(args):
-    """Config E: 256 MiB message in pinned host memory -> H2D (copy stream) -> CRC per
-    fragment (compute stream) -> D2H of the u32 array, chunked and overlapped."""
+    """Config E: a 256 MiB message in host memory through the library's host-message path
+    (lampi_host_msg_csum / lampi_host_msg_bcopy, one C-ABI call per message: chunked H2D ||
+    checksum kernels || D2H inside the library).  Reported beside the raw pinned H2D / D2H rates of
+    the same box; every result is checked against the committed config E digests (and the copies
+    against the message)."""
     import numpy as np
     import torch
 
-    from lampi_amd import device as dv
     from lampi_amd import shard
+    from lampi_amd._lib import check, lib as _clib
 
     torch.cuda.set_device(0)
+    c = _clib()
     msg_bytes = 256 << 20
-    chunk = 16 << 20
     with open(os.path.join(ROOT, "tests", "golden", "fixtures.json")) as f:
         gold = json.load(f)["digests"]["E"]
-    host = torch.empty(msg_bytes, dtype=torch.uint8).pin_memory()
+    from lampi_amd import device as dv
+
+    pinned = torch.empty(msg_bytes, dtype=torch.uint8).pin_memory()
     staged = torch.empty(msg_bytes, dtype=torch.uint8, device="cuda")
     dv.fill_stream(staged, seed=gold["seed"])  # the message, generated on the device, then parked in host memory
-    host.copy_(staged)
-    del staged
-    res = {}
-    for L in (4096, 16384, 65456):
-        per_chunk = (chunk // L) * L  # whole fragments per chunk (last fragment of the message may be short)
-        nfr = (msg_bytes + L - 1) // L
-        out_host = torch.empty(nfr, dtype=torch.int32).pin_memory()
-        nbuf = 3
-        dbufs = [torch.empty(per_chunk, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
-        douts = [torch.empty(per_chunk // L + 1, dtype=torch.int32, device="cuda") for _ in range(nbuf)]
-        cp, cs = torch.cuda.Stream(), torch.cuda.Stream()
-        h2d_done = [torch.cuda.Event() for _ in range(nbuf)]
-        crc_done = [torch.cuda.Event() for _ in range(nbuf)]
+    pinned.copy_(staged)
+    torch.cuda.synchronize()
+    pageable = pinned.numpy().copy()
+    reps = max(3, min(args.steps, 10))
 
-        def one_pass():
-            off, fi, i = 0, 0, 0
-            while off < msg_bytes:
-                b = i % nbuf
-                nb = min(per_chunk, msg_bytes - off)
-                nf = (nb + L - 1) // L
-                with torch.cuda.stream(cp):
-                    cp.wait_event(crc_done[b])  # buffer b free again
-                    dbufs[b][:nb].copy_(host[off:off + nb], non_blocking=True)
-                    h2d_done[b].record(cp)
-                with torch.cuda.stream(cs):
-                    cs.wait_event(h2d_done[b])
-                    dv.msg_csum(dbufs[b], L, msg_len=nb, out=douts[b], stream=cs)
-                    out_host[fi:fi + nf].copy_(douts[b][:nf], non_blocking=True)
-                    crc_done[b].record(cs)
-                off += nb
-                fi += nf
-                i += 1
-            torch.cuda.synchronize()
-
-        one_pass()
-        reps = 5
+    def timed(fn):
+        fn()
         t0 = time.perf_counter()
         for _ in range(reps):
-            one_pass()
-        dt = (time.perf_counter() - t0) / reps
-        got = shard.digest(out_host.numpy().view(np.uint32), np.arange(nfr, dtype=np.uint64))
+            fn()
+        return (time.perf_counter() - t0) / reps
+
+    # raw PCIe rates of this box: pinned H2D and D2H of the whole message (torch copies)
+    t_h2d = timed(lambda: (staged.copy_(pinned, non_blocking=True), torch.cuda.synchronize()))
+    t_d2h = timed(lambda: (pinned.copy_(staged, non_blocking=True), torch.cuda.synchronize()))
+    del staged
+    h2d, d2h = msg_bytes / GIB / t_h2d, msg_bytes / GIB / t_d2h
+    res = {}
+    ok_all = True
+    for L in (4096, 16384, 65456):
+        nfr = (msg_bytes + L - 1) // L
         g = gold[str(L)]
-        res[str(L)] = {"GiB_per_s_incl_h2d_d2h": round(msg_bytes / GIB / dt, 2), "ms_per_256MiB": round(dt * 1e3, 3),
-                       "fragments": int(nfr),
-                       "bit_exact": bool(nfr == g["n"] and got == (g["crc_xor"], g["crc_wsum"]))}
-    # raw pinned H2D bandwidth for reference
-    d = torch.empty(msg_bytes, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(5):
-        d.copy_(host, non_blocking=True)
-    torch.cuda.synchronize()
-    h2d = msg_bytes * 5 / GIB / (time.perf_counter() - t0)
-    print(json.dumps({"metric": "end-to-end host-memory fragment-CRC (config E, 256 MiB pinned, chunked "
-                                "H2D + CRC + D2H overlapped)", "unit": "GiB/s", "results": res,
-                      "pinned_h2d_GiB_per_s": round(h2d, 2), "chunk_bytes": chunk}))
+        out = np.empty(nfr, dtype=np.uint32)
+        ks = np.arange(nfr, dtype=np.uint64)
+        row = {"fragments": int(nfr)}
+        for src_kind, src_ptr in (("pinned", pinned.data_ptr()), ("pageable", pageable.ctypes.data)):
+            out.fill(0)
+            t = timed(lambda: check(c.lampi_host_msg_csum(src_ptr, msg_bytes, L, 0, nfr, 0xFFFFFFFF,
+                                                          out.ctypes.data, 0), "lampi_host_msg_csum"))
+            ok = nfr == g["n"] and shard.digest(out, ks) == (g["crc_xor"], g["crc_wsum"])
+            ok_all &= ok
+            row[f"csum_{src_kind}_src"] = {"GiB_per_s": round(msg_bytes / GIB / t, 2), "ms": round(t * 1e3, 3),
+                                           "frac_of_pinned_h2d": round(msg_bytes / GIB / t / h2d, 4),
+                                           "bit_exact": bool(ok)}
+        # fused copy into NIC buffers: each payload behind a 72-byte header, buffers of L + 80 bytes
+        # (65,456-byte payloads: GM's 64 KiB buffers, src/path/gm/state.h:48-57)
+        stride = L + 80
+        ring = torch.empty(nfr * stride, dtype=torch.uint8).pin_memory()
+        ring_pg = np.empty(nfr * stride, dtype=np.uint8)
+        for ring_kind, ring_arr, ring_ptr in (("pinned", ring.numpy(), ring.data_ptr() + 72),
+                                              ("pageable", ring_pg, ring_pg.ctypes.data + 72)):
+            out.fill(0)
+            t = timed(lambda: check(c.lampi_host_msg_bcopy(pinned.data_ptr(), msg_bytes, L, 0, nfr, ring_ptr, stride,
+                                                           0xFFFFFFFF, out.ctypes.data, 0), "lampi_host_msg_bcopy"))
+            full = msg_bytes // L
+            msg = pageable
+            copy_ok = bool(np.array_equal(np.lib.stride_tricks.as_strided(ring_arr[72:], (full, L), (stride, 1)),
+                                          msg[:full * L].reshape(full, L)))
+            tail = msg_bytes - full * L
+            if tail:
+                copy_ok &= bool(np.array_equal(ring_arr[72 + full * stride:72 + full * stride + tail], msg[full * L:]))
+            ok = nfr == g["n"] and shard.digest(out, ks) == (g["crc_xor"], g["crc_wsum"]) and copy_ok
+            ok_all &= ok
+            row[f"bcopy_pinned_src_{ring_kind}_ring"] = {
+                "GiB_per_s": round(msg_bytes / GIB / t, 2), "ms": round(t * 1e3, 3),
+                "frac_of_min_h2d_d2h": round(msg_bytes / GIB / t / min(h2d, d2h), 4),
+                "slot_stride": stride, "bit_exact_and_copied": bool(ok)}
+        del ring
+        res[str(L)] = row
+    print(json.dumps({"metric": "end-to-end host-memory fragment-CRC (config E: 256 MiB message in host memory, "
+                                "one lampi_host_msg_csum / lampi_host_msg_bcopy call per message)",
+                      "unit": "GiB/s", "results": res, "pinned_h2d_GiB_per_s": round(h2d, 2),
+                      "pinned_d2h_GiB_per_s": round(d2h, 2), "reps": reps,
+                      "parity_ok": bool(ok_all)}), flush=True)
 
 
 def run_bcopy(args):

@@ -1,14 +1,18 @@
 /*
  * lampi/MemFunctions.h -- drop-in replacement for LA-MPI's src/util/MemFunctions.h
- * (ref src/util/MemFunctions.h:31-65).  Restores the reference's C++ overload names and
- * signatures on top of the C ABI of liblampi_csum.so, so src/path compiles unchanged:
+ * (ref src/util/MemFunctions.h:31-65).  Declares the reference's twelve C++ overloads with its
+ * own prototypes; liblampi_csum.so defines them (lampi_amd/csrc/memfunctions_abi.cc) and
+ * exports their mangled names, so either
  *
- *     #include "util/MemFunctions.h"   ->   #include "lampi/MemFunctions.h"
+ *     #include "util/MemFunctions.h"   ->   #include "lampi/MemFunctions.h"     (recompile), or
+ *     keep the reference header and replace MemFunctions.o with -llampi_csum    (relink only)
+ *
  *     link:  -L<repo>/lampi_amd -llampi_csum
  *
  * All twelve overloads are provided: the 32-bit uicrc/bcopy_uicrc/uicsum/bcopy_uicsum (the
  * only ones with callers in src/) and the 64-bit csum/bcopy_csum
- * (MemFunctions.h:43-50, no path caller).
+ * (MemFunctions.h:43-50, no path caller).  C callers use the
+ * lampi_* entry points of lampi_csum.h directly.
  */
 #ifndef LAMPI_DROPIN_MEMFUNCTIONS_H
 #define LAMPI_DROPIN_MEMFUNCTIONS_H
@@ -24,56 +28,34 @@
 
 #ifdef __cplusplus
 
-inline unsigned int uicrc(const void *source, unsigned long crclen, unsigned int partial_crc) {
-    return lampi_uicrc(source, crclen, partial_crc);
-}
-inline unsigned int uicrc(const void *source, unsigned long crclen) {
-    return lampi_uicrc(source, crclen, CRC_INITIAL_REGISTER);
-}
-inline unsigned int bcopy_uicrc(const void *source, void *destination, unsigned long copylen,
-                                unsigned long crclen, unsigned int partial_crc) {
-    return lampi_bcopy_uicrc(source, destination, copylen, crclen, partial_crc);
-}
-inline unsigned int bcopy_uicrc(const void *source, void *destination, unsigned long copylen,
-                                unsigned long crclen) {
-    return lampi_bcopy_uicrc(source, destination, copylen, crclen, CRC_INITIAL_REGISTER);
-}
-inline unsigned int uicsum(const void *source, unsigned long csumlen, unsigned int *lastPartialInt,
-                           unsigned int *lastPartialLength) {
-    return lampi_uicsum(source, csumlen, lastPartialInt, lastPartialLength);
-}
-inline unsigned int uicsum(const void *source, unsigned long csumlen) {
-    unsigned int pint = 0, plen = 0;
-    return lampi_uicsum(source, csumlen, &pint, &plen);
-}
-inline unsigned int bcopy_uicsum(const void *source, void *destination, unsigned long copylen,
-                                 unsigned long csumlen, unsigned int *lastPartialInt,
-                                 unsigned int *lastPartialLength) {
-    return lampi_bcopy_uicsum(source, destination, copylen, csumlen, lastPartialInt, lastPartialLength);
-}
-inline unsigned int bcopy_uicsum(const void *source, void *destination, unsigned long copylen,
-                                 unsigned long csumlen) {
-    unsigned int pint = 0, plen = 0;
-    return lampi_bcopy_uicsum(source, destination, copylen, csumlen, &pint, &plen);
-}
-// 64-bit additive checksums (MemFunctions.h:43-50; no path caller in the reference)
-inline unsigned long csum(const void *source, unsigned long csumlen, unsigned long *lastPartialLong,
-                          unsigned long *lastPartialLength) {
-    return lampi_csum(source, csumlen, lastPartialLong, lastPartialLength);
-}
-inline unsigned long csum(const void *source, unsigned long csumlen) {
-    unsigned long plong = 0, plen = 0;
-    return lampi_csum(source, csumlen, &plong, &plen);
-}
-inline unsigned long bcopy_csum(const void *source, void *destination, unsigned long copylen, unsigned long csumlen,
-                                unsigned long *lastPartialLong, unsigned long *lastPartialLength) {
-    return lampi_bcopy_csum(source, destination, copylen, csumlen, lastPartialLong, lastPartialLength);
-}
-inline unsigned long bcopy_csum(const void *source, void *destination, unsigned long copylen,
-                                unsigned long csumlen) {
-    unsigned long plong = 0, plen = 0;
-    return lampi_bcopy_csum(source, destination, copylen, csumlen, &plong, &plen);
-}
+/* 64-bit additive checksums (MemFunctions.h:43-50; no path caller in the reference) */
+unsigned long bcopy_csum(const void *source, void *destination, unsigned long copylen, unsigned long csumlen);
+unsigned long bcopy_csum(const void *source, void *destination, unsigned long copylen, unsigned long csumlen,
+                         unsigned long *lastPartialLong, unsigned long *lastPartialLength);
+unsigned long csum(const void *source, unsigned long csumlen);
+unsigned long csum(const void *source, unsigned long csumlen, unsigned long *lastPartialLong,
+                   unsigned long *lastPartialLength);
+
+/* 32-bit additive checksums (MemFunctions.h:52-59) */
+unsigned int bcopy_uicsum(const void *source, void *destination, unsigned long copylen, unsigned long csumlen);
+unsigned int bcopy_uicsum(const void *source, void *destination, unsigned long copylen, unsigned long csumlen,
+                          unsigned int *lastPartialInt, unsigned int *lastPartialLength);
+unsigned int uicsum(const void *source, unsigned long csumlen);
+unsigned int uicsum(const void *source, unsigned long csumlen, unsigned int *lastPartialInt,
+                    unsigned int *lastPartialLength);
+
+/* CRC-32 (MemFunctions.h:60-65) */
+unsigned int bcopy_uicrc(const void *source, void *destination, unsigned long copylen, unsigned long crclen);
+unsigned int bcopy_uicrc(const void *source, void *destination, unsigned long copylen, unsigned long crclen,
+                         unsigned int partial_crc);
+unsigned int uicrc(const void *source, unsigned long crclen, unsigned int partial_crc);
+unsigned int uicrc(const void *source, unsigned long crclen);
+
+/* The rest of the reference's MemFunctions.o, so the object can be replaced whole at link time:
+ * ulm_initialize_crc_table (MemFunctions.cc:1242-1261; here: build the current device's tables now)
+ * and poisonMemory (MemFunctions.cc:1380-1393, declared in src/util/Utility.h:45). */
+void ulm_initialize_crc_table();
+void poisonMemory(void *ptr, long lenInBytes, int pattern);
 
 #endif /* __cplusplus */
 #endif /* LAMPI_DROPIN_MEMFUNCTIONS_H */

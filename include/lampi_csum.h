@@ -88,6 +88,46 @@ unsigned long lampi_bcopy_csum(const void *src, void *dst, unsigned long copylen
                                unsigned long *plong, unsigned long *plen);
 
 /* ------------------------------------------------------------------------------------
+ * Host-memory message path: a range of a host message's fragments in one call.
+ * Fragment k of the message = bytes [k*frag_len, min((k+1)*frag_len, msg_len)) -- the path
+ * layer's split (src/path/gm/path.cc:98-121); a zero-length message is one empty fragment.
+ * The call covers fragments k_first .. k_first+k_count-1 (a sender gated by clear-to-send /
+ * maxOutstandingFrags, gm/path.cc:104-118, passes the fragments it may send now) and writes
+ * their checksums to h_out[0 .. k_count).  Every fragment starts from `partial` (CRC mode,
+ * CRC_INITIAL_REGISTER for the path's per-fragment value) or a fresh state (SUM mode).
+ *
+ * Inside, a chunked pipeline on the calling thread's own streams: H2D of chunk i+1 overlaps
+ * the checksum kernels of chunk i and the D2H of chunk i-1.  Buffers that are page-locked
+ * (hipHostMalloc'd, or registered with lampi_host_register) are DMA'd directly; pageable ones
+ * go through the thread's pinned bounce buffers (a CPU copy into them, overlapped with the
+ * DMA).  Synchronous: everything is written when the call returns.  Returns 0 or a hipError_t
+ * (invalid arguments: hipErrorInvalidValue; nothing is written then).
+ * ---------------------------------------------------------------------------------- */
+
+/* Checksum-only: what the sender stores in dataChecksum for each fragment of the range --
+ * the per-fragment uicrc / uicsum of gmSendFragDesc::init (src/path/gm/sendFrag.cc:147-155)
+ * without the copy, and the Quadrics checksum over the DMA source
+ * (src/path/quadrics/sendFrag.h:861-872). */
+int lampi_host_msg_csum(const void *h_msg, size_t msg_len, size_t frag_len, size_t k_first, size_t k_count,
+                        uint32_t partial, uint32_t *h_out, int mode);
+
+/* Fused copy + checksum into NIC buffers: fragment k_first+i is copied to
+ * h_ring + i*slot_stride (slot_stride >= frag_len; e.g. the payload area of a ring of
+ * header + payload buffers: h_ring = first buffer + 72, slot_stride = the buffer size) and
+ * h_out[i] = bcopy_uicrc / bcopy_uicsum of it (copylen = crclen = the fragment length), as the
+ * send loop of gmPath::send does per fragment (src/path/gm/path.cc:98-176, sendFrag.cc:147-155).
+ * The bytes written to the slots are exactly the bytes checksummed; no other byte of the ring
+ * is touched.  h_ring must not overlap h_msg. */
+int lampi_host_msg_bcopy(const void *h_msg, size_t msg_len, size_t frag_len, size_t k_first, size_t k_count,
+                         void *h_ring, size_t slot_stride, uint32_t partial, uint32_t *h_out, int mode);
+
+/* Page-lock [h_ptr, h_ptr+len) for direct DMA by the host paths (hipHostRegister) and undo it:
+ * the analogue of registering NIC buffers with the network (GM gm_register_memory).  Return 0
+ * or a hipError_t. */
+int lampi_host_register(void *h_ptr, size_t len);
+int lampi_host_unregister(void *h_ptr);
+
+/* ------------------------------------------------------------------------------------
  * Device-resident batched entry points.
  * ---------------------------------------------------------------------------------- */
 
@@ -257,6 +297,10 @@ int lampi_fill_stream_frags(void *d_dst, size_t n, size_t frag_len, uint64_t see
  * buffers, pinned bounce buffer).  They are also released automatically when the thread exits
  * or switches to another device; the next host call on the thread allocates them again. */
 void lampi_host_release(void);
+
+/* Bytes of page-locked host memory the library's host paths hold right now, over all threads
+ * (bounce buffers, result words, staging): a leak check for callers with short-lived threads. */
+int64_t lampi_host_pinned_bytes(void);
 
 /* Version string of the engine and the gfx target it was built for. */
 const char *lampi_csum_version(void);

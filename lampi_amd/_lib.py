@@ -89,6 +89,13 @@ PROTOTYPES = {
     "lampi_fill_stream_frags": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                                ctypes.c_uint64, c_void_p]),
     "lampi_host_release": (None, []),
+    "lampi_host_pinned_bytes": (ctypes.c_int64, []),
+    "lampi_host_msg_csum": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_size_t, c_size_t, ctypes.c_uint32,
+                                           c_void_p, ctypes.c_int]),
+    "lampi_host_msg_bcopy": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_size_t, c_size_t, c_void_p, c_size_t,
+                                            ctypes.c_uint32, c_void_p, ctypes.c_int]),
+    "lampi_host_register": (ctypes.c_int, [c_void_p, c_size_t]),
+    "lampi_host_unregister": (ctypes.c_int, [c_void_p]),
     "lampi_csum_version": (ctypes.c_char_p, []),
 }
 

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +20,7 @@
 #include "../../include/lampi_csum.h"
 #include "crc_tables.h"
 #include "frag_csum_kernels.h"
+#include "host_internal.h"
 
 namespace lampi {
 namespace {
@@ -32,18 +34,23 @@ struct DeviceTables {
 };
 DeviceTables g_tables[kMaxDevices];
 
-hipError_t current_device(int *dev) {
-    hipError_t e = hipGetDevice(dev);
-    if (e != hipSuccess) return e;
-    if (*dev < 0 || *dev >= kMaxDevices) return hipErrorInvalidDevice;
-    return hipSuccess;
-}
 
 // The table image is built on the host (GF(2) algebra, crc_tables.cc) once per process and
 // uploaded once per device; kernels stage it into LDS.
 const std::vector<uint32_t> &host_image() {
     static const std::vector<uint32_t> img = build_table_image();
     return img;
+}
+
+std::atomic<int64_t> g_pinned_bytes{0};
+
+}  // namespace
+
+hipError_t current_device(int *dev) {
+    hipError_t e = hipGetDevice(dev);
+    if (e != hipSuccess) return e;
+    if (*dev < 0 || *dev >= kMaxDevices) return hipErrorInvalidDevice;
+    return hipSuccess;
 }
 
 hipError_t device_tables(int dev, const uint32_t **out) {
@@ -59,14 +66,54 @@ hipError_t device_tables(int dev, const uint32_t **out) {
     return t.err;
 }
 
-int to_int(hipError_t e) { return (int)e; }
+hipError_t launch_msg_csum(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, uint32_t *out,
+                           int mode, int dev, const uint32_t *img, hipStream_t s) {
+    const size_t n = msg_len ? (msg_len + frag_len - 1) / frag_len : 1;
+    const int grid = crc_grid(dev);
+    if (mode == LAMPI_CSUM_SUM32) return launch_sum_msg(base, msg_len, frag_len, n, out, img, grid, s);
+    const bool regular = msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 &&
+                         regular_msg_frag(frag_len, false) && ((uintptr_t)base & 15u) == 0;
+    if (regular) return launch_crc_regular(base, n, frag_len, partial, out, img, grid, s);
+    return launch_crc_msg(base, msg_len, frag_len, partial, n, out, img, grid, s);
+}
 
-// ------------------------------------------------------------------ host-path context
+hipError_t pinned_alloc(void **p, size_t bytes, unsigned flags) {
+    const hipError_t e = hipHostMalloc(p, bytes, flags);
+    if (e == hipSuccess) g_pinned_bytes.fetch_add((int64_t)bytes, std::memory_order_relaxed);
+    return e;
+}
+
+void pinned_free(void *p, size_t bytes) {
+    if (!p) return;
+    (void)hipHostFree(p);
+    g_pinned_bytes.fetch_sub((int64_t)bytes, std::memory_order_relaxed);
+}
+
+bool host_range_pinned(const void *p, size_t len) {
+    if (!p || !len) return false;
+    const uint8_t *ends[2] = {(const uint8_t *)p, (const uint8_t *)p + len - 1};
+    for (const uint8_t *q : ends) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();  // pageable memory: not an error of the call
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
+
 [[noreturn]] void die(const char *what, hipError_t e) {
     std::fprintf(stderr, "liblampi_csum: %s failed: %s (%d); no CPU fallback exists\n", what,
                  hipGetErrorString(e), (int)e);
     std::abort();
 }
+
+namespace {
+
+int to_int(hipError_t e) { return (int)e; }
+
+// ------------------------------------------------------------------ host-path context
 
 #define LAMPI_CHECK(call)                      \
     do {                                       \
@@ -86,12 +133,15 @@ constexpr size_t kBounceHalf = 4u << 20;  // pinned bounce buffer: two halves (p
 constexpr size_t kZeroCopy = 256u << 10;
 constexpr uint64_t kPieceMin = 64 * 1024;  // host path: bytes per fragment piece
 constexpr uint32_t kMaxPieces = 16384;     // combine kernel capacity (LDS ping-pong)
+constexpr size_t kResBytes = 8 * sizeof(uint64_t);
+constexpr size_t kDescBytes = kMaxPieces * sizeof(lampi_frag_desc);
+constexpr size_t kZpinBytes = kZeroCopy + 64;  // + slack: aligned word reads past a body (uicsum)
 
 struct HostCtx {
     int dev = -1;
     hipStream_t stream = nullptr;
     hipEvent_t half_free[2] = {nullptr, nullptr};  // the last transfer through each bounce half
-    uint8_t *pin = nullptr;                       // 2 x kBounceHalf pinned bytes
+    uint8_t *pin = nullptr;                       // 2 x kBounceHalf pinned bytes (first call > kZeroCopy)
     uint64_t *pres = nullptr;                     // pinned, host-coherent result words (4 x u64) + signal word
     uint64_t seq = 0;                             // the last signal value asked for (wait_done)
     uint8_t *zpin = nullptr;                      // pinned, host-coherent staging of small calls
@@ -127,10 +177,10 @@ struct HostCtx {
         if (ddesc) (void)hipFree(ddesc);
         if (dvals64) (void)hipFree(dvals64);
         for (auto &kv : combine_tabs) (void)hipFree(kv.second);
-        if (pin) (void)hipHostFree(pin);
-        if (pres) (void)hipHostFree(pres);
-        if (hdesc) (void)hipHostFree(hdesc);
-        if (zpin) (void)hipHostFree(zpin);
+        pinned_free(pin, 2 * kBounceHalf);
+        pinned_free(pres, kResBytes);
+        pinned_free(hdesc, kDescBytes);
+        pinned_free(zpin, kZpinBytes);
         for (hipEvent_t &e : half_free)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
@@ -167,12 +217,13 @@ HostCtx &host_ctx() {
         ctx.dev = dev;
         LAMPI_CHECK(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
         for (hipEvent_t &e : ctx.half_free) LAMPI_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        LAMPI_CHECK(hipHostMalloc((void **)&ctx.pin, 2 * kBounceHalf, hipHostMallocDefault));
+        // the 8 MiB bounce buffer waits for the first call above kZeroCopy (bounce()): threads
+        // that only make small calls stay cheap to create and tear down
         constexpr unsigned kCoherent = hipHostMallocMapped | hipHostMallocCoherent;
-        LAMPI_CHECK(hipHostMalloc((void **)&ctx.pres, 8 * sizeof(uint64_t), kCoherent));
+        LAMPI_CHECK(pinned_alloc((void **)&ctx.pres, kResBytes, kCoherent));
         ctx.pres[kSignalWord] = ctx.seq = 0;
-        LAMPI_CHECK(hipHostMalloc((void **)&ctx.hdesc, kMaxPieces * sizeof(lampi_frag_desc), kCoherent));
-        LAMPI_CHECK(hipHostMalloc((void **)&ctx.zpin, kZeroCopy + 64, kCoherent));  // + slack: aligned word reads past a body (uicsum)
+        LAMPI_CHECK(pinned_alloc((void **)&ctx.hdesc, kDescBytes, kCoherent));
+        LAMPI_CHECK(pinned_alloc((void **)&ctx.zpin, kZpinBytes, kCoherent));
         LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.zpin_d, ctx.zpin, 0));
         LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.pres_d, ctx.pres, 0));
         LAMPI_CHECK(hipHostGetDevicePointer((void **)&ctx.hdesc_d, ctx.hdesc, 0));
@@ -363,6 +414,11 @@ unsigned long empty_sum64(unsigned long *plong, unsigned long *plen) {
     return 0;
 }
 
+// The pinned bounce buffer, allocated on the thread's first call above kZeroCopy.
+void bounce(HostCtx &c) {
+    if (!c.pin) LAMPI_CHECK(pinned_alloc((void **)&c.pin, 2 * kBounceHalf, hipHostMallocDefault));
+}
+
 // host -> c.dbuf through the pinned bounce buffer: pieces of kBounceHalf bytes alternate between
 // its two halves; a half is refilled once its previous DMA has completed (event), so the CPU
 // copy of one piece overlaps the DMA of the other.
@@ -372,6 +428,7 @@ Staged stage_in(HostCtx &c, const void *src, uint64_t len) {
         return {c.zpin_d, true};
     }
     ensure(c.dbuf, c.dcap, (size_t)len);
+    bounce(c);
     const uint8_t *s = (const uint8_t *)src;
     for (uint64_t off = 0, i = 0; off < len; off += kBounceHalf, ++i) {
         const size_t n = (size_t)std::min<uint64_t>(kBounceHalf, len - off);
@@ -393,6 +450,7 @@ void stage_out(HostCtx &c, const Staged &st, void *dst, uint64_t len) {
         std::memcpy(dst, c.zpin, (size_t)len);
         return;
     }
+    bounce(c);
     uint8_t *d = (uint8_t *)dst;
     const uint64_t np = (len + kBounceHalf - 1) / kBounceHalf;
     auto issue = [&](uint64_t i) {
@@ -572,21 +630,14 @@ int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t 
     if (frag_len == 0 || frag_len > 0xFFFFFFFFull || !d_out || (msg_len && !d_msg))
         return to_int(hipErrorInvalidValue);
     // a zero-length message is one empty fragment (the path layer still sends a header)
-    const size_t n = msg_len ? (msg_len + frag_len - 1) / frag_len : 1;
     int dev = 0;
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
-    hipStream_t s = (hipStream_t)stream;
-    const uint8_t *base = (const uint8_t *)d_msg;
-    const int grid = crc_grid(dev);
     const uint32_t *img = nullptr;
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
-    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_msg(base, msg_len, frag_len, n, d_out, img, grid, s));
-    const bool regular = msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 &&
-                         regular_msg_frag(frag_len, false) && ((uintptr_t)base & 15u) == 0;
-    if (regular) return to_int(launch_crc_regular(base, n, frag_len, partial, d_out, img, grid, s));
-    return to_int(launch_crc_msg(base, msg_len, frag_len, partial, n, d_out, img, grid, s));
+    return to_int(launch_msg_csum((const uint8_t *)d_msg, msg_len, frag_len, partial, d_out, mode, dev, img,
+                                  (hipStream_t)stream));
 }
 
 int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_dst, size_t dst_stride,
@@ -697,7 +748,22 @@ int lampi_fill_stream_frags(void *d_dst, size_t n, size_t frag_len, uint64_t see
                                     (hipStream_t)stream));
 }
 
-void lampi_host_release(void) { t_ctx.release(); }
+void lampi_host_release(void) {
+    t_ctx.release();
+    release_pipeline();
+}
+
+int64_t lampi_host_pinned_bytes(void) { return g_pinned_bytes.load(std::memory_order_relaxed); }
+
+int lampi_host_register(void *h_ptr, size_t len) {
+    if (!h_ptr || !len) return to_int(hipErrorInvalidValue);
+    return to_int(hipHostRegister(h_ptr, len, hipHostRegisterDefault));
+}
+
+int lampi_host_unregister(void *h_ptr) {
+    if (!h_ptr) return to_int(hipErrorInvalidValue);
+    return to_int(hipHostUnregister(h_ptr));
+}
 
 const char *lampi_csum_version(void) { return "lampi-frag-csum 0.1 (gfx950, CDNA4)"; }
 

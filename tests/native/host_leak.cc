@@ -1,7 +1,10 @@
 // host_leak.cc -- the host entry points' staging must not leak: 1,000 short-lived threads each
 // make host calls and exit (thread_local release), then 1,000 call + lampi_host_release()
 // rounds on one thread (the same release a device switch runs).  Prints device memory in use
-// before and after each phase (hipMemGetInfo) and the checksum XOR of all calls.
+// before and after each phase (hipMemGetInfo) and the page-locked host memory the library holds
+// (lampi_host_pinned_bytes: bounce buffers, result words, staging -- invisible to hipMemGetInfo).
+// The calls include the host-message pipeline (lampi_host_msg_csum / _bcopy) and calls above the
+// zero-copy limit, so every kind of staging is allocated and must be released.
 // Build: make -C tests/native
 #include <hip/hip_runtime.h>
 
@@ -23,24 +26,41 @@ int main(int argc, char **argv) {
     std::vector<unsigned char> buf(1 << 20);
     for (size_t i = 0; i < buf.size(); ++i) buf[i] = (unsigned char)(i * 131 + 7);
     std::vector<unsigned char> dst(buf.size());
+    std::vector<uint32_t> frag(buf.size() / 4096);
     unsigned x = lampi_uicrc(buf.data(), buf.size(), 0xFFFFFFFFu);  // warm: tables, first context
     const unsigned want = x;
+    if (lampi_host_msg_csum(buf.data(), buf.size(), 4096, 0, frag.size(), 0xFFFFFFFFu, frag.data(), 0) != 0) return 2;
+    const uint32_t want0 = frag[0];
     const size_t u0 = used();
+    const long long p0 = (long long)lampi_host_pinned_bytes();
     unsigned bad = 0;
     for (int r = 0; r < rounds; ++r) {
         std::thread t([&] {
             if (lampi_uicrc(buf.data(), buf.size(), 0xFFFFFFFFu) != want) ++bad;
             unsigned pi = 0, pl = 0;
             (void)lampi_bcopy_uicsum(buf.data(), dst.data(), 4096, 4099, &pi, &pl);
+            std::vector<uint32_t> f(frag.size());
+            if (r % 4 == 0) {  // the pipeline, pageable source and ring: every bounce buffer
+                if (lampi_host_msg_bcopy(buf.data(), buf.size(), 4096, 0, f.size(), dst.data(), 4096, 0xFFFFFFFFu,
+                                         f.data(), 0) != 0 || f[0] != want0)
+                    ++bad;
+            }
         });
         t.join();
     }
     const size_t u1 = used();
+    const long long p1 = (long long)lampi_host_pinned_bytes();
     for (int r = 0; r < rounds; ++r) {
         if (lampi_bcopy_uicrc(buf.data(), dst.data(), 65456, 65456, 0xFFFFFFFFu) == 0x12345678u) ++bad;
+        if (r % 8 == 0 && lampi_host_msg_csum(buf.data(), buf.size(), 4096, 0, frag.size(), 0xFFFFFFFFu, frag.data(),
+                                              0) != 0)
+            ++bad;
         lampi_host_release();
     }
     const size_t u2 = used();
-    std::printf("rounds %d used_before %zu after_threads %zu after_release %zu bad %u\n", rounds, u0, u1, u2, bad);
+    const long long p2 = (long long)lampi_host_pinned_bytes();
+    std::printf("rounds %d used_before %zu after_threads %zu after_release %zu pinned_before %lld "
+                "pinned_after_threads %lld pinned_after_release %lld bad %u\n",
+                rounds, u0, u1, u2, p0, p1, p2, bad);
     return bad != 0;
 }

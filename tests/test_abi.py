@@ -40,6 +40,61 @@ def test_library_exports_every_declared_symbol():
     assert set(lampi_amd._lib.PROTOTYPES) == set(declared_functions())
 
 
+# the reference's twelve overloads (src/util/MemFunctions.h:43-65) by their mangled names
+REFERENCE_MANGLED = [
+    "_Z5uicrcPKvm", "_Z5uicrcPKvmj", "_Z11bcopy_uicrcPKvPvmm", "_Z11bcopy_uicrcPKvPvmmj",
+    "_Z6uicsumPKvm", "_Z6uicsumPKvmPjS1_", "_Z12bcopy_uicsumPKvPvmm", "_Z12bcopy_uicsumPKvPvmmPjS2_",
+    "_Z4csumPKvm", "_Z4csumPKvmPmS1_", "_Z10bcopy_csumPKvPvmm", "_Z10bcopy_csumPKvPvmmPmS2_",
+    # the rest of MemFunctions.o (MemFunctions.cc:1242-1261, :1380-1393)
+    "_Z24ulm_initialize_crc_tablev", "_Z12poisonMemoryPvli",
+]
+
+
+def test_library_exports_the_reference_cxx_abi():
+    """libmpi can swap MemFunctions.o for -llampi_csum without recompiling: the library defines every
+    function of the reference's object (the twelve overloads, ulm_initialize_crc_table, poisonMemory)
+    under its mangled name -- exactly the set the compiled reference exports."""
+    import lampi_amd
+
+    out = subprocess.run(["nm", "-D", "--defined-only", lampi_amd._lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (_Z\w+)", out))
+    for name in REFERENCE_MANGLED:
+        assert name in exported, name
+    ref = os.path.join(ROOT, "oracle", "_ref", "libref_memfunctions.so")
+    if os.path.exists(ref):  # the reference compiled here exports exactly these
+        rout = subprocess.run(["nm", "-D", "--defined-only", ref], capture_output=True, text=True, check=True).stdout
+        assert set(re.findall(r" T (_Z\w+)", rout)) == set(REFERENCE_MANGLED)
+
+
+def test_object_compiled_against_reference_header_links(tmp_path):
+    """A caller compiled against the REFERENCE's own MemFunctions.h (this container only) links against
+    liblampi_csum.so alone: a relink, no source or header change."""
+    import lampi_amd
+
+    ref_src = "/root/reference/src"
+    if not os.path.exists(os.path.join(ref_src, "util", "MemFunctions.h")):
+        pytest.skip("reference sources absent")
+    src = tmp_path / "ref_caller.cc"
+    src.write_text(r'''
+#include "util/MemFunctions.h"
+unsigned int f(const void *s, void *d, unsigned long n) {
+    unsigned int a = 0, b = 0;
+    unsigned long c = 0, e = 0;
+    return uicrc(s, n) + uicrc(s, n, 1u) + bcopy_uicrc(s, d, n, n) + bcopy_uicrc(s, d, n, n, 1u) + uicsum(s, n) +
+           uicsum(s, n, &a, &b) + bcopy_uicsum(s, d, n, n) + bcopy_uicsum(s, d, n, n, &a, &b) +
+           (unsigned)(csum(s, n) + csum(s, n, &c, &e) + bcopy_csum(s, d, n, n) + bcopy_csum(s, d, n, n, &c, &e));
+}
+void poisonMemory(void *ptr, ssize_t lenInBytes, int pattern);  // src/util/Utility.h:45
+void ulm_initialize_crc_table();                                  // MemFunctions.cc:1242
+void g(void *p) { ulm_initialize_crc_table(); poisonMemory(p, 64, 0x5a5a5a5a); }
+int main(int argc, char **) { return argc > 5 ? (int)f(0, 0, 0) : 0; }
+''')
+    libdir = os.path.dirname(lampi_amd._lib.LIB_PATH)
+    subprocess.run(["g++", "-w", "-I", ref_src, "-I", os.path.join(ref_src, "include"), str(src), "-L", libdir,
+                    "-llampi_csum", "-o", str(tmp_path / "ref_caller")], check=True)
+
+
 def test_library_targets_gfx950():
     """The embedded code object is built for gfx950 (and only for it)."""
     import lampi_amd

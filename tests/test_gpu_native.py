@@ -82,3 +82,25 @@ def test_native_host_staging_does_not_leak(cuda):
     # a leaked context holds >= 1 MiB of device buffers: 1,000 leaks would be >= 1 GiB
     assert f["after_threads"] - f["used_before"] < (64 << 20), r.stdout
     assert f["after_release"] - f["used_before"] < (64 << 20), r.stdout
+    # page-locked host staging (bounce buffers, result words): exactly back where it was after the
+    # thread churn, and none at all once the last context was released
+    assert f["pinned_before"] > 0
+    assert f["pinned_after_threads"] == f["pinned_before"], r.stdout
+    assert f["pinned_after_release"] == 0, r.stdout
+
+
+def test_native_host_message_path_matches_oracle(cuda):
+    """lampi_host_msg_csum / lampi_host_msg_bcopy from a native C++ caller (tests/native/host_msg_caller.cc):
+    GM 65,456-byte payloads in 64 KiB buffers, 4 KiB / 16 KiB / IB 1,976-byte fragments, a fragment
+    larger than a pipeline chunk, short and empty messages, fragment sub-ranges, pinned and pageable
+    sources and rings, both modes, two threads at once; every fragment against the oracle inside the
+    program, every slot byte against the source, sentinels around the slots untouched."""
+    r = subprocess.run([_bin("host_msg_caller"), "6", "2"], capture_output=True, text=True, timeout=600)
+    out = r.stdout
+    assert r.returncode == 0, out[-4000:] + r.stderr[-2000:]
+    assert out.strip().endswith("bad 0 done"), out[-2000:]
+    lines = [ln for ln in out.splitlines() if ln.startswith(("csum ", "bcopy_", "invalid"))]
+    assert lines and all(ln.endswith(" ok") for ln in lines)
+    # 7 shapes x 2 modes x 2 sources x 4 ranges x 3 calls, on 2 threads + the main thread, + 1
+    assert len(lines) == 7 * 2 * 2 * 4 * 3 * (2 + 1) + 1
+    assert "pinned_after_release 0" in out

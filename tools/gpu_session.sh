@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
-#   smoke | tests | tests_bcopy | bench | bench16k | benchsum | benchC | benchD | bcopy | prof | profC | pmc | pmcC | e2e | microbench
+#   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchD | bcopy | prof | profC | pmc | pmcC | e2e | microbench
 # Any failure (a test failure, fault, abort, segfault, timeout or kill) ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -55,6 +55,7 @@ for step in "$@"; do
     tests_chain) run pytest_chain 600 python -m pytest tests/test_gpu_chain.py -m gpu -x -q ;;
     tests_csum64) run pytest_csum64 600 python -m pytest tests/test_gpu_csum64.py -m gpu -x -q ;;
     tests_verify) run pytest_verify 600 python -m pytest tests/test_gpu_verify.py -m gpu -x -q ;;
+    tests_native) run pytest_native 600 python -u -m pytest tests/test_gpu_native.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     sweep) run sweep 500 tools/microbench/frags_sweep ;;
     microbench) run microbench 300 tools/microbench/readbw ;;
     *) echo "unknown step $step"; exit 2 ;;
