@@ -237,6 +237,16 @@ int lampi_header_check_batch(const void *d_hdrs, size_t n, size_t stride, uint32
                              uint32_t word_count, uint32_t csum_offset, uint32_t *d_mask,
                              uint32_t *d_nbad, int mode, void *stream);
 
+/* The IB receiver's header check (ref src/path/ib/path.cc:652-680): header i fails unless the
+ * 32-bit value stored at csum_offset (native byte order, NOT swapped) equals
+ *   CRC mode: uicrc(hdr_i, crclen)     SUM mode: uicsum(hdr_i, crclen) (fresh state)
+ * -- e.g. crclen 68 / csum_offset 68 for an ibDataHdr_t, crclen = length - 4 / csum_offset =
+ * length - 4 for an ACK (ib/sendFrag.cc:306-314, :327-335).  The sender's side of it is
+ * lampi_frag_csum_batch_strided over descriptors {hdr_i, crclen, CRC_INITIAL_REGISTER} with
+ * d_out = d_hdrs + csum_offset and out_stride = stride. */
+int lampi_header_compare_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t csum_offset,
+                               uint32_t *d_mask, uint32_t *d_nbad, int mode, void *stream);
+
 /* CheckData (ref src/path/gm/recvFrag.h:213-257): fragment i fails iff its length is nonzero
  * and d_calc[i] != its expected checksum.  Expected checksums and lengths are 32-bit values
  * read at d_expected + i*expected_stride and d_lengths + i*lengths_stride -- e.g. straight

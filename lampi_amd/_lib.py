@@ -78,6 +78,8 @@ PROTOTYPES = {
                                                ctypes.c_int, c_void_p]),
     "lampi_header_check_batch": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, ctypes.c_uint32,
                                                 ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_int, c_void_p]),
+    "lampi_header_compare_batch": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                                  c_void_p, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_frag_csum_batch_strided": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.c_int, c_void_p]),
     "lampi_check_data_batch": (ctypes.c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_void_p,
                                               c_void_p, c_void_p]),

@@ -2524,6 +2524,33 @@ __global__ void __launch_bounds__(256) header_check_kernel(const uint8_t *__rest
     emit_mask(i, n, bad, mask, nbad);
 }
 
+// The IB variant (ref src/path/ib/path.cc:652-680; senders src/path/ib/sendFrag.cc:306-314, ACKs
+// :327-335): the sender stores uicrc(h, crclen) / uicsum(h, crclen) as it is (not byte-swapped) and
+// the receiver recomputes it over the same crclen bytes and compares it with the stored word.
+// uicsum of a fresh state: little-endian words, a 1-3 byte tail zero-padded in its high bytes.
+__global__ void __launch_bounds__(256) header_compare_kernel(const uint8_t *__restrict__ hdrs, uint32_t n,
+                                                             size_t stride, uint32_t crclen, uint32_t csum_offset,
+                                                             int mode, const uint32_t *__restrict__ img,
+                                                             uint32_t *mask, uint32_t *nbad) {
+    __shared__ uint32_t S[1024];
+    if (mode == LAMPI_CSUM_CRC32) stage_slices(S, img);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    if (i < n) {
+        gbyte *h = (gbyte *)(hdrs + (size_t)i * stride);
+        uint32_t v = 0;
+        if (mode == LAMPI_CSUM_CRC32) {
+            v = thread_crc(S, h, crclen, kCrcInit);
+        } else {
+            uint32_t w = 0;
+            for (; w + 4 <= crclen; w += 4) v += *(guint *)(h + w);
+            for (uint32_t b = 0; w + b < crclen; ++b) v += (uint32_t)h[w + b] << (8 * b);
+        }
+        bad = v != *(guint *)(h + csum_offset);
+    }
+    emit_mask(i, n, bad, mask, nbad);
+}
+
 // CheckData (ref src/path/gm/recvFrag.h:213-257): fragment i is corrupt iff its length is
 // nonzero and calc[i] != expected; expected values and lengths are read through byte strides
 // (e.g. straight out of an array of headers: dataChecksum @64, dataLength @20).
@@ -3205,6 +3232,15 @@ hipError_t launch_header_check(const uint8_t *hdrs, size_t n, size_t stride, uin
     if (e != hipSuccess || n == 0) return e;
     hipLaunchKernelGGL(header_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hdrs, (uint32_t)n,
                        stride, hdr_bytes, word_count, csum_offset, mode, img, mask, nbad);
+    return hipGetLastError();
+}
+
+hipError_t launch_header_compare(const uint8_t *hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t csum_offset,
+                                 int mode, const uint32_t *img, uint32_t *mask, uint32_t *nbad, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(nbad, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess || n == 0) return e;
+    header_compare_kernel<<<dim3((unsigned)((n + 255) / 256)), 256, 0, s>>>(hdrs, (uint32_t)n, stride, crclen,
+                                                                         csum_offset, mode, img, mask, nbad);
     return hipGetLastError();
 }
 

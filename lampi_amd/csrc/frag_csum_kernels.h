@@ -50,6 +50,8 @@ hipError_t launch_header_csum(const uint8_t *hdrs, size_t n, size_t stride, uint
 hipError_t launch_header_check(const uint8_t *hdrs, size_t n, size_t stride, uint32_t hdr_bytes, uint32_t word_count,
                                uint32_t csum_offset, int mode, const uint32_t *img, uint32_t *mask, uint32_t *nbad,
                                hipStream_t s);
+hipError_t launch_header_compare(const uint8_t *hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t csum_offset,
+                                 int mode, const uint32_t *img, uint32_t *mask, uint32_t *nbad, hipStream_t s);
 hipError_t launch_check_data(const uint32_t *calc, const uint8_t *expected, size_t exp_stride, const uint8_t *lengths,
                              size_t len_stride, size_t n, uint32_t *mask, uint32_t *nbad, hipStream_t s);
 // dst + i*stride = vals[i] (4-byte aligned records).

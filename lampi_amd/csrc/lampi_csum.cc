@@ -715,6 +715,22 @@ int lampi_header_check_batch(const void *d_hdrs, size_t n, size_t stride, uint32
                                       img, d_mask, d_nbad, (hipStream_t)stream));
 }
 
+int lampi_header_compare_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t csum_offset,
+                               uint32_t *d_mask, uint32_t *d_nbad, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    if (!d_nbad || (n && (!d_hdrs || !d_mask)) || ((uintptr_t)d_hdrs & 3u) || (stride & 3u) || (csum_offset & 3u) ||
+        n > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    return to_int(launch_header_compare((const uint8_t *)d_hdrs, n, stride, crclen, csum_offset, mode, img, d_mask,
+                                        d_nbad, (hipStream_t)stream));
+}
+
 int lampi_check_data_batch(const uint32_t *d_calc, const void *d_expected, size_t expected_stride,
                            const void *d_lengths, size_t lengths_stride, size_t n, uint32_t *d_mask, uint32_t *d_nbad,
                            void *stream) {

@@ -252,6 +252,18 @@ def header_check_batch(hdrs: torch.Tensor, n: int, stride: int, hdr_bytes: int, 
     return mask, nbad
 
 
+def header_compare_batch(hdrs: torch.Tensor, n: int, stride: int, crclen: int, csum_offset: int, mode: int = CRC32,
+                         stream: torch.cuda.Stream | None = None):
+    """The IB receiver's header check (src/path/ib/path.cc:652-680): uicrc / uicsum of crclen bytes vs the
+    stored, unswapped word at csum_offset; returns (mask, nbad), mask bit set = bad."""
+    _records(hdrs, n, stride, "hdrs")
+    mask, nbad = _mask_out(n, hdrs.device)
+    check(lib().lampi_header_compare_batch(hdrs.data_ptr(), n, stride, crclen, csum_offset, mask.data_ptr(),
+                                           nbad.data_ptr(), mode, _stream_handle(stream)),
+          "lampi_header_compare_batch")
+    return mask, nbad
+
+
 def check_data_batch(calc: torch.Tensor, expected: torch.Tensor, expected_stride: int = 4,
                      lengths: torch.Tensor | None = None, lengths_stride: int = 4, n: int | None = None,
                      expected_offset: int = 0, lengths_offset: int = 0, stream: torch.cuda.Stream | None = None):

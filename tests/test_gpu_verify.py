@@ -166,3 +166,70 @@ def test_verify_rejects_misaligned(cuda):
     assert rc != 0
     rc = lampi_amd.lib().lampi_frag_csum_batch_strided(buf.data_ptr(), 4, buf.data_ptr(), 70, 0, None)
     assert rc != 0
+
+
+# ---- the IB variant: uicrc/uicsum of the header stored unswapped and compared by the receiver ----
+# ibDataHdr_t is 72 bytes with the header checksum last (ref src/path/ib/header.h:48-62); the sender
+# stores uicrc(p, 68) / uicsum(p, 68) (src/path/ib/sendFrag.cc:306-314), an ACK uicrc(p, len - 4)
+# (:327-335); the receiver recomputes over the same bytes and compares (src/path/ib/path.cc:652-680).
+IB_BUF = 2048  # ibData2KMsg_t: header + 1,976 payload bytes (ib/header.h:75-80)
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("crclen,stride", [(68, IB_BUF), (60, 64), (57, 64), (67, 1096)])
+def test_ib_header_stamp_and_compare(cuda, oracle, mode, crclen, stride):
+    """Sender (lampi_frag_csum_batch_strided over one descriptor per header, stored at crclen rounded up to
+    a word) matches the oracle's uicrc/uicsum; the receiver check (lampi_header_compare_batch) passes every
+    record and flags exactly the corrupted ones, including the reference's |= 0xA4A4 corruption."""
+    import torch
+
+    dv = _dv()
+    n = 6000
+    off = (crclen + 3) // 4 * 4  # where the sender keeps the checksum word
+    rec = torch.empty(n * stride, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(rec, seed=90 + crclen)
+    v = rec.view(n, stride)
+    descs = dv.make_descs(rec, np.arange(n, dtype=np.uint64) * stride, np.full(n, crclen))
+    dv.frag_csum_batch_strided(descs, rec, stride, offset=off, mode=mode)
+    host = v.cpu().numpy()
+    stored = host[:, off:off + 4].copy().view("<u4").ravel()
+    if mode == 0:
+        want = np.array([oracle.uicrc(host[i, :crclen], crclen) for i in range(n)], np.uint32)
+    else:
+        want = np.array([oracle.uicsum(host[i, :crclen], crclen)[0] for i in range(n)], np.uint32)
+    assert np.array_equal(stored, want)
+    mask, nbad = dv.header_compare_batch(rec, n, stride, crclen, off, mode=mode)
+    assert int(nbad.item()) == 0 and not dv.mask_bits(mask, n).any()
+
+    rng = np.random.default_rng(crclen)
+    bad = np.sort(rng.choice(n, size=555, replace=False))
+    for k, i in enumerate(bad):
+        if k % 5 == 0:  # ENABLE_RELIABILITY's artificial corruption of the stored checksum
+            w = int(stored[i])
+            w2 = w | 0xA4A4 if (w | 0xA4A4) != w else w ^ 0xA4A4
+            host[i, off:off + 4] = np.frombuffer(w2.to_bytes(4, "little"), np.uint8)
+        else:  # a flipped byte in the checked header bytes
+            host[i, int(rng.integers(0, crclen))] ^= np.uint8(rng.integers(1, 256))
+    v.copy_(torch.from_numpy(host).to(cuda))
+    mask, nbad = dv.header_compare_batch(rec, n, stride, crclen, off, mode=mode)
+    assert np.array_equal(np.nonzero(dv.mask_bits(mask, n))[0], bad)
+    assert int(nbad.item()) == bad.size
+    # the bytes past crclen (e.g. the payload of an ibData2KMsg) are not part of the check
+    if stride > off + 8:
+        host[:, off + 4:] ^= np.uint8(0x5A)
+        v.copy_(torch.from_numpy(host).to(cuda))
+        mask, nbad = dv.header_compare_batch(rec, n, stride, crclen, off, mode=mode)
+        assert np.array_equal(np.nonzero(dv.mask_bits(mask, n))[0], bad)
+
+
+def test_ib_header_compare_rejects_bad_arguments(cuda):
+    import torch
+
+    import lampi_amd
+
+    buf = torch.zeros(4096, dtype=torch.uint8, device=cuda)
+    c = lampi_amd.lib()
+    assert c.lampi_header_compare_batch(buf.data_ptr() + 1, 4, 72, 68, 68, buf.data_ptr(), buf.data_ptr(), 0, None) != 0
+    assert c.lampi_header_compare_batch(buf.data_ptr(), 4, 70, 68, 68, buf.data_ptr(), buf.data_ptr(), 0, None) != 0
+    assert c.lampi_header_compare_batch(buf.data_ptr(), 4, 72, 68, 66, buf.data_ptr(), buf.data_ptr(), 0, None) != 0
+    assert c.lampi_header_compare_batch(buf.data_ptr(), 4, 72, 68, 68, buf.data_ptr(), buf.data_ptr(), 3, None) != 0
