@@ -16,6 +16,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lampi_csum.h")
 
 CRC32 = 0  # enum lampi_csum_mode (include/lampi_csum.h)
 SUM32 = 1
+BY_BYTES = 0x100  # LAMPI_CSUM_BY_BYTES: byte-balanced descriptor batches (OR'ed into the mode)
 CRC_POLYNOMIAL = 0x04C11DB7  # ref src/util/MemFunctions.h:36
 CRC_INITIAL_REGISTER = 0xFFFFFFFF  # ref src/util/MemFunctions.h:37
 

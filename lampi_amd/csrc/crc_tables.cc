@@ -134,6 +134,12 @@ std::vector<uint32_t> build_table_image() {
         abort();
     }
 
+    // the table-light fused copy's uniform shifts: 1024 bytes, then 16 * 2^j bytes (j = 0..5)
+    for (int t = 0; t < kLightTables; ++t) {
+        const uint64_t nbytes = t == 0 ? 1024u : (16ull << (t - 1));
+        nibble_tables(swapped(shift_matrix(nbytes)), &img[kImgLightNib + 128 * (size_t)t]);
+    }
+
     // powers of two for arbitrary shifts, normal domain (squaring from one byte)
     Gf2Mat pw = shift_matrix(1);
     for (int e = 0; e < 32; ++e) {

@@ -46,7 +46,16 @@ constexpr size_t kImgPow2Cols = kImgHorner16Cols + 32;
 //   [kImgZero, +16)          zeros: the row loads of crc_stream_kernel read chunks wholly outside a
 //                            fragment from here
 constexpr size_t kImgZero = kImgPow2Cols + 1024;
-constexpr size_t kImgWords = kImgZero + 16;
+//   [kImgLightNib, +7*128)   nibble tables (swapped domain, out[p*16 + v] of nibble_tables) of the
+//                            table-light fused copy (crc_light_copy_kernel): table 0 shifts by 1024
+//                            bytes (a lane's next chunk of the row), table 1 + j by 16 * 2^j bytes,
+//                            j = 0..5 (the six levels of its lane tree)
+constexpr size_t kImgLightNib = kImgZero + 16;
+constexpr int kLightTables = 7;
+//   [kImgTrash, +256)        write-only: 16 bytes per lane that the table-light copy's padding chunks
+//                            are stored to (straight-line stores, so the compiler's waits stay exact)
+constexpr size_t kImgTrash = kImgLightNib + kLightTables * 128;
+constexpr size_t kImgWords = kImgTrash + 256;
 constexpr int kChunkBytes = 16;                          // coalesced layout: 16-byte chunks
 constexpr int kChunkStep = kRowBytes / 4 - kChunkBytes;  // 1008 zero bytes between a lane's chunks
 

@@ -46,10 +46,6 @@
 #include "crc_tables.h"
 #include "frag_csum_kernels.h"
 
-#ifndef LAMPI_EXP
-#define LAMPI_EXP 0
-#endif
-
 namespace lampi {
 
 namespace {
@@ -80,49 +76,21 @@ typedef __attribute__((address_space(1))) u32x4_a4 gwu32x4_a4;
 
 // Copy destinations are written with non-temporal stores (the `nt` bit: streamed past the caches
 // the payload is not re-read from): +1.3 to +2 points of read + write bandwidth in the copy shapes
-// measured (tools/microbench/copy5.hip, profiles/r02_copy5.txt).  -DLAMPI_NT_STORES=0 for A/B runs.
-#ifndef LAMPI_NT_STORES
-#define LAMPI_NT_STORES 1
-#endif
+// measured (tools/microbench/copy5.hip, profiles/r02_copy5.txt).
 // (The asm-issued row loads stay cached: with the nt bit, read-only CRC fell from 80.6% to 42.3%
 // and config C from 73.6% to 44.1%; profiles/r02_sumcopy/ab_ntal/.)
-#if LAMPI_NT_STORES
 #define LAMPI_ST_NT " nt"
-#else
-#define LAMPI_ST_NT ""
-#endif
-__device__ __forceinline__ void st16(gwu32x4_a4 *p, const u32x4 &v) {
-#if LAMPI_NT_STORES
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
-}
+__device__ __forceinline__ void st16(gwu32x4_a4 *p, const u32x4 &v) { __builtin_nontemporal_store(v, p); }
 // source loads of the SUM copy kernels: non-temporal (read once; same-box A/B, profiles/r02_sumcopy/
 // ab_ntl/: descriptors +1 to +2.5 points, messages, slots and +1 destinations +0.5 to +1.4)
-#ifndef LAMPI_NT_LOADS
-#define LAMPI_NT_LOADS 1
-#endif
-__device__ __forceinline__ u32x4 ld16u(gu32x4_a1 *p) {
-#if LAMPI_NT_LOADS
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
+__device__ __forceinline__ u32x4 ld16u(gu32x4_a1 *p) { return __builtin_nontemporal_load(p); }
 // coalesced row loads of crc_rows_kernel (fused CRC copies of descriptors, the receive step,
 // ragged messages): non-temporal, same-box A/B (profiles/r02_sumcopy/ab_cntl/) descriptors, +1
 // destinations, the receive step and GM 65,456-byte slots +0.5 to +1 point.  The same bit on
 // crc_regular_kernel<copy>'s asm loads cost 1.6-2.2 points there (not used).
 __device__ __forceinline__ u32x4 ld16c(gu32x4_a1 *p) { return __builtin_nontemporal_load(p); }
 typedef __attribute__((address_space(1))) u32x4_a1 gwu32x4_a1;  // unaligned 16-byte stores
-__device__ __forceinline__ void st16u(gwu32x4_a1 *p, const u32x4 &v) {
-#if LAMPI_NT_STORES
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
-}
+__device__ __forceinline__ void st16u(gwu32x4_a1 *p, const u32x4 &v) { __builtin_nontemporal_store(v, p); }
 
 struct FragInfo {
     gbyte *addr;
@@ -306,6 +274,41 @@ template <class S>
 struct IsRecv : std::false_type {};
 template <>
 struct IsRecv<RecvSource> : std::true_type {};
+
+// Byte-balanced descriptor batches (launch_crc_desc / launch_sum_desc for n <= kPlanMax): plan_kernel
+// cuts every fragment longer than the plan's window B into segments of at most B bytes and groups the
+// segments into workgroups by bytes, not by count.  A segment is checksummed like a fragment of its
+// own -- CRC from the fragment's register (its first segment) or from 0 (the others), SUM from a fresh
+// state -- and the kernel joins the parts of a split fragment: crc(s, A||B) = shift_|B|(crc(s, A)) ^
+// crc(0, B), so each part is shifted past the rest of its fragment and XORed into out[f] (zeroed by
+// the plan); sums simply add.  CRC segments are cut from the fragment's end (every shift is a whole
+// number of 4 KiB rows), SUM segments from its start (every segment on the fragment's word grid).
+struct SegDesc {
+    uint32_t frag;  // the descriptor it belongs to
+    uint32_t off;   // its first byte in the fragment (0: the fragment's first segment, which takes its register)
+    uint32_t len;
+    uint32_t rows;  // bit 31: the fragment is split; bits 0..30: 4 KiB rows of it after this segment (CRC)
+};
+static_assert(sizeof(SegDesc) == 16, "plan layout");
+constexpr uint32_t kSegSplit = 1u << 31;
+
+// (the plan reads only the lengths; address and register come from the descriptor itself)
+struct SegSource {
+    static constexpr bool kCopy = false;
+    static constexpr bool kPhase = false;
+    const SegDesc *s;
+    const lampi_frag_desc *d;
+    __device__ FragInfo get(size_t j) const {
+        const SegDesc x = s[j];
+        const lampi_frag_desc D = d[x.frag];
+        return {(gbyte *)(uintptr_t)(D.addr + x.off), x.len, x.off == 0u ? D.partial : 0u, nullptr, 0u};
+    }
+};
+
+template <class S>
+struct IsSeg : std::false_type {};
+template <>
+struct IsSeg<SegSource> : std::true_type {};
 
 // every kernel stores a fragment's checksum through this: receive sources also decide it
 template <class Src, class Acc>
@@ -1272,6 +1275,43 @@ constexpr RowShifts row_shifts() {
 constexpr RowShifts kRowShift = row_shifts();
 static_assert(gf_mulmod(0x80000000u, 2u) == 0x04C11DB7u, "x^31 * x = x^32 = P - x^32");
 
+// The same multiplications as columns: kRowCols.c[j][i] = x^i * kRowShift.k[j] mod P, so
+// v * kRowShift.k[j] = XOR of the columns of v's set bits -- 32 independent select-and-XORs on
+// four accumulators instead of gf_mulmod's 32 dependent shift-reduce steps (a single thread's join
+// tail: each multiply ~0.5 us as a dependent chain).
+struct RowCols {
+    uint32_t c[20][32];
+};
+constexpr RowCols row_cols() {
+    RowCols t{};
+    for (int j = 0; j < 20; ++j)
+        for (int i = 0; i < 32; ++i) t.c[j][i] = gf_mulmod(1u << i, kRowShift.k[j]);
+    return t;
+}
+constexpr RowCols kRowCols = row_cols();
+
+template <int J>
+__device__ __forceinline__ uint32_t mul_row_shift(uint32_t v) {
+    uint32_t r[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t m = (uint32_t)((int32_t)(v << (31 - i)) >> 31);  // bit i of v as a mask
+        r[i & 3] ^= m & kRowCols.c[J][i];
+    }
+    return (r[0] ^ r[1]) ^ (r[2] ^ r[3]);
+}
+
+// v (normal domain) * x^(8 * 4096 * h) mod P: the register after h rows of zero bytes, h < 2^20
+template <int J = 0>
+__device__ __forceinline__ uint32_t shift_rows(uint32_t v, uint32_t h) {
+    if constexpr (J < 20) {
+        if ((h >> J) & 1u) v = mul_row_shift<J>(v);
+        return (h >> (J + 1)) ? shift_rows<J + 1>(v, h) : v;
+    } else {
+        return v;
+    }
+}
+
 // C (swapped domain) after 64*m zero bytes, m < 2^26: the low six bits of m through lane
 // (63 - (m & 63))'s combine column in LDS, the rows (h = m >> 6, 4096 bytes each) as products
 // with compile-time constants x^(8 * 4096 * 2^j) mod P -- no memory traffic (the shift-by-2^e
@@ -1283,13 +1323,7 @@ __device__ uint32_t shift_pieces(const uint32_t *lds, const uint32_t *__restrict
     const uint32_t l = (uint32_t)(m & 63u);
     if (l) C = combine_at(lds, comb_col(63u - l), C);
     const uint32_t h = (uint32_t)(m >> 6);
-    if (h) {
-        uint32_t c = __builtin_bswap32(C);
-#pragma unroll
-        for (int j = 0; j < 20; ++j)
-            if ((h >> j) & 1u) c = gf_mulmod(c, kRowShift.k[j]);
-        C = __builtin_bswap32(c);
-    }
+    if (h) C = __builtin_bswap32(shift_rows(__builtin_bswap32(C), h));
     return C;
 }
 
@@ -1662,7 +1696,8 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 // profiles/r01_stream_ablation.txt.)
 template <class Src, int kD = 3, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kWaveCap > 0 ? kWaveCap : 1)))
-crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
+crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out,
+                  const uint32_t *__restrict__ plan) {
     static_assert(!Src::kCopy, "fused copies run crc_rows_kernel / sum_rows_kernel");
     constexpr int kPB = 64;  // piece bytes
     constexpr uint32_t kThreads = 64 * kWv;
@@ -1680,8 +1715,14 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     __shared__ uint64_t wpieces[kWv];
     __shared__ uint32_t wcount[kWv];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, t = threadIdx.x;
-    const size_t base = (size_t)blockIdx.x * fpg;
-    const uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
+    size_t base = (size_t)blockIdx.x * fpg;
+    uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
+    if constexpr (IsSeg<Src>::value) {  // the plan's workgroups: plan[0] of them, segments [plan[1+i], plan[2+i])
+        const uint32_t g = plan[0];
+        if (blockIdx.x >= g) return;  // the launch is sized for the largest plan
+        base = plan[1 + blockIdx.x];
+        nwg = plan[2 + blockIdx.x] - (uint32_t)base;
+    }
 
     FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
     if (t < nwg) mine = src.get(base + t);
@@ -1818,7 +1859,304 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     __syncthreads();
     if (gown != ~0u) sres[sj[gown]] = kSum ? sjoin[t] : __builtin_bswap32(sjoin[t]);
     __syncthreads();
-    if (t < nwg) emit(src, out, base + t, sres[t], mine);
+    if (t >= nwg) return;
+    if constexpr (IsSeg<Src>::value) {  // a segment: its fragment's value, or its part of a split one
+        const SegDesc x = src.s[base + t];
+        uint32_t v = sres[t];
+        if (!(x.rows & kSegSplit)) {
+            out[x.frag] = v;
+        } else if constexpr (kSum) {
+            atomicAdd(out + x.frag, v);
+        } else {
+            atomicXor(out + x.frag, shift_rows(v, x.rows & ~kSegSplit));  // past the fragment's later rows
+        }
+    } else {
+        emit(src, out, base + t, sres[t], mine);
+    }
+}
+
+// The byte-balanced plan of a descriptor batch (n <= kPlanMax fragments, one 1024-thread workgroup):
+//   T = total bytes; the window B = max(ceil(T / gb), min(384 KiB, max(64 KiB, ceil(T / 256)))), rounded
+//   up to a power of two (shifts, not 64-bit divisions: those made a single-threaded plan of 16K
+//   fragments take 60-75 us) -- at most gb windows (gb <= 2048 from the host), ~384-512 KiB per
+//   workgroup (the table staging amortised, as the count split's 96 x 4 KiB) and about 256
+//   workgroups for small batches (the prologue-bound sizes: DESIGN.md 6);
+//   fragments longer than B -> ceil(len / B) segments (SegDesc, in fragment order);
+//   workgroup i = segments [plan[1+i], plan[2+i]): a new one starts at segment 0, every kPlanF-th
+//   segment, and where a segment starts in a new B-byte window of the batch -- at most kPlanF
+//   segments and ~2B bytes each; plan[0] = the number of workgroups.
+// out[f] of a split fragment is zeroed (its parts are XORed / added in).
+constexpr uint32_t kPlanMax = 32768;
+constexpr uint32_t kPlanF = 96;
+
+// exclusive prefix sum over the kT threads of the workgroup (kT = 64: one wave, no barrier)
+template <uint32_t kT>
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *sh, uint64_t *total) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint64_t y = __shfl_up(x, s, 64);
+        if (lane >= (uint32_t)s) x += y;
+    }
+    if constexpr (kT == 64) {
+        *total = __shfl(x, 63, 64);
+        return x - v;
+    } else {
+        if (lane == 63u) sh[w] = x;
+        __syncthreads();
+        uint64_t before = 0, all = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kT / 64; ++i) {
+            if (i < w) before += sh[i];
+            all += sh[i];
+        }
+        __syncthreads();
+        *total = all;
+        return before + x - v;
+    }
+}
+
+// one wave for n <= 64 (a few microseconds less than the 1024-thread plan on every small call),
+// 256 threads up to 2048 fragments, 1024 up to kPlanMax
+template <uint32_t kT, uint32_t kMax>
+__global__ void __launch_bounds__(kT) plan_kernel(const lampi_frag_desc *__restrict__ d, uint32_t n, int sum,
+                                                  uint32_t gb, SegDesc *__restrict__ segs, uint32_t *__restrict__ plan,
+                                                  uint32_t *__restrict__ out) {
+    constexpr uint32_t kPlanThreads = kT;
+    __shared__ uint32_t lens[kMax];
+    __shared__ uint64_t sh[kT / 64 + 1];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < n; i += kPlanThreads) lens[i] = d[i].length;
+    __syncthreads();
+    const uint32_t per = (n + kPlanThreads - 1) / kPlanThreads;
+    const uint32_t f0 = min(n, t * per), f1 = min(n, f0 + per);
+    uint64_t mine = 0;
+    for (uint32_t f = f0; f < f1; ++f) mine += lens[f];
+    uint64_t T = 0;
+    const uint64_t byte0 = block_excl_scan64<kT>(mine, sh, &T);
+    const uint64_t want = max((T + gb - 1) / gb, min((uint64_t)384 << 10, max((uint64_t)64 << 10, (T + 255) / 256)));
+    const uint32_t lb = 64u - (uint32_t)__clzll(want - 1);  // B = 2^lb >= want (>= 64 KiB)
+    const uint64_t B = 1ull << lb;
+    auto nseg = [&](uint32_t len) -> uint32_t { return len > B ? (uint32_t)(((uint64_t)len + B - 1) >> lb) : 1u; };
+    // segment k of a fragment of len bytes cut into K: [a, e)
+    auto seg = [&](uint32_t len, uint32_t K, uint32_t k, uint32_t *a, uint32_t *e) {
+        if (sum) {
+            *a = (uint32_t)((uint64_t)k << lb);
+            *e = (uint32_t)min((uint64_t)len, (uint64_t)(k + 1) << lb);
+        } else {
+            *e = (uint32_t)(len - ((uint64_t)(K - 1 - k) << lb));
+            *a = k == 0 ? 0u : (uint32_t)(*e - B);
+        }
+    };
+    uint64_t kmine = 0;
+    for (uint32_t f = f0; f < f1; ++f) kmine += nseg(lens[f]);
+    uint64_t M = 0;
+    const uint64_t seg0 = block_excl_scan64<kT>(kmine, sh, &M);
+    // the segment before this thread's first one: the last segment of fragment f0 - 1
+    uint64_t prev_len = 0;
+    if (f0 > 0 && f0 < f1) {
+        const uint32_t L = lens[f0 - 1], K = nseg(L);
+        uint32_t a, e;
+        seg(L, K, K - 1, &a, &e);
+        prev_len = e - a;
+    }
+    // pass 1: write the segments, count workgroup starts
+    uint32_t j = (uint32_t)seg0;  // segments < n + gb < 2^32
+    uint64_t P = byte0, starts = 0;
+    uint64_t Pprev = P - prev_len;
+    for (uint32_t f = f0; f < f1; ++f) {
+        const uint32_t L = lens[f], K = nseg(L);
+        if (K > 1) out[f] = 0u;
+        for (uint32_t k = 0; k < K; ++k, ++j) {
+            uint32_t a, e;
+            seg(L, K, k, &a, &e);
+            const uint32_t rows = sum ? 0u : (K - 1 - k) << (lb - 12);
+            segs[j] = SegDesc{f, a, e - a, rows | (K > 1 ? kSegSplit : 0u)};
+            if (j == 0 || j % kPlanF == 0 || (P >> lb) != (Pprev >> lb)) ++starts;
+            Pprev = P;
+            P += e - a;
+        }
+    }
+    uint64_t G = 0;
+    const uint64_t g0 = block_excl_scan64<kT>(starts, sh, &G);
+    // pass 2: the workgroup starts
+    j = (uint32_t)seg0;
+    P = byte0;
+    Pprev = P - prev_len;
+    uint32_t g = (uint32_t)g0;
+    for (uint32_t f = f0; f < f1; ++f) {
+        const uint32_t L = lens[f], K = nseg(L);
+        for (uint32_t k = 0; k < K; ++k, ++j) {
+            uint32_t a, e;
+            seg(L, K, k, &a, &e);
+            if (j == 0 || j % kPlanF == 0 || (P >> lb) != (Pprev >> lb)) plan[1 + g++] = j;
+            Pprev = P;
+            P += e - a;
+        }
+    }
+    if (t == 0) {
+        plan[0] = (uint32_t)G;
+        plan[1 + G] = (uint32_t)M;
+    }
+}
+
+// ---- CRC fused copy of messages, table-light (lampi_msg_bcopy) ------------------------------------
+// The copy shape that reaches ~75% of read + write into GM ring slots on MI355X is one 4 KiB row per
+// wave in short-lived 4-wave workgroups holding at most ~36 KiB of LDS, four per CU (the same with
+// 52 / 80 KiB: 72% / 50%; tools/microbench/copy_occ.hip, profiles/r03/copy_occ.txt).  The 64 KiB
+// table set of the other CRC kernels does not fit that, so this kernel keeps only
+//   [0, 32 KiB)        the slicing tables in 128-byte rows: entry e of S_j, copy c at e*128 + j*32 + 4c.
+//                      Lane octet g reads table q ^ g in instruction q: 32 distinct banks per 32-lane
+//                      group.  One v_perm puts X's byte into bits 8..15 and twice the table offset into
+//                      bits 0..7; a shift right by one makes the address.  Built from compile-time
+//                      constants.
+//   [32 KiB, +3.5 KiB) nibble tables of seven uniform shifts (every lane reads the same 16 entries per
+//                      lookup: conflict free), copied from the table image: 1024 bytes, and 16 * 2^j
+//                      bytes for j = 0..5
+// and no per-lane combine tables.  Lane l holds the 16-byte chunks at 16l + 1024q of its row (q = 0..3,
+// the coalesced layout: each load and store instruction covers 1 KiB).  It CRCs each chunk from a
+// zero register (four independent chains of four words), joins them by Horner over the 1024-byte
+// step, and a six-level DPP tree XORs shift_{16(63-l)}(R_l) over the lanes into lane 63.  A
+// fragment's rows are right-aligned in a frame of R = ceil(L / 4096) rows (the leading padding reads
+// as zeros, free for a zero register) and its register is injected into its first four bytes.
+// R == 1: the row value is the fragment's checksum.  R > 1: row values go to scratch and
+// crc_light_join_kernel shifts each past its fragment's later rows and XORs them.
+// Preconditions (launch_msg_bcopy): base and frag_len and msg_len multiples of 16, dst and dst_stride
+// of 4 (a dword-aligned dwordx4 store runs at the aligned rate).
+constexpr uint32_t kLtNib = 32768;
+constexpr uint32_t kLtBytes = kLtNib + kLightTables * 512;
+
+// slicing tables in 128-byte rows (build_slices' fill with half the row stride)
+__device__ __forceinline__ void build_slices_light(char *b) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t sj = (t & 7u) >> 1, r0 = t >> 3;
+    uint32_t base = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t k = sel4(sj, kSliceBasis.lo[0][i], kSliceBasis.lo[1][i], kSliceBasis.lo[2][i],
+                                kSliceBasis.lo[3][i]);
+        base ^= ((r0 >> i) & 1u) ? k : 0u;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+        const uint32_t v = base ^ sel4(sj, kSliceBasis.hi[0][kk], kSliceBasis.hi[1][kk], kSliceBasis.hi[2][kk],
+                                       kSliceBasis.hi[3][kk]);
+        *reinterpret_cast<u32x4 *>(b + (r0 + 32 * kk) * 128 + (t & 7u) * 16) = u32x4{v, v, v, v};
+    }
+}
+
+// register after the uniform shift of nibble table `tab` (swapped domain)
+template <int kTab>
+__device__ __forceinline__ uint32_t light_shift(const uint32_t *lds, uint32_t C) {
+    constexpr uint32_t base = kLtNib + 512u * kTab;
+    uint32_t r = lds_u32(lds, base + ((C << 2) & 0x3Cu));
+#pragma unroll
+    for (int p = 1; p < 8; ++p) r ^= lds_u32(lds, base + 64u * p + ((C >> (4 * p - 2)) & 0x3Cu));
+    return r;
+}
+
+// four words from a zero register through the compact slicing tables
+__device__ __forceinline__ uint32_t light_chunk(const uint32_t *lds, uint32_t lanec2, const uint32_t sel[4],
+                                                const u32x4 &d) {
+    auto look = [&](uint32_t X) {
+        const uint32_t t0 = lds_u32(lds, __builtin_amdgcn_perm(X, lanec2, sel[0]) >> 1);
+        const uint32_t t1 = lds_u32(lds, __builtin_amdgcn_perm(X, lanec2, sel[1]) >> 1);
+        const uint32_t t2 = lds_u32(lds, __builtin_amdgcn_perm(X, lanec2, sel[2]) >> 1);
+        const uint32_t t3 = lds_u32(lds, __builtin_amdgcn_perm(X, lanec2, sel[3]) >> 1);
+        return Look4{t0, t1, t2, t3};
+    };
+    Look4 t = look(d.x);
+    t = look(xor3(xor3(t.t0, t.t1, t.t2), t.t3, d.y));
+    t = look(xor3(xor3(t.t0, t.t1, t.t2), t.t3, d.z));
+    t = look(xor3(xor3(t.t0, t.t1, t.t2), t.t3, d.w));
+    return xor3(t.t0, t.t1, t.t2) ^ t.t3;
+}
+
+__global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__restrict__ base, size_t msg_len,
+                                                             uint32_t frag_len, uint32_t R, size_t nitems,
+                                                             uint32_t partial, uint8_t *__restrict__ dst,
+                                                             size_t dst_stride, const uint32_t *__restrict__ img,
+                                                             uint32_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const size_t item = (size_t)blockIdx.x * 4 + (t >> 6);  // (fragment, row) of this wave
+    const bool live = item < nitems;
+    const size_t f = live ? item / R : 0;
+    const uint32_t r = live ? (uint32_t)(item - f * R) : 0u;
+    const size_t foff = f * frag_len;
+    const uint32_t L = (uint32_t)min((size_t)frag_len, msg_len - foff);
+    const uint32_t P = R * (uint32_t)kRowBytes - L;  // frame padding (a multiple of 16)
+    // the uniform shift tables from the image (L2) first: vmcnt counts in order, so waiting for this
+    // load leaves the row loads issued after it in flight
+    u32x4 nib = u32x4{0u, 0u, 0u, 0u};
+    if (t < kLightTables * 32) nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+    // the row's chunks: frame offset o = 4096r + 1024q + 16l, fragment byte o - P
+    // (unconditional loads -- padding chunks read the image's zero chunk -- so the four are in flight
+    // together: loads under a branch each got their own vmcnt(0) wait, four round trips per row)
+    u32x4 d[4];
+    int64_t b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        b[q] = (int64_t)r * kRowBytes + 1024 * q + 16 * lane - P;
+        const u32x4 *a = (live && b[q] >= 0) ? (const u32x4 *)(base + foff + b[q]) : (const u32x4 *)(img + kImgZero);
+        d[q] = __builtin_nontemporal_load(a);
+    }
+    // tables: slicing from constants, then the uniform shifts, while the row loads fly
+    build_slices_light(reinterpret_cast<char *>(lds));
+    if (t < kLightTables * 32) reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
+    __syncthreads();
+    if (!live) return;
+    // the copy: every chunk of the fragment, dword-aligned 16-byte stores; padding chunks go to this
+    // lane's trash slot (stores under a branch made the compiler wait for them to complete before the
+    // CRC: it merges the paths' counters)
+    uint8_t *drow = dst + f * dst_stride;
+    uint8_t *trash = (uint8_t *)(uintptr_t)(img + kImgTrash) + 16 * lane;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st16((gwu32x4_a4 *)(b[q] >= 0 ? drow + b[q] : trash), d[q]);
+    // the fragment's register enters as data in its first four bytes (frame offset P)
+    if ((P >> 12) == r && ((P >> 4) & 63u) == lane) {
+        const uint32_t qi = (P >> 10) & 3u, inj = __builtin_bswap32(partial);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if ((uint32_t)q == qi) d[q].x ^= inj;
+    }
+    // lane constants: twice the table offsets j*32 + 4c (c = lane & 7), selectors for table q ^ octet
+    const uint32_t c8 = (lane & 7u) * 8u;
+    const uint32_t lanec2 = c8 | ((c8 + 64u) << 8) | ((c8 + 128u) << 16) | ((c8 + 192u) << 24);
+    const uint32_t g = (lane >> 3) & 3u;
+    uint32_t sel[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t j = (uint32_t)q ^ g;
+        sel[q] = j | ((4u + j) << 8) | 0x0C0C0000u;
+    }
+    const uint32_t c0 = light_chunk(lds, lanec2, sel, d[0]);
+    const uint32_t c1 = light_chunk(lds, lanec2, sel, d[1]);
+    const uint32_t c2 = light_chunk(lds, lanec2, sel, d[2]);
+    const uint32_t c3 = light_chunk(lds, lanec2, sel, d[3]);
+    uint32_t v = light_shift<0>(lds, light_shift<0>(lds, light_shift<0>(lds, c0) ^ c1) ^ c2) ^ c3;
+    // lane tree: after level j the last lane of every 2^(j+1)-lane block holds that block's value
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<1>(lds, v), 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<2>(lds, v), 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<3>(lds, v), 0x114, 0xF, 0xF, false);  // row_shr:4
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<4>(lds, v), 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<5>(lds, v), 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<6>(lds, v), 0x143, 0xC, 0xF, false);  // row_bcast:31
+    if (lane == 63u) out[R == 1 ? f : item] = __builtin_bswap32(v);
+}
+
+// out[f] = XOR over the rows r of fragment f of row value r shifted past the R - 1 - r rows after it
+// (normal domain; one wave per fragment, lanes take rows l, l + 64, ...)
+__global__ void __launch_bounds__(256) crc_light_join_kernel(const uint32_t *__restrict__ rows, size_t n, uint32_t R,
+                                                             uint32_t *__restrict__ out) {
+    const size_t f = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (f >= n) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t acc = 0;
+    for (uint32_t r = lane; r < R; r += 64) acc ^= shift_rows(rows[f * R + r], R - 1 - r);
+    acc = wave_xor(acc);
+    if (lane == 0) out[f] = acc;
 }
 
 // ---- CRC fast path: regular batches -------------------------------------------------------
@@ -2177,10 +2515,8 @@ __device__ __forceinline__ void store_head16(gwbyte *q, const u32x4 &v, uint32_t
 // 0.53 ms, now ahead of sum_rows_kernel's 0.61 at every size), 16 KiB / 65,456-byte descriptors
 // 71.5 / 61.4 -> 69.9 / 58.1%; 64 threads: small fragments faster still (64 B 3.4x) but +8 and +1
 // destinations 66%; 192: 75.7%.  The row kernel keeps 256 (128 / 64: GM slots 75 -> 71 / 64%).
-#ifndef LAMPI_SUMWG_T
-#define LAMPI_SUMWG_T 128
-#endif
-template <class Src, int kT = LAMPI_SUMWG_T>
+constexpr int kSumWgThreads = 128;
+template <class Src, int kT = kSumWgThreads>
 __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
     static_assert(Src::kCopy && !Src::kPhase, "word-grid copy sources only");
     constexpr uint32_t kW = kT / 64;
@@ -2402,10 +2738,8 @@ __global__ void __launch_bounds__(64 * kWv) sum_rows_kernel(Src src, size_t n, u
 // added atomically into out[f], zeroed beforehand (the sum is order-free and a row starts on the
 // fragment's word grid).  Fragment f spans [f*frag_len, min(.., msg_len)); a workgroup takes rows
 // blockIdx.x + k*gridDim.x (one, unless there are more than kMaxWgGrid).
-#ifndef LAMPI_SUMROW_T
-#define LAMPI_SUMROW_T 256
-#endif
-template <int kT = LAMPI_SUMROW_T>
+constexpr int kSumRowThreads = 256;
+template <int kT = kSumRowThreads>
 __global__ void __launch_bounds__(kT) sum_copy_row_kernel(const uint8_t *__restrict__ base, size_t msg_len,
                                                           size_t frag_len, uint32_t rpf, uint32_t nrows,
                                                           uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
@@ -2938,10 +3272,9 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
     // 10-wave workgroups (20 waves/CU): 61% against 69% (4M x 4 KiB); with half the fragments per
     // wave, 4 / 6 waves: descriptors 62-64 / 52% against 74-75% (profiles/r02_crc_copy_fpw/waves/)
     constexpr int kWv = 2 * kWaves;
-#ifndef LAMPI_RCOPY_FPW_MUL
-#define LAMPI_RCOPY_FPW_MUL 2  // in quarters (see LAMPI_CCOPY_FPW_MUL)
-#endif
-    const uint32_t fpw = spread_fpw(std::max(1u, pick_fpw(n, R) / 2 * LAMPI_RCOPY_FPW_MUL / 4), n, kWv, frag_len);
+    // a quarter of the read kernel's fragments per wave: half for the 8-wave workgroup (the same span),
+    // half again for the copy (shorter-lived workgroups, profiles/r02_crc_copy_fpw/: +2-3 points)
+    const uint32_t fpw = spread_fpw(std::max(1u, pick_fpw(n, R) / 4), n, kWv, frag_len);
     const dim3 grid((unsigned)((n + (size_t)kWv * fpw - 1) / ((size_t)kWv * fpw)));
     hipLaunchKernelGGL((crc_rows_kernel<Src, kWv>), grid, dim3(64 * kWv), 0, s, src, n, fpw, img, out);
 }
@@ -2956,11 +3289,9 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
 // With the fragment length known (messages), large fragments are spread as in spread_fpw
 // (16,404 x 65,456 bytes: 6 fragments per workgroup, not 48: CRC 55 -> 62%, SUM 62 -> 74%;
 // profiles/r02_bigfrag_ab.txt).
-#ifndef LAMPI_CRC_FPG
-#define LAMPI_CRC_FPG 96
-#endif
+constexpr uint32_t kCrcFpg = 96;
 static uint32_t frags_per_wg(size_t n, size_t frag_len = 0) {
-    uint32_t fpg = LAMPI_CRC_FPG;
+    uint32_t fpg = kCrcFpg;
     while (fpg > 3 && n / fpg < 256) fpg >>= 1;
     return spread_fpw(fpg, n, 1, frag_len);
 }
@@ -2973,18 +3304,10 @@ constexpr int kStreamD = 2, kStreamK = 1, kStreamWv = 12, kStreamCap = 6;
 // descriptors 78.9 -> 79.1-80.3%; 24 / 32 / 64 fragments 71 / 76.5 / 77.5%; 8-wave workgroups 76.6%;
 // 256-thread workgroups of 8 / 16 / 32 fragments 78.2-78.9 / 77.5-77.9 / 76.4% (4 KiB descriptors
 // 74 / 80 / 77%); 8 waves per SIMD spills (scratch next to the asm load ring: not run).
-#ifndef LAMPI_SUM_WV
-#define LAMPI_SUM_WV 12
-#endif
-#ifndef LAMPI_SUM_CAP
-#define LAMPI_SUM_CAP 6
-#endif
-#ifndef LAMPI_SUM_FPG
-#define LAMPI_SUM_FPG 48
-#endif
-constexpr int kSumWv = LAMPI_SUM_WV, kSumCap = LAMPI_SUM_CAP;
+constexpr int kSumWv = 12, kSumCap = 6;
+constexpr uint32_t kSumFpg = 48;
 static uint32_t sum_frags_per_wg(size_t n, size_t frag_len = 0) {
-    uint32_t fpg = LAMPI_SUM_FPG;
+    uint32_t fpg = kSumFpg;
     while (fpg > 3 && n / fpg < 256) fpg >>= 1;
     return spread_fpw(fpg, n, 1, frag_len);
 }
@@ -2993,13 +3316,52 @@ static dim3 frags_grid(size_t n, uint32_t fpg) { return dim3((unsigned)((n + fpg
 
 static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size_t)kWaves * fpw - 1) / ((size_t)kWaves * fpw))); }
 
+// Descriptor batches of up to kPlanMax fragments with LAMPI_CSUM_BY_BYTES run byte-balanced (plan_kernel,
+// then the piece streams over its segments): the host cannot see the lengths, and a count split leaves
+// a batch of few large fragments to a few workgroups (1 GiB of 4 MiB descriptors: 34% of the roofline).
+// Not the default: the plan launch adds ~10 us to every call (1 x 4 KiB: 7.8 -> 20 us, 4,096 x 4 KiB:
+// 10.6 -> 23 us; profiles/r03/bigdesc_ab.txt).  Larger batches keep the count split.
+template <bool kSum, int kWv, int kCap>
+static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
+                                 hipStream_t s) {
+    // byte windows at most: ~4 workgroups per resident slot for large batches, fewer for small ones
+    // (every window the plan cannot fill is a workgroup that starts and exits)
+    const uint32_t gb = (uint32_t)std::min<size_t>(2048, std::max<size_t>(64, 16 * n));
+    const size_t cap = n + gb;                                                            // segments at most
+    const size_t gmax = 2 + (cap + kPlanF - 1) / kPlanF + gb;                             // workgroups at most
+    const size_t seg_bytes = (cap * sizeof(SegDesc) + 255) & ~(size_t)255;
+    uint8_t *scratch = nullptr;
+    hipError_t e = hipMallocAsync((void **)&scratch, seg_bytes + (gmax + 2) * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    SegDesc *segs = (SegDesc *)scratch;
+    uint32_t *plan = (uint32_t *)(scratch + seg_bytes);
+    if (n <= 64)
+        hipLaunchKernelGGL((plan_kernel<64, 64>), dim3(1), dim3(64), 0, s, d, (uint32_t)n, kSum ? 1 : 0, gb, segs,
+                           plan, out);
+    else if (n <= 2048)
+        hipLaunchKernelGGL((plan_kernel<256, 2048>), dim3(1), dim3(256), 0, s, d, (uint32_t)n, kSum ? 1 : 0, gb, segs,
+                           plan, out);
+    else
+        hipLaunchKernelGGL((plan_kernel<1024, kPlanMax>), dim3(1), dim3(1024), 0, s, d, (uint32_t)n, kSum ? 1 : 0, gb,
+                           segs, plan, out);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL((crc_stream_kernel<SegSource, kStreamD, kStreamK, kSum, kWv, kCap>), dim3((unsigned)gmax),
+                           dim3(64 * kWv), 0, s, SegSource{segs, d}, cap, 0u, img, out, (const uint32_t *)plan);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(scratch, s);
+    return e != hipSuccess ? e : f;
+}
+
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
-                           hipStream_t s) {
+                           hipStream_t s, bool plan) {
     (void)grid;
     if (n == 0) return hipSuccess;
+    if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
     const uint32_t fpg = frags_per_wg(n);
-    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg,
-                       img, out);
+    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
+                       frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
     return hipGetLastError();
 }
 
@@ -3025,7 +3387,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (n == 0) return hipSuccess;
     const uint32_t fpg = frags_per_wg(n, frag_len);
     hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
-                       MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out);
+                       MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out, nullptr);
     return hipGetLastError();
 }
 
@@ -3081,10 +3443,7 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 // profiles/r02_crc_copy_fpw/: message 69.8 -> 72.2%, descriptors 72.1 -> 74.4%, +8 sources
 // 71.8 -> 74.2%, +8 destinations 67.4 -> 69.5-70.4%, the receive step 71.2 -> 72%; a quarter:
 // about the same, +1 destinations 2 points lower; twice: no change; 3/4: 2 points lower)
-#ifndef LAMPI_CCOPY_FPW_MUL
-#define LAMPI_CCOPY_FPW_MUL 2  // in quarters of pick_fpw
-#endif
-    const uint32_t fpw = std::max(1u, pick_fpw(n, (uint32_t)(frag_len / kRowBytes)) * LAMPI_CCOPY_FPW_MUL / 4);
+    const uint32_t fpw = std::max(1u, pick_fpw(n, (uint32_t)(frag_len / kRowBytes)) / 2);  // half the read kernel's
     // (one chain per wave and / or a two-deep ring: within a point of this, profiles/r02_crc_copy_fpw/chains/)
     hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, true>), grid_for(n, fpw), dim3(kBlock), 0, s, base,
                        (uint32_t)n, fpw, frag_len, partial, img, out, dst, dst_stride);
@@ -3095,7 +3454,7 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 // workgroup per fragment (the textbook copy shape).
 template <class Src>
 static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(sum_copy_wg_kernel<Src>, dim3((unsigned)std::min<size_t>(n, kMaxWgGrid)), dim3(LAMPI_SUMWG_T), 0, s, src,
+    hipLaunchKernelGGL(sum_copy_wg_kernel<Src>, dim3((unsigned)std::min<size_t>(n, kMaxWgGrid)), dim3(kSumWgThreads), 0, s, src,
                        n, out);
 }
 
@@ -3145,13 +3504,14 @@ hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t 
 }
 
 hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
-                           hipStream_t s) {
+                           hipStream_t s, bool plan) {
     (void)grid;
     if (n == 0) return hipSuccess;
+    if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
     if (img) {  // piece streams (img: the zero chunk)
         const uint32_t fpg = sum_frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, true, kSumWv, kSumCap>),
-                           frags_grid(n, fpg), dim3(64 * kSumWv), 0, s, DescSource{d}, n, fpg, img, out);
+                           frags_grid(n, fpg), dim3(64 * kSumWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
@@ -3170,13 +3530,49 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (img) {
         const uint32_t fpg = sum_frags_per_wg(n, frag_len);
         hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, true, kSumWv, kSumCap>),
-                           frags_grid(n, fpg), dim3(64 * kSumWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out);
+                           frags_grid(n, fpg), dim3(64 * kSumWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, fpg, img, out,
+                           nullptr);
         return hipGetLastError();
     }
     const uint32_t fpw = pick_fpw(n, 1);
     hipLaunchKernelGGL(sum_rows_kernel<MsgSource>, grid_for(n, fpw), dim3(kBlock), 0, s,
                        MsgSource{base, msg_len, frag_len, 0u}, n, fpw, out);
     return hipGetLastError();
+}
+
+// The table-light CRC copy (crc_light_copy_kernel) takes contiguous messages whose source chunks are all
+// 16-byte aligned and whose destination is dword-aligned.
+static bool light_copy_ok(const uint8_t *base, size_t msg_len, size_t frag_len, const uint8_t *dst, size_t dst_stride,
+                          size_t n) {
+    const size_t R = (frag_len + kRowBytes - 1) / kRowBytes;
+    return msg_len != 0 && frag_len >= kRowBytes && frag_len % 16 == 0 && msg_len % 16 == 0 &&
+           ((uintptr_t)base & 15u) == 0 && ((uintptr_t)dst & 3u) == 0 && dst_stride % 4 == 0 &&
+           frag_len <= (1u << 30) && n * R <= (1ull << 26);  // <= 2^24 workgroups of 256 threads
+}
+
+static hipError_t launch_crc_light_copy(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial,
+                                        uint8_t *dst, size_t dst_stride, size_t n, uint32_t *out, const uint32_t *img,
+                                        hipStream_t s) {
+    const uint32_t R = (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes);
+    const size_t items = n * R;
+    const dim3 grid((unsigned)((items + 3) / 4));
+    if (R == 1) {
+        hipLaunchKernelGGL(crc_light_copy_kernel, grid, dim3(256), 0, s, base, msg_len, (uint32_t)frag_len, R, items,
+                           partial, dst, dst_stride, img, out);
+        return hipGetLastError();
+    }
+    uint32_t *rows = nullptr;
+    hipError_t e = hipMallocAsync((void **)&rows, items * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(crc_light_copy_kernel, grid, dim3(256), 0, s, base, msg_len, (uint32_t)frag_len, R, items,
+                       partial, dst, dst_stride, img, rows);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(crc_light_join_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, rows, n, R, out);
+        e = hipGetLastError();
+    }
+    const hipError_t fe = hipFreeAsync(rows, s);
+    return e != hipSuccess ? e : fe;
 }
 
 hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, uint8_t *dst,
@@ -3186,6 +3582,8 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                          ((uintptr_t)base & 15u) == 0 && ((uintptr_t)dst & 3u) == 0 && dst_stride % 4 == 0 &&
                          n <= 0xFFFFFFFFull;  // dword-aligned dwordx4 stores run at the aligned rate (GM slots)
     if (mode == LAMPI_CSUM_CRC32) {
+        if (light_copy_ok(base, msg_len, frag_len, dst, dst_stride, n))
+            return launch_crc_light_copy(base, msg_len, frag_len, partial, dst, dst_stride, n, out, img, s);
         if (regular) return launch_crc_regular_copy(base, n, frag_len, partial, dst, dst_stride, out, img, s);
         launch_crc_rows_copy(MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n,
                              (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes), img, out, s, frag_len);
@@ -3199,7 +3597,7 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
             const hipError_t e = hipMemsetAsync(out, 0, n * sizeof(uint32_t), s);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(sum_copy_row_kernel<>, dim3((unsigned)std::min<size_t>(n * rpf, kMaxWgGrid)), dim3(LAMPI_SUMROW_T), 0, s,
+        hipLaunchKernelGGL(sum_copy_row_kernel<>, dim3((unsigned)std::min<size_t>(n * rpf, kMaxWgGrid)), dim3(kSumRowThreads), 0, s,
                            base, msg_len, frag_len, (uint32_t)rpf, (uint32_t)(n * rpf), out, dst, dst_stride);
         return hipGetLastError();
     }
@@ -3298,10 +3696,10 @@ hipError_t launch_host_one(const uint8_t *addr, uint32_t len, uint32_t partial, 
     const HostOneSource src{(uint64_t)(uintptr_t)addr, len, partial, sig, seq};
     if (mode == LAMPI_CSUM_CRC32)
         hipLaunchKernelGGL((crc_stream_kernel<HostOneSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), dim3(1),
-                           dim3(64 * kStreamWv), 0, s, src, (size_t)1, 1u, img, out);
+                           dim3(64 * kStreamWv), 0, s, src, (size_t)1, 1u, img, out, nullptr);
     else
         hipLaunchKernelGGL((crc_stream_kernel<HostOneSource, kStreamD, kStreamK, true, kStreamWv, kStreamCap>), dim3(1),
-                           dim3(64 * kStreamWv), 0, s, src, (size_t)1, 1u, img, out);
+                           dim3(64 * kStreamWv), 0, s, src, (size_t)1, 1u, img, out, nullptr);
     return hipGetLastError();
 }
 

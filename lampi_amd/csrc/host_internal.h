@@ -23,10 +23,6 @@ hipError_t launch_msg_csum(const uint8_t *base, size_t msg_len, size_t frag_len,
 hipError_t pinned_alloc(void **p, size_t bytes, unsigned flags);
 void pinned_free(void *p, size_t bytes);
 
-// True when [p, p + len) lies in page-locked host memory the DMA engines can read directly
-// (hipHostMalloc'd or hipHostRegister'ed): both ends are checked.
-bool host_range_pinned(const void *p, size_t len);
-
 // The host-message pipeline's per-thread state (host_msg.cc), released with the rest of the
 // thread's staging by lampi_host_release() and at thread exit.
 void release_pipeline();

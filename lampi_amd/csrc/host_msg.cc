@@ -7,17 +7,19 @@
 // (Quadrics, src/path/quadrics/sendFrag.h:861-872).  Here one call takes a range of those
 // fragments and runs a chunked pipeline on three per-thread streams:
 //
-//   s_in : H2D of chunk i (DMA straight from the caller's buffer when it is page-locked, through
-//          a ring of pinned bounce pieces otherwise)
+//   s_in : H2D of chunk i, straight from the caller's buffer
 //   s_k  : the checksum kernels of chunk i (the same launches as lampi_msg_csum) into a device
 //          array of per-fragment results
 //   s_out: (bcopy) D2H of chunk i's bytes -- the very bytes the kernel checksummed -- into the
-//          caller's fragment slots: one 2D copy per chunk (slot pitch) when the slots are
-//          page-locked, a pinned bounce and a CPU scatter otherwise
+//          caller's fragment slots, one pitched 2D copy per chunk
 //
 // with kBufs device chunks in flight, so chunk i+1 moves over PCIe while chunk i is checksummed
-// and copied out.  The results come back in one D2H at the end.  There is no CPU checksum: the
-// CPU only moves bytes between pageable memory and pinned staging.
+// and copied out.  The results come back in one D2H at the end.  Page-locked and pageable host
+// buffers take the same calls: the runtime stages pageable H2D at the pinned rate (52.7 against
+// 53.3 GiB/s, a CPU copy into pinned bounce buffers reached 25, tools/microbench/pcie_duplex.hip,
+// profiles/r03/pcie_duplex_run*.txt); pageable slots cost the D2H half its rate (19.8 against
+// 32.8 GiB/s beside a concurrent H2D), so NIC rings should be page-locked (lampi_host_register).
+// There is no CPU checksum and no CPU copy of payload bytes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,26 +32,22 @@ namespace lampi {
 namespace {
 
 constexpr int kBufs = 3;                    // device chunks in flight
-constexpr size_t kChunkTarget = 16u << 20;  // bytes per chunk (whole fragments; at least one)
-constexpr int kInSlots = 4;                 // pageable sources: pinned bounce pieces ...
-constexpr size_t kInPiece = 4u << 20;       // ... of this many bytes
+// Bytes per chunk (whole fragments; at least one).  Back-to-back 16 MiB H2D copies ran at 51.3-51.5
+// GiB/s against 52.9-53.3 for 64 MiB ones (profiles/r03/pcie_duplex_run*.txt), and every chunk adds
+// cross-stream waits; three 64 MiB chunks are 192 MiB of HBM.
+constexpr size_t kChunkTarget = 64u << 20;
 
 // Everything a thread's pipeline holds; a plain aggregate, so release() can reset it.
 struct PipeState {
     int dev = -1;
     hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
-    hipEvent_t in_done[kBufs] = {}, k_done[kBufs] = {}, out_done[kBufs] = {}, bin_free[kInSlots] = {};
-    hipEvent_t bout_done[2] = {};
+    hipEvent_t in_done[kBufs] = {}, k_done[kBufs] = {}, out_done[kBufs] = {};
     uint8_t *dchunk = nullptr;  // kBufs chunks of chunk_bytes
     size_t chunk_bytes = 0;
     uint32_t *dres = nullptr;  // per-fragment results of the call
     size_t res_cap = 0;
-    uint32_t *hres = nullptr;  // pinned copy of them (when the caller's array is pageable)
+    uint32_t *hres = nullptr;  // pinned landing place of the results (then copied to the caller's array)
     size_t hres_cap = 0;
-    uint8_t *bin = nullptr;    // pinned bounce pieces for pageable sources (kInSlots x kInPiece)
-    uint32_t bin_next = 0;     // next bounce piece to fill
-    uint8_t *bout = nullptr;   // pinned bounce for pageable slots: two chunks
-    size_t bout_chunk = 0;
 };
 
 struct PipeCtx {
@@ -72,15 +70,9 @@ struct PipeCtx {
         if (p.dchunk) (void)hipFree(p.dchunk);
         if (p.dres) (void)hipFree(p.dres);
         pinned_free(p.hres, p.hres_cap * sizeof(uint32_t));
-        pinned_free(p.bin, kInSlots * kInPiece);
-        pinned_free(p.bout, 2 * p.bout_chunk);
         for (int b = 0; b < kBufs; ++b)
             for (hipEvent_t e : {p.in_done[b], p.k_done[b], p.out_done[b]})
                 if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : p.bin_free)
-            if (e) (void)hipEventDestroy(e);
-        for (hipEvent_t e : p.bout_done)
-            if (e) (void)hipEventDestroy(e);
         for (hipStream_t s : {p.s_in, p.s_k, p.s_out})
             if (s) (void)hipStreamDestroy(s);
         if (have_cur && cur != p.dev) (void)hipSetDevice(cur);
@@ -107,8 +99,6 @@ hipError_t pipe_ctx(PipeState **out) {
         for (int b = 0; b < kBufs; ++b)
             for (hipEvent_t *e : {&p.in_done[b], &p.k_done[b], &p.out_done[b]})
                 TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        for (hipEvent_t &e : p.bin_free) TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        for (hipEvent_t &e : p.bout_done) TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     *out = &p;
     return hipSuccess;
@@ -129,7 +119,7 @@ hipError_t ensure_chunks(PipeState &p, size_t chunk) {
     return hipSuccess;
 }
 
-hipError_t ensure_results(PipeState &p, size_t n, bool host) {
+hipError_t ensure_results(PipeState &p, size_t n) {
     if (p.res_cap < n) {
         if (p.dres) {
             TRY(hipStreamSynchronize(p.s_k));
@@ -140,28 +130,12 @@ hipError_t ensure_results(PipeState &p, size_t n, bool host) {
         TRY(hipMalloc((void **)&p.dres, n * sizeof(uint32_t)));
         p.res_cap = n;
     }
-    if (host && p.hres_cap < n) {
+    if (p.hres_cap < n) {
         pinned_free(p.hres, p.hres_cap * sizeof(uint32_t));
         p.hres = nullptr;
         p.hres_cap = 0;
         TRY(pinned_alloc((void **)&p.hres, n * sizeof(uint32_t), hipHostMallocDefault));
         p.hres_cap = n;
-    }
-    return hipSuccess;
-}
-
-// H2D of nb bytes at h into d on s_in: one DMA from page-locked memory, or bounce pieces.
-hipError_t copy_in(PipeState &p, uint8_t *d, const uint8_t *h, size_t nb, bool pinned) {
-    if (pinned) return hipMemcpyAsync(d, h, nb, hipMemcpyHostToDevice, p.s_in);
-    if (!p.bin) TRY(pinned_alloc((void **)&p.bin, kInSlots * kInPiece, hipHostMallocDefault));
-    for (size_t o = 0; o < nb; o += kInPiece) {
-        const size_t n = std::min(kInPiece, nb - o);
-        const uint32_t j = p.bin_next++ % kInSlots;
-        uint8_t *slot = p.bin + (size_t)j * kInPiece;
-        TRY(hipEventSynchronize(p.bin_free[j]));  // its previous DMA has read it
-        std::memcpy(slot, h + o, n);
-        TRY(hipMemcpyAsync(d + o, slot, n, hipMemcpyHostToDevice, p.s_in));
-        TRY(hipEventRecord(p.bin_free[j], p.s_in));
     }
     return hipSuccess;
 }
@@ -172,8 +146,8 @@ struct Range {
 
 // D2H of a chunk's fragments [f0, f0 + nf) (bytes d, packed frag_len apart; the last one
 // possibly short) into slots h_ring + f*stride, on s_out.
-hipError_t copy_out_pinned(PipeState &p, uint8_t *h_ring, size_t stride, const uint8_t *d, size_t f0, size_t nf,
-                           const Range &r) {
+hipError_t copy_out(PipeState &p, uint8_t *h_ring, size_t stride, const uint8_t *d, size_t f0, size_t nf,
+                    const Range &r) {
     const bool short_tail = f0 + nf == r.nfrag && r.last != r.frag_len;
     const size_t full = nf - (short_tail ? 1 : 0);
     uint8_t *h = h_ring + f0 * stride;
@@ -183,25 +157,6 @@ hipError_t copy_out_pinned(PipeState &p, uint8_t *h_ring, size_t stride, const u
         TRY(hipMemcpy2DAsync(h, stride, d, r.frag_len, r.frag_len, full, hipMemcpyDeviceToHost, p.s_out));
     if (short_tail && r.last)
         TRY(hipMemcpyAsync(h + full * stride, d + full * r.frag_len, r.last, hipMemcpyDeviceToHost, p.s_out));
-    return hipSuccess;
-}
-
-// Pageable slots: the chunk goes to a pinned bounce half (s_out), the CPU scatters it later.
-struct PendingScatter {
-    bool live = false;
-    int half = 0;
-    size_t f0 = 0, nf = 0;
-};
-
-hipError_t scatter(PipeState &p, const PendingScatter &ps, uint8_t *h_ring, size_t stride, const Range &r) {
-    if (!ps.live) return hipSuccess;
-    TRY(hipEventSynchronize(p.bout_done[ps.half]));
-    const uint8_t *b = p.bout + (size_t)ps.half * p.bout_chunk;
-    for (size_t i = 0; i < ps.nf; ++i) {
-        const size_t f = ps.f0 + i;
-        const size_t n = f + 1 == r.nfrag ? r.last : r.frag_len;
-        std::memcpy(h_ring + f * stride, b + i * r.frag_len, n);
-    }
     return hipSuccess;
 }
 
@@ -220,55 +175,35 @@ hipError_t host_msg(const uint8_t *h_msg, size_t msg_len, size_t frag_len, size_
     const size_t fpc = std::max<size_t>(1, kChunkTarget / frag_len);  // fragments per chunk
     const size_t cb = fpc * frag_len;
     TRY(ensure_chunks(p, cb));
-    const bool out_pinned = host_range_pinned(h_out, k_count * sizeof(uint32_t));
-    TRY(ensure_results(p, k_count, !out_pinned));
-    const bool src_pinned = host_range_pinned(h_msg + b0, b1 - b0);
+    TRY(ensure_results(p, k_count));
     const bool copy = h_ring != nullptr;
-    const bool ring_pinned = copy && host_range_pinned(h_ring, (k_count - 1) * stride + r.last);
-    if (copy && !ring_pinned && p.bout_chunk < cb) {
-        pinned_free(p.bout, 2 * p.bout_chunk);
-        p.bout = nullptr;
-        p.bout_chunk = 0;
-        TRY(pinned_alloc((void **)&p.bout, 2 * cb, hipHostMallocDefault));
-        p.bout_chunk = cb;
-    }
 
-    PendingScatter pending;
     const size_t nchunks = (k_count + fpc - 1) / fpc;
     for (size_t i = 0; i < nchunks; ++i) {
         const int b = (int)(i % kBufs);
         const size_t f0 = i * fpc, nf = std::min(fpc, k_count - f0);
         const size_t off = b0 + f0 * frag_len, nb = std::min(nf * frag_len, b1 - off);
         uint8_t *d = p.dchunk + (size_t)b * p.chunk_bytes;
-        // chunk b is free once chunk i - kBufs was checksummed and copied out
-        TRY(hipStreamWaitEvent(p.s_in, p.k_done[b], 0));
-        if (copy) TRY(hipStreamWaitEvent(p.s_in, p.out_done[b], 0));
-        TRY(copy_in(p, d, h_msg + off, nb, src_pinned));
+        // chunk b is free once chunk i - kBufs was checksummed and copied out (the previous call
+        // drained both streams before it returned)
+        if (i >= (size_t)kBufs) {
+            TRY(hipStreamWaitEvent(p.s_in, p.k_done[b], 0));
+            if (copy) TRY(hipStreamWaitEvent(p.s_in, p.out_done[b], 0));
+        }
+        TRY(hipMemcpyAsync(d, h_msg + off, nb, hipMemcpyHostToDevice, p.s_in));
         TRY(hipEventRecord(p.in_done[b], p.s_in));
         TRY(hipStreamWaitEvent(p.s_k, p.in_done[b], 0));
         TRY(launch_msg_csum(d, nb, frag_len, partial, p.dres + f0, mode, dev, img, p.s_k));
         TRY(hipEventRecord(p.k_done[b], p.s_k));
         if (!copy) continue;
         TRY(hipStreamWaitEvent(p.s_out, p.in_done[b], 0));
-        if (ring_pinned) {
-            TRY(copy_out_pinned(p, h_ring, stride, d, f0, nf, r));
-        } else {
-            const int half = (int)(i & 1);  // its previous chunk (i - 2) was scattered below
-            TRY(hipMemcpyAsync(p.bout + (size_t)half * p.bout_chunk, d, nb, hipMemcpyDeviceToHost, p.s_out));
-            TRY(hipEventRecord(p.bout_done[half], p.s_out));
-        }
+        TRY(copy_out(p, h_ring, stride, d, f0, nf, r));
         TRY(hipEventRecord(p.out_done[b], p.s_out));
-        if (!ring_pinned) {
-            TRY(scatter(p, pending, h_ring, stride, r));  // chunk i - 1, while chunk i moves
-            pending = {true, (int)(i & 1), f0, nf};
-        }
     }
-    if (copy && !ring_pinned) TRY(scatter(p, pending, h_ring, stride, r));
-    uint32_t *res = out_pinned ? h_out : p.hres;
-    TRY(hipMemcpyAsync(res, p.dres, k_count * sizeof(uint32_t), hipMemcpyDeviceToHost, p.s_k));
+    TRY(hipMemcpyAsync(p.hres, p.dres, k_count * sizeof(uint32_t), hipMemcpyDeviceToHost, p.s_k));
     TRY(hipStreamSynchronize(p.s_k));
     if (copy) TRY(hipStreamSynchronize(p.s_out));
-    if (!out_pinned) std::memcpy(h_out, p.hres, k_count * sizeof(uint32_t));
+    std::memcpy(h_out, p.hres, k_count * sizeof(uint32_t));
     return hipSuccess;
 }
 

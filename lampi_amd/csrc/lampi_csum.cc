@@ -89,20 +89,6 @@ void pinned_free(void *p, size_t bytes) {
     g_pinned_bytes.fetch_sub((int64_t)bytes, std::memory_order_relaxed);
 }
 
-bool host_range_pinned(const void *p, size_t len) {
-    if (!p || !len) return false;
-    const uint8_t *ends[2] = {(const uint8_t *)p, (const uint8_t *)p + len - 1};
-    for (const uint8_t *q : ends) {
-        hipPointerAttribute_t a;
-        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
-            (void)hipGetLastError();  // pageable memory: not an error of the call
-            return false;
-        }
-        if (a.type != hipMemoryTypeHost) return false;
-    }
-    return true;
-}
-
 [[noreturn]] void die(const char *what, hipError_t e) {
     std::fprintf(stderr, "liblampi_csum: %s failed: %s (%d); no CPU fallback exists\n", what,
                  hipGetErrorString(e), (int)e);
@@ -333,10 +319,10 @@ uint32_t device_crc(HostCtx &c, const Staged &st, uint64_t len, uint32_t partial
         LAMPI_CHECK(launch_host_one(st.base, (uint32_t)len, partial, res, LAMPI_CSUM_CRC32, img, c.stream,
                                     signal_word(c, seq), seq));
     } else if (n == 1) {
-        LAMPI_CHECK(launch_crc_desc(upload_descs(c, 1, false), 1, res, img, grid, c.stream));
+        LAMPI_CHECK(launch_crc_desc(upload_descs(c, 1, false), 1, res, img, grid, c.stream, false));
     } else {
         ensure(c.dvals, c.vcap, (size_t)n + 4);
-        LAMPI_CHECK(launch_crc_desc(upload_descs(c, n, st.zero_copy), n, c.dvals, img, grid, c.stream));
+        LAMPI_CHECK(launch_crc_desc(upload_descs(c, n, st.zero_copy), n, c.dvals, img, grid, c.stream, false));
         LAMPI_CHECK(launch_crc_combine(c.dvals, n, combine_tables(c, B), next_pow2(n), res, c.stream,
                                        signal_word(c, seq), seq));
     }
@@ -370,7 +356,7 @@ uint32_t device_sum(HostCtx &c, const Staged &st, uint64_t len, unsigned int *pi
     }
     if (n) {
         const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
-        LAMPI_CHECK(launch_sum_desc(d, n, c.dvals, nullptr, grid, c.stream));
+        LAMPI_CHECK(launch_sum_desc(d, n, c.dvals, nullptr, grid, c.stream, false));
     }
     LAMPI_CHECK(launch_sum_finish(c.dvals, n, st.base, len, *pint, *plen, out3, c.stream, signal_word(c, seq), seq));
     wait_done(c, seq);
@@ -549,6 +535,8 @@ int lampi_frag_csum64_batch(const lampi_frag_desc *d_descs, size_t n, uint64_t *
 }
 
 int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
+    const bool by_bytes = (mode & LAMPI_CSUM_BY_BYTES) != 0;
+    mode &= ~LAMPI_CSUM_BY_BYTES;
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;
     if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);
@@ -559,8 +547,8 @@ int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_
     const uint32_t *img = nullptr;
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
-    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_desc(d_descs, n, d_out, img, crc_grid(dev), s));
-    return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s));
+    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_desc(d_descs, n, d_out, img, crc_grid(dev), s, by_bytes));
+    return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s, by_bytes));
 }
 
 int lampi_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode,
@@ -579,7 +567,8 @@ int lampi_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uin
 
 int lampi_frag_csum_batch_strided(const lampi_frag_desc *d_descs, size_t n, void *d_out, size_t out_stride, int mode,
                                   void *stream) {
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    const int base_mode = mode & ~LAMPI_CSUM_BY_BYTES;
+    if (base_mode != LAMPI_CSUM_CRC32 && base_mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;
     if (!d_descs || !d_out || ((uintptr_t)d_out & 3u) || (out_stride & 3u) || out_stride < 4 || n > 0xFFFFFFFFull)
         return to_int(hipErrorInvalidValue);

@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ._lib import CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
+from ._lib import BY_BYTES, CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
 
 __all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
            "make_descs", "make_copy_descs", "as_u32", "chain_csum_batch", "header_csum_batch", "header_check_batch", "check_data_batch",
@@ -98,8 +98,9 @@ def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC3
 
 
 def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
-                    stream: torch.cuda.Stream | None = None) -> torch.Tensor:
-    """out[i] = checksum of fragment descs[i] (piece streams: fragments of any size share rows)."""
+                    stream: torch.cuda.Stream | None = None, by_bytes: bool = False) -> torch.Tensor:
+    """out[i] = checksum of fragment descs[i] (piece streams: fragments of any size share rows).
+    by_bytes: LAMPI_CSUM_BY_BYTES -- plan the work by bytes (large fragments split across workgroups)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 16 if n is None else int(n)
     if out is None:
@@ -107,8 +108,8 @@ def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32
     _require_cuda(out, "out")
     if out.numel() < count:
         raise ValueError("out is too small")
-    check(lib().lampi_frag_csum_batch(descs.data_ptr(), count, out.data_ptr(), mode, _stream_handle(stream)),
-          "lampi_frag_csum_batch")
+    check(lib().lampi_frag_csum_batch(descs.data_ptr(), count, out.data_ptr(), mode | (BY_BYTES if by_bytes else 0),
+                                      _stream_handle(stream)), "lampi_frag_csum_batch")
     return out
 
 

@@ -112,7 +112,7 @@ static void run_suite(int tid, const std::vector<Shape> &shapes, uint8_t *msg_pa
 int main(int argc, char **argv) {
     const uint64_t seed = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 6;
     const int nthreads = argc > 2 ? std::atoi(argv[2]) : 2;
-    const size_t kMsg = (40u << 20) + 12345;  // three 16 MiB pipeline chunks, ragged end
+    const size_t kMsg = (150u << 20) + 12345;  // three 64 MiB pipeline chunks, ragged end
     std::vector<uint8_t> pageable(kMsg + 1);
     oracle_fill_stream(pageable.data(), seed, 0, kMsg);
     uint8_t *pinned = nullptr;
@@ -125,10 +125,10 @@ int main(int argc, char **argv) {
     }
     const std::vector<Shape> shapes = {
         {65456, kMsg, 72 + 8},            // GM: 65,456-byte payloads in 64 KiB buffers after the header
-        {4096, (16u << 20) + 4096 * 5, 0},  // 4 KiB, one chunk + a few fragments, packed slots
+        {4096, (64u << 20) + 4096 * 5, 0},  // 4 KiB, one chunk + a few fragments, packed slots
         {16384, kMsg, 80},                // 16 KiB
         {1976, 3u << 20, 72},             // IB: 1,976-byte payloads
-        {(20u << 20) + 3, kMsg, 16},      // fragments larger than a pipeline chunk
+        {(70u << 20) + 3, kMsg, 16},      // fragments larger than a pipeline chunk
         {4096, 4095, 0},                  // one short fragment
         {4096, 0, 0},                     // empty message: one empty fragment
     };

@@ -213,6 +213,11 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     (65456 * 200 + 4000, 65456, 65536 + 4, 4),  # a last fragment of 4,000 bytes (one partial row)
     (4112 * 3000, 4112, 4112 + 12, 12),       # a second row of 16 bytes per fragment
     (49152 * 100 + 4096 * 5, 49152, 49152, 0),  # a last fragment of 5 of its 12 rows
+    # CRC: 16-byte-multiple messages of fragments >= 4 KiB take the table-light copy
+    # (crc_light_copy_kernel: one row per wave; rows of longer fragments joined by crc_light_join_kernel)
+    ((1 << 20) * 40 + 4096 * 3 + 48, 1 << 20, (1 << 20) + 76, 4),  # 256-row fragments, a 3-row last one
+    (4096 * 100000, 4096, 4096 + 80, 72),       # 4 KiB payloads into GM-style slots, 100,000 rows
+    (65456 * 4000 + 400, 65456, 65536, 72),     # a GM message with a 400-byte last fragment
     # fragments under 2 KiB (SUM: one 128-thread workgroup each, ragged tails)
     (1976 * 5000 + 3, 1976, 2048 + 4, 4),     # shared-memory-sized fragments, ragged tail
     (100 * 3000, 100, 128, 1),                # tiny fragments, byte-misaligned destinations

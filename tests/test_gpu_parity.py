@@ -109,10 +109,12 @@ def test_descriptor_batch_edges_and_alignment(cuda, oracle, mode):
     parts[::3] = 0xFFFFFFFF
     descs = dv.make_descs(base, offs, lens, parts)
     want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
-    for fn in (dv.frag_csum_batch, dv.frag_csum_batch_per_wave):  # piece streams / one wave per fragment
+    by_bytes = lambda d, mode: dv.frag_csum_batch(d, mode=mode, by_bytes=True)  # noqa: E731
+    # piece streams (count split, byte plan) / one wave per fragment
+    for name, fn in (("count", dv.frag_csum_batch), ("bytes", by_bytes), ("per_wave", dv.frag_csum_batch_per_wave)):
         got = dv.as_u32(fn(descs, mode=mode))
         bad = np.nonzero(got != want)[0]
-        assert bad.size == 0, (fn.__name__, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
+        assert bad.size == 0, (name, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
 
 
 def test_descriptor_batch_random(cuda, oracle):
@@ -129,9 +131,10 @@ def test_descriptor_batch_random(cuda, oracle):
     parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
     descs = dv.make_descs(base, offs, lens, parts)
     for mode in (0, 1):
-        got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
         want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
-        assert np.array_equal(got, want)
+        for by_bytes in (False, True):
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, by_bytes=by_bytes))
+            assert np.array_equal(got, want), by_bytes
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
@@ -167,10 +170,12 @@ def test_descriptor_batch_fragments_across_chains(cuda, oracle, case, mode):
     parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
     descs = dv.make_descs(base, offs, lens, parts)
     want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
-    for fn in (dv.frag_csum_batch, dv.frag_csum_batch_per_wave):  # piece streams / one wave per fragment
+    by_bytes = lambda d, mode: dv.frag_csum_batch(d, mode=mode, by_bytes=True)  # noqa: E731
+    # piece streams (count split, byte plan) / one wave per fragment
+    for name, fn in (("count", dv.frag_csum_batch), ("bytes", by_bytes), ("per_wave", dv.frag_csum_batch_per_wave)):
         got = dv.as_u32(fn(descs, mode=mode))
         bad = np.nonzero(got != want)[0]
-        assert bad.size == 0, (fn.__name__, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
+        assert bad.size == 0, (name, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
 
 
 def test_descriptor_batch_maximum_length(cuda):
@@ -203,6 +208,68 @@ def test_descriptor_batch_maximum_length(cuda):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("case", ["one_huge", "few_huge_ragged", "gm_65456", "mb4_x256", "huge_among_tiny"])
+def test_descriptor_batch_byte_balanced(cuda, oracle, case, mode):
+    """With LAMPI_CSUM_BY_BYTES, batches of up to 32,768 descriptors are planned by bytes (plan_kernel): fragments longer than
+    the plan's window are cut into segments checksummed by different workgroups -- CRC segments from
+    the fragment's end, the first from the fragment's register, the others from 0, each part shifted
+    past the rest of its fragment and XORed into out[f]; SUM segments from its start, added.  Every
+    fragment against the oracle (or, for the 1 GiB batches, against lampi_msg_csum over the same
+    bytes, an independent kernel, and a sample against the oracle)."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(abs(hash(case)) % 2**32)
+    MiB = 1 << 20
+    if case == "one_huge":  # one Quadrics-sized checksum-only send at an odd address
+        lens = np.array([9 * MiB + 13], np.uint64)
+        offs = np.array([7], np.uint64)
+    elif case == "few_huge_ragged":
+        lens = np.array([3 * MiB + 1, 0, 17 * MiB + 4095, 2, 6 * MiB, 64 * 1024 + 5, 1 * MiB], np.uint64)
+        offs = (np.concatenate([[3], np.cumsum(lens)[:-1] + 3]) + np.arange(lens.size) * 1) .astype(np.uint64)
+    elif case == "gm_65456":  # 1 GiB of GM payload-sized fragments (a 1 GiB message, 16,404 fragments)
+        n = (1 << 30) // 65456
+        lens = np.full(n, 65456, np.uint64)
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(65456)
+    elif case == "mb4_x256":  # 1 GiB of 4 MiB fragments
+        lens = np.full(256, 4 * MiB, np.uint64)
+        offs = np.arange(256, dtype=np.uint64) * np.uint64(4 * MiB)
+    else:  # a few huge fragments among thousands of tiny ones and empties
+        n = 5000
+        lens = rng.integers(0, 600, size=n).astype(np.uint64)
+        big = rng.choice(n, size=6, replace=False)
+        lens[big] = rng.integers(2 * MiB, 12 * MiB, size=6)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) + np.uint64(1)
+    size = int((offs + lens).max()) + 64
+    base = torch.empty(size, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=55)
+    parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
+    if case in ("gm_65456", "mb4_x256"):
+        parts[:] = 0xFFFFFFFF
+    descs = dv.make_descs(base, offs, lens, parts)
+    got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, by_bytes=True))
+    if case in ("gm_65456", "mb4_x256"):
+        L = int(lens[0])
+        want = dv.as_u32(dv.msg_csum(base[:lens.size * L], L, mode=mode))
+        assert np.array_equal(got, want)
+        idx = rng.choice(lens.size, size=24, replace=False)
+        host = base[:lens.size * L].cpu().numpy()
+        ref = oracle.desc_batch(host, offs[idx], lens[idx], parts[idx].astype(np.uint32) if mode == 0 else None, mode)
+        assert np.array_equal(got[idx], ref)
+    else:
+        host = base.cpu().numpy()
+        want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+    # the same batch again on a fresh output (split fragments are accumulated into out: the plan zeroes them)
+    out = torch.full((lens.size,), -1, dtype=torch.int32, device=cuda)
+    dv.frag_csum_batch(descs, mode=mode, out=out, by_bytes=True)
+    assert np.array_equal(dv.as_u32(out), got)
+    # and the default count split gives the same values
+    assert np.array_equal(dv.as_u32(dv.frag_csum_batch(descs, mode=mode)), got)
+
+
 @pytest.mark.parametrize("n", [30000, 300000])
 def test_descriptor_batch_small_fragments(cuda, oracle, n):
     """Fragments of 16..1024 bytes (multiples of 16, 16-byte aligned) mixed with unaligned,
@@ -227,10 +294,11 @@ def test_descriptor_batch_small_fragments(cuda, oracle, n):
     parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
     descs = dv.make_descs(base, offs, lens, parts)
     for mode in (dv.CRC32, dv.SUM32):
-        got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
         want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == dv.CRC32 else None, mode)
-        bad = np.nonzero(got != want)[0]
-        assert bad.size == 0, [(mode, int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+        for by_bytes in (False, True):  # (above 32,768 descriptors the byte plan falls back to the count split)
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, by_bytes=by_bytes))
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, [(mode, by_bytes, int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
 
 
 def test_kat_check_values(cuda):

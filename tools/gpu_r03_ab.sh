@@ -1,0 +1,15 @@
+#!/usr/bin/env bash
+# Round-3 same-box A/B of the copy and descriptor paths: ab/old.so (the tree before the change) against
+# the current library, interleaved.  Usage: tools/gpu_r03_ab.sh ROUNDS
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=${1:-2}
+for r in $(seq 1 "$R"); do
+  for v in old new; do
+    if [ $v = old ]; then L=ab/old.so; else L=lampi_amd/liblampi_csum.so; fi
+    echo "== round $r $v"
+    LAMPI_CSUM_LIB=$L timeout -k 10 300 python tools/microbench/msg_bcopy_slots.py 2>&1 | grep -v amdgpu.ids || exit 1
+    LAMPI_CSUM_LIB=$L timeout -k 10 300 python bench.py --bcopy --steps 10 --no-cpu-baseline 2>&1 | grep '^{' | \
+      python -c "import json,sys; d=json.loads(sys.stdin.read()); print('bcopy crc msg', d['roofline']['frac'], 'desc', d['descriptor_batch']['frac'], 'src8', d['descriptor_batch_src8']['frac'], 'dst8', d['descriptor_batch_dst8']['frac'], 'dst1', d['descriptor_batch_dst1']['frac'], 'parity', d['parity']['ok_all'])" || exit 1
+  done
+done

@@ -1,6 +1,8 @@
-"""Descriptor batches of large uniform fragments through the piece streams (lampi_frag_csum_batch):
-few fragments per workgroup, so every fragment spans several chains and stream_join decides.
-python tools/microbench/bigdesc_scan.py"""
+"""Descriptor batches of large uniform fragments (lampi_frag_csum_batch), on the default count split and
+with LAMPI_CSUM_BY_BYTES (below 32,768 descriptors: plan_kernel + the piece streams over segments).
+Reports the fraction of the 8 TB/s HBM-read roofline per shape and checks every batch against
+lampi_msg_csum over the same bytes (an independent kernel).
+python tools/microbench/bigdesc_scan.py [crc|sum]"""
 import os
 import sys
 
@@ -11,20 +13,34 @@ import torch  # noqa: E402
 
 from lampi_amd import device as dv  # noqa: E402
 
+mode = dv.SUM32 if len(sys.argv) > 1 and sys.argv[1] == "sum" else dv.CRC32
 buf = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
 dv.fill_stream(buf, seed=9)
-for L in (65536, 262144, 1 << 20, 4 << 20):
-    n = (1 << 30) // L
-    d = dv.make_descs(buf, np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, np.uint64))
-    out = torch.empty(n, dtype=torch.int32, device="cuda")
-    for _ in range(20):
-        dv.frag_csum_batch(d, n=n, out=out)
+
+
+def timed(fn, reps=20):
+    for _ in range(5):
+        fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(20):
-        dv.frag_csum_batch(d, n=n, out=out)
+    for _ in range(reps):
+        fn()
     e1.record()
     torch.cuda.synchronize()
-    t = e0.elapsed_time(e1) / 20 / 1e3
-    print(f"descriptors L={L:8d} n={n:6d} 1 GiB crc {n * L / t / 8e12:.3f} of 8 TB/s", flush=True)
+    return e0.elapsed_time(e1) / reps / 1e3
+
+
+for total, L in ((1 << 30, 65456), (1 << 30, 65536), (1 << 30, 262144), (1 << 30, 1 << 20), (1 << 30, 4 << 20),
+                 (4 << 30, 65456), (4 << 20, 4 << 20), (16 << 20, 4 << 20), (64 << 20, 16 << 20), (16 << 20, 4096),
+                 (1 << 20, 4096), (4096, 4096)):
+    n = total // L
+    d = dv.make_descs(buf, np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, np.uint64))
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    ref = dv.msg_csum(buf[:n * L], L, mode=mode)
+    for by_bytes in (False, True):
+        t = timed(lambda: dv.frag_csum_batch(d, n=n, out=out, mode=mode, by_bytes=by_bytes))
+        ok = bool(torch.equal(out, ref))
+        print(f"{'crc' if mode == dv.CRC32 else 'sum'} {'by_bytes' if by_bytes else 'count   '} descriptors L={L:8d} "
+              f"n={n:6d} {n * L / 2**20:8.1f} MiB {t * 1e6:9.2f} us  {n * L / t / 8e12:.3f} of 8 TB/s  "
+              f"same_as_msg_csum={ok}", flush=True)

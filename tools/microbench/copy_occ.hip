@@ -1,0 +1,108 @@
+// copy_occ.hip -- which copy shapes reach ~78% of read+write on MI355X when every workgroup must
+// also hold LDS (a table-light CRC copy needs ~36 KiB of tables; the current CRC copies hold 64 KiB
+// and top out near 71%).  16 GiB of 4 KiB rows copied to a destination 8 bytes past
+// a 16-byte boundary (GM ring slots after the 72-byte header) or aligned, non-temporal stores:
+//   * short-lived 256-thread workgroups, each wave one row of R KiB (R = 1: one 16-byte chunk per
+//     lane, the textbook copy; R = 4: four coalesced 1 KiB instructions per lane)
+//   * LDS padding per workgroup to cap residency (workgroups per CU = 160 KiB / padding)
+//   * a proxy of the CRC's LDS traffic: X dependent ds_read_b32 per 16 bytes
+// Prints GB/s (read + write) and the fraction of 8 TB/s per configuration.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 copy_occ.hip -o copy_occ
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+
+#define CK(x)                                                   \
+    do {                                                        \
+        hipError_t e_ = (x);                                    \
+        if (e_ != hipSuccess) {                                 \
+            std::printf("%s: %s\n", #x, hipGetErrorString(e_)); \
+            std::exit(1);                                       \
+        }                                                       \
+    } while (0)
+
+template <int R, int LDS_BYTES, int X>
+__global__ void __launch_bounds__(256) copy_rows(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                 size_t rows_total, uint32_t *sink) {
+    __shared__ uint32_t lds[LDS_BYTES / 4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    // a constant fill of the tables' size (the staging a table-light CRC copy would do)
+    for (uint32_t i = threadIdx.x; i < LDS_BYTES / 16; i += 256)
+        reinterpret_cast<u32x4 *>(lds)[i] = u32x4{i, i * 3u, i ^ 7u, i + 11u};
+    const size_t row = ((size_t)blockIdx.x * 4 + wave);  // one row of R KiB per wave
+    if (row * R >= rows_total) return;
+    const u32x4 *s = reinterpret_cast<const u32x4 *>(src + row * R * 1024) + lane;
+    u32x4 v[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) v[q] = __builtin_nontemporal_load(s + 64 * q);
+    __syncthreads();
+    uint32_t acc = lane;
+    if (X > 0) {
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+#pragma unroll
+            for (int k = 0; k < 4 * X; ++k) acc = lds[((acc ^ v[q][k & 3]) & 255u) * 4 + (k & 3)] ^ acc;
+        }
+    }
+    u32x4_a4 *d = reinterpret_cast<u32x4_a4 *>(dst + row * R * 1024) + lane;
+#pragma unroll
+    for (int q = 0; q < R; ++q) __builtin_nontemporal_store(v[q], d + 64 * q);
+    if (X > 0 && acc == 0x9E3779B9u) sink[0] = acc;  // keeps the lookups alive
+}
+
+template <int R, int LDS_BYTES, int X>
+static void run(const uint8_t *src, uint8_t *dst, size_t bytes, uint32_t *sink, const char *tag) {
+    const size_t rows = bytes / 1024;  // 1 KiB units
+    const unsigned grid = (unsigned)((rows / R + 3) / 4);
+    for (int i = 0; i < 3; ++i) copy_rows<R, LDS_BYTES, X><<<grid, 256>>>(src, dst, rows, sink);
+    CK(hipDeviceSynchronize());
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a));
+    const int reps = 10;
+    for (int i = 0; i < reps; ++i) copy_rows<R, LDS_BYTES, X><<<grid, 256>>>(src, dst, rows, sink);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    const double gbs = 2.0 * bytes / (ms / reps * 1e-3) / 1e9;
+    std::printf("%-40s R=%d KiB/wave LDS=%6d B (WG/CU<=%2d) X=%d lookups/16B: %7.1f GB/s = %.3f\n", tag, R, LDS_BYTES,
+                LDS_BYTES ? 163840 / LDS_BYTES : 8, X, gbs, gbs / 8000.0);
+    std::fflush(stdout);
+}
+
+int main() {
+    const size_t N = 16ull << 30;
+    uint8_t *src, *dst;
+    uint32_t *sink;
+    CK(hipMalloc(&src, N));
+    CK(hipMalloc(&dst, N + 4096));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(src, 0x5A, N));
+    uint8_t *d8 = dst + 8;
+    for (int pass = 0; pass < 2; ++pass) {
+        run<1, 16, 0>(src, d8, N, sink, "textbook (1 KiB/wave)");
+        run<1, 36864, 0>(src, d8, N, sink, "textbook + 36 KiB LDS");
+        run<1, 36864, 4>(src, d8, N, sink, "textbook + 36 KiB LDS + lookups");
+        run<2, 36864, 0>(src, d8, N, sink, "2 KiB/wave + 36 KiB LDS");
+        run<2, 36864, 4>(src, d8, N, sink, "2 KiB/wave + 36 KiB LDS + lookups");
+        run<4, 16, 0>(src, d8, N, sink, "4 KiB/wave");
+        run<4, 36864, 0>(src, d8, N, sink, "4 KiB/wave + 36 KiB LDS");
+        run<4, 36864, 4>(src, d8, N, sink, "4 KiB/wave + 36 KiB LDS + lookups");
+        run<4, 40960, 4>(src, d8, N, sink, "4 KiB/wave + 40 KiB LDS + lookups");
+        run<4, 53248, 4>(src, d8, N, sink, "4 KiB/wave + 52 KiB LDS + lookups");
+        run<4, 81920, 4>(src, d8, N, sink, "4 KiB/wave + 80 KiB LDS + lookups");
+        run<4, 24576, 4>(src, d8, N, sink, "4 KiB/wave + 24 KiB LDS + lookups");
+        run<4, 36864, 8>(src, d8, N, sink, "4 KiB/wave + 36 KiB LDS + 2x lookups");
+        run<1, 16, 0>(src, dst, N, sink, "textbook, aligned dst");
+        run<4, 36864, 4>(src, dst, N, sink, "4 KiB/wave + 36 KiB + lookups, aligned");
+    }
+    std::printf("done\n");
+    return 0;
+}

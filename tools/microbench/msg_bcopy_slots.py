@@ -31,6 +31,7 @@ for L, n, stride, off in ((4096, 1 << 20, 4096 + 80, 72),   # 4 KiB payloads in 
         torch.cuda.synchronize()
         s = e0.elapsed_time(e1) / 20 / 1e3
         ok = torch.equal(dst[off:off + n * stride].view(n, stride)[:, :L], msg.view(n, L))
+        same = torch.equal(out, dv.msg_csum(msg, L, mode=mode))  # the read-only kernels, an independent path
         print(f"L={L} slot={stride} {name}: {2 * n * L / s / 1e9:.1f} GB/s = {2 * n * L / s / 8e12:.3f} of 8 TB/s, "
-              f"copy ok {ok}", flush=True)
+              f"copy ok {ok}, checksums = msg_csum {same}", flush=True)
     del msg, dst, out

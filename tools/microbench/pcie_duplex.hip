@@ -130,6 +130,27 @@ int main() {
         rate("D2H into a fresh pageable buffer (runtime staging)", [&] {
             CK(hipMemcpyAsync(fresh2.data(), d2, N, hipMemcpyDeviceToHost, s2));
         });
+        rate_rows("D2H 2D into pageable slots (runtime), 16 MiB pieces", [&] {
+            const size_t pr = (16u << 20) / L;
+            for (size_t r = 0; r < rows; r += pr)
+                CK(hipMemcpy2DAsync(fresh2.data() + 72 + r * S, S, d2 + r * L, L, L, std::min(pr, rows - r),
+                                    hipMemcpyDeviceToHost, s2));
+        });
+        rate_rows("H2D pageable || D2H 2D pageable slots, 16 MiB pieces", [&] {
+            const size_t pr = (16u << 20) / L;
+            for (size_t r = 0; r < rows; r += pr) {
+                CK(hipMemcpyAsync(d + r * L, fresh.data() + r * L, std::min(pr, rows - r) * L, hipMemcpyHostToDevice, s1));
+                CK(hipMemcpy2DAsync(fresh2.data() + 72 + r * S, S, d2 + r * L, L, L, std::min(pr, rows - r),
+                                    hipMemcpyDeviceToHost, s2));
+            }
+        });
+        rate_rows("H2D pageable || D2H 2D pinned slots, 16 MiB pieces", [&] {
+            const size_t pr = (16u << 20) / L;
+            for (size_t r = 0; r < rows; r += pr) {
+                CK(hipMemcpyAsync(d + r * L, fresh.data() + r * L, std::min(pr, rows - r) * L, hipMemcpyHostToDevice, s1));
+                CK(hipMemcpy2DAsync(h2 + 72 + r * S, S, d2 + r * L, L, L, std::min(pr, rows - r), hipMemcpyDeviceToHost, s2));
+            }
+        });
     }
     rate("D2H 256 MiB, one copy (again)", [&] { CK(hipMemcpyAsync(h2, d2, N, hipMemcpyDeviceToHost, s2)); });
     rate("H2D 256 MiB in 16 MiB copies (again)", [&] {
