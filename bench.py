@@ -497,7 +497,7 @@ def run_device(args):
                     if args.shard is not None else
                     f"{n} x {L} B fragments per GPU, device-resident, "
                     f"{'CRC-32/MPEG-2 (uicrc)' if crc else 'uicsum'}, "
-                    f"{'one descriptor per fragment (piece streams)' if args.desc else 'one wavefront per fragment'}")
+                    f"{'one descriptor per fragment (piece streams)' if args.desc else 'uniform fragments (regular kernel schedule)'}")
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -893,8 +893,9 @@ def run_recv(args):
     got = shard.digest(vals, np.arange(n, dtype=np.uint64))
     want = golden_digest(args.seed, n, L, mode == dv.CRC32)
     app_ok = bool(torch.equal(app.view(n, L), nic.view(n, stride)[:, 72:72 + L]))
+    # no committed digest for this shape: the checksums are unpinned (ok None), whatever the copy says
     ok = (int(nbad.item()) == 0 and bool((copied == L).all().item()) and app_ok
-          and (want is None or got == tuple(want)))
+          and (None if want is None else got == tuple(want)))
     moved = 2.0 * n * L
     achieved = moved / kern / 1e9
     print(json.dumps({
@@ -913,13 +914,14 @@ def run_recv(args):
                      "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}"),
                      "traffic_source": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}", "source"),
                      "kernel": "crc_rows_kernel<RecvSource, 8>" if mode == dv.CRC32 else
-                               "sum_rows_kernel<RecvSource, uint32_t, false, 8>",
+                               "sum_copy_wg_kernel<RecvSource> (one 128-thread workgroup per fragment)",
                      "kernel_avg_ms": round(kern * 1e3, 4), "algorithmic_bytes_per_launch": int(moved),
                      "note": "algorithmic bytes = payload read + payload written; the 4-byte expected value and "
                              "32-byte descriptor per fragment excluded"},
         "parity": {"check": "nbad == 0, every fragment fully copied, app == slot payloads, checksum digest vs "
-                            "committed config digest", "xor": f"{got[0]:08x}", "wsum": f"{got[1]:08x}",
-                   "ok": bool(ok)},
+                            "committed config digest" + ("" if want is not None else
+                                                         " (none committed for this shape: unpinned)"),
+                   "xor": f"{got[0]:08x}", "wsum": f"{got[1]:08x}", "ok": None if ok is None else bool(ok)},
         "cpu_baseline": None}), flush=True)
 
 

@@ -134,10 +134,15 @@ std::vector<uint32_t> build_table_image() {
         abort();
     }
 
-    // the table-light fused copy's uniform shifts: 1024 bytes, then 16 * 2^j bytes (j = 0..5)
+    for (int j = 0; j < 4; ++j) {
+        for (int b = 0; b < 5; ++b) img[kImgSliceBasis + 16 * j + b] = S[j][1u << b];
+        for (int k = 0; k < 8; ++k) img[kImgSliceBasis + 16 * j + 5 + k] = S[j][32 * k];
+    }
+
+    // the table-light fused copy's shifts: 1024 bytes, 16 * 2^j bytes (j = 0..2), 128 * (7 - g) (g = 0..6)
     for (int t = 0; t < kLightTables; ++t) {
-        const uint64_t nbytes = t == 0 ? 1024u : (16ull << (t - 1));
-        nibble_tables(swapped(shift_matrix(nbytes)), &img[kImgLightNib + 128 * (size_t)t]);
+        const uint64_t nbytes = t == 0 ? 1024u : t < 4 ? (16ull << (t - 1)) : 128ull * (uint64_t)(7 - (t - 4));
+        nibble_tables(swapped(shift_matrix(nbytes)), &img[kImgLightNib + kLightTableWords * (size_t)t]);
     }
 
     // powers of two for arbitrary shifts, normal domain (squaring from one byte)

@@ -46,16 +46,23 @@ constexpr size_t kImgPow2Cols = kImgHorner16Cols + 32;
 //   [kImgZero, +16)          zeros: the row loads of crc_stream_kernel read chunks wholly outside a
 //                            fragment from here
 constexpr size_t kImgZero = kImgPow2Cols + 1024;
-//   [kImgLightNib, +7*128)   nibble tables (swapped domain, out[p*16 + v] of nibble_tables) of the
+//   [kImgLightNib, +11*144)  nibble tables (swapped domain, out[p*16 + v] of nibble_tables, 128 words
+//                            each, 144 apart so that tables 4 + g, g = 0..3, start on banks 16g) of the
 //                            table-light fused copy (crc_light_copy_kernel): table 0 shifts by 1024
 //                            bytes (a lane's next chunk of the row), table 1 + j by 16 * 2^j bytes,
-//                            j = 0..5 (the six levels of its lane tree)
+//                            j = 0..2 (the three levels of its lane tree), table 4 + g by 128 * (7 - g)
+//                            bytes, g = 0..6 (the eight-lane groups to the row end)
 constexpr size_t kImgLightNib = kImgZero + 16;
-constexpr int kLightTables = 7;
+constexpr int kLightTables = 11;
+constexpr int kLightTableWords = 144;
 //   [kImgTrash, +256)        write-only: 16 bytes per lane that the table-light copy's padding chunks
 //                            are stored to (straight-line stores, so the compiler's waits stay exact)
-constexpr size_t kImgTrash = kImgLightNib + kLightTables * 128;
-constexpr size_t kImgWords = kImgTrash + 256;
+constexpr size_t kImgTrash = kImgLightNib + kLightTables * kLightTableWords;
+//   [kImgSliceBasis, +64)    slicing-table basis of table j at 16 j: words 0..4 S_j[1 << b], 5..12 S_j[32 k],
+//                            13..15 zero (S_j is linear in its index; the table-light copy builds its
+//                            tables from these instead of selecting compile-time constants per lane)
+constexpr size_t kImgSliceBasis = kImgTrash + 256;
+constexpr size_t kImgWords = kImgSliceBasis + 64;
 constexpr int kChunkBytes = 16;                          // coalesced layout: 16-byte chunks
 constexpr int kChunkStep = kRowBytes / 4 - kChunkBytes;  // 1008 zero bytes between a lane's chunks
 

@@ -2025,35 +2025,36 @@ __global__ void __launch_bounds__(kT) plan_kernel(const lampi_frag_desc *__restr
 // Preconditions (launch_msg_bcopy): base and frag_len and msg_len multiples of 16, dst and dst_stride
 // of 4 (a dword-aligned dwordx4 store runs at the aligned rate).
 constexpr uint32_t kLtNib = 32768;
-constexpr uint32_t kLtBytes = kLtNib + kLightTables * 512;
+constexpr uint32_t kLtTab = 4 * kLightTableWords;  // bytes between the nibble tables
+constexpr uint32_t kLtBytes = kLtNib + kLightTables * kLtTab;
 
-// slicing tables in 128-byte rows (build_slices' fill with half the row stride)
-__device__ __forceinline__ void build_slices_light(char *b) {
-    const uint32_t t = threadIdx.x;
-    const uint32_t sj = (t & 7u) >> 1, r0 = t >> 3;
+// slicing tables in 128-byte rows (build_slices' fill with half the row stride), from the basis of the
+// thread's table j in the image (bs: its 16 words, kImgSliceBasis) -- the per-lane selection of
+// compile-time constants cost ~150 VALU per wave (gfx9 VALU takes no literal operands: every constant
+// needed a v_mov), about a fifth of the kernel's VALU, which bounds it (SQ counters,
+// profiles/r03/pmc_light_*)
+__device__ __forceinline__ void build_slices_light(char *b, const u32x4 bs[4]) {
+    const uint32_t t = threadIdx.x, r0 = t >> 3;
     uint32_t base = 0;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const uint32_t k = sel4(sj, kSliceBasis.lo[0][i], kSliceBasis.lo[1][i], kSliceBasis.lo[2][i],
-                                kSliceBasis.lo[3][i]);
-        base ^= ((r0 >> i) & 1u) ? k : 0u;
-    }
+    for (int i = 0; i < 5; ++i) base ^= ((r0 >> i) & 1u) ? bs[i >> 2][i & 3] : 0u;
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-        const uint32_t v = base ^ sel4(sj, kSliceBasis.hi[0][kk], kSliceBasis.hi[1][kk], kSliceBasis.hi[2][kk],
-                                       kSliceBasis.hi[3][kk]);
+        const uint32_t v = base ^ bs[(5 + kk) >> 2][(5 + kk) & 3];
         *reinterpret_cast<u32x4 *>(b + (r0 + 32 * kk) * 128 + (t & 7u) * 16) = u32x4{v, v, v, v};
     }
 }
 
-// register after the uniform shift of nibble table `tab` (swapped domain)
-template <int kTab>
-__device__ __forceinline__ uint32_t light_shift(const uint32_t *lds, uint32_t C) {
-    constexpr uint32_t base = kLtNib + 512u * kTab;
+// register after the shift of nibble table `base` (a byte address in LDS; swapped domain)
+__device__ __forceinline__ uint32_t light_shift_at(const uint32_t *lds, uint32_t base, uint32_t C) {
     uint32_t r = lds_u32(lds, base + ((C << 2) & 0x3Cu));
 #pragma unroll
     for (int p = 1; p < 8; ++p) r ^= lds_u32(lds, base + 64u * p + ((C >> (4 * p - 2)) & 0x3Cu));
     return r;
+}
+template <int kTab>
+__device__ __forceinline__ uint32_t light_shift(const uint32_t *lds, uint32_t C) {
+    return light_shift_at(lds, kLtNib + kLtTab * kTab, C);
 }
 
 // four words from a zero register through the compact slicing tables
@@ -2089,8 +2090,16 @@ __global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__re
     const uint32_t P = R * (uint32_t)kRowBytes - L;  // frame padding (a multiple of 16)
     // the uniform shift tables from the image (L2) first: vmcnt counts in order, so waiting for this
     // load leaves the row loads issued after it in flight
-    u32x4 nib = u32x4{0u, 0u, 0u, 0u};
-    if (t < kLightTables * 32) nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+    // (396 16-byte pieces: two per thread for the first 140; the clamped rest load and store the last
+    // piece again -- a load or store under a branch waits for itself before the row loads issue)
+    constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
+    static_assert(kNibPieces > 256 && kNibPieces <= 512, "two nibble-table pieces per thread at most");
+    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+    const uint32_t t2 = min(256u + t, kNibPieces - 1);
+    const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
+    u32x4 bs[4];  // the slicing basis of table (t & 7) >> 1
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
     // the row's chunks: frame offset o = 4096r + 1024q + 16l, fragment byte o - P
     // (unconditional loads -- padding chunks read the image's zero chunk -- so the four are in flight
     // together: loads under a branch each got their own vmcnt(0) wait, four round trips per row)
@@ -2103,8 +2112,9 @@ __global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__re
         d[q] = __builtin_nontemporal_load(a);
     }
     // tables: slicing from constants, then the uniform shifts, while the row loads fly
-    build_slices_light(reinterpret_cast<char *>(lds));
-    if (t < kLightTables * 32) reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
+    build_slices_light(reinterpret_cast<char *>(lds), bs);
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;  // (t >= 140: the last piece again)
     __syncthreads();
     if (!live) return;
     // the copy: every chunk of the fragment, dword-aligned 16-byte stores; padding chunks go to this
@@ -2136,20 +2146,40 @@ __global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__re
     const uint32_t c2 = light_chunk(lds, lanec2, sel, d[2]);
     const uint32_t c3 = light_chunk(lds, lanec2, sel, d[3]);
     uint32_t v = light_shift<0>(lds, light_shift<0>(lds, light_shift<0>(lds, c0) ^ c1) ^ c2) ^ c3;
-    // lane tree: after level j the last lane of every 2^(j+1)-lane block holds that block's value
+    // lane tree, three levels: after level j the last lane of every 2^(j+1)-lane block holds that block's
+    // value relative to the block's end
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<1>(lds, v), 0x111, 0xF, 0xF, false);  // row_shr:1
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<2>(lds, v), 0x112, 0xF, 0xF, false);  // row_shr:2
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<3>(lds, v), 0x114, 0xF, 0xF, false);  // row_shr:4
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<4>(lds, v), 0x118, 0xF, 0xF, false);  // row_shr:8
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<5>(lds, v), 0x142, 0xA, 0xF, false);  // row_bcast:15
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<6>(lds, v), 0x143, 0xC, 0xF, false);  // row_bcast:31
+    // then each eight-lane group g (its last lane 8g + 7) shifts by 128 * (7 - g) to the row end through
+    // its own table (tables 4..10, 576 bytes apart: groups 0..3 and 4..7 each read 64 distinct banks;
+    // group 7 needs none) -- one lookup round instead of three more tree levels -- and the eight values
+    // are XORed into lane 63: row_shr:8, row_bcast:15, row_bcast:31
+    const uint32_t grp = lane >> 3;
+    if (grp < 7u) v = light_shift_at(lds, kLtNib + kLtTab * (4u + grp), v);
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
     if (lane == 63u) out[R == 1 ? f : item] = __builtin_bswap32(v);
 }
 
 // out[f] = XOR over the rows r of fragment f of row value r shifted past the R - 1 - r rows after it
-// (normal domain; one wave per fragment, lanes take rows l, l + 64, ...)
+// (normal domain).  R <= kJoinThreadRows: one thread per fragment, Horner over its rows with the
+// constant multiply by x^(8 * 4096) (GM's 16 rows: 15 multiplies, a few VALU per fragment and row
+// across the wave -- one wave per fragment spent ~420 VALU on each); longer fragments: one wave each,
+// lanes take rows l, l + 64, ... and shift them directly.
+constexpr uint32_t kJoinThreadRows = 32;
 __global__ void __launch_bounds__(256) crc_light_join_kernel(const uint32_t *__restrict__ rows, size_t n, uint32_t R,
                                                              uint32_t *__restrict__ out) {
+    if (R <= kJoinThreadRows) {
+        const size_t f = (size_t)blockIdx.x * 256 + threadIdx.x;
+        if (f >= n) return;
+        const uint32_t *p = rows + f * R;
+        uint32_t acc = p[0];
+        for (uint32_t r = 1; r < R; ++r) acc = mul_row_shift<0>(acc) ^ p[r];
+        out[f] = acc;
+        return;
+    }
     const size_t f = (size_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (f >= n) return;
     const uint32_t lane = threadIdx.x & 63u;
@@ -3568,7 +3598,9 @@ static hipError_t launch_crc_light_copy(const uint8_t *base, size_t msg_len, siz
                        partial, dst, dst_stride, img, rows);
     e = hipGetLastError();
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(crc_light_join_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, rows, n, R, out);
+        const size_t per_wg = R <= kJoinThreadRows ? 256 : 4;  // fragments per workgroup
+        hipLaunchKernelGGL(crc_light_join_kernel, dim3((unsigned)((n + per_wg - 1) / per_wg)), dim3(256), 0, s, rows, n,
+                           R, out);
         e = hipGetLastError();
     }
     const hipError_t fe = hipFreeAsync(rows, s);

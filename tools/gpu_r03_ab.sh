@@ -1,12 +1,15 @@
 #!/usr/bin/env bash
-# Round-3 same-box A/B of the copy and descriptor paths: ab/old.so (the tree before the change) against
-# the current library, interleaved.  Usage: tools/gpu_r03_ab.sh ROUNDS
+# Round-3 same-box A/B of the copy and descriptor paths: the libraries under ab/ (earlier trees, each
+# ab/NAME.so) against the current library, interleaved.  Usage: tools/gpu_r03_ab.sh ROUNDS [NAME ...]
+# (default NAME: old)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=${1:-2}
+shift
+VARIANTS="${*:-old} new"
 for r in $(seq 1 "$R"); do
-  for v in old new; do
-    if [ $v = old ]; then L=ab/old.so; else L=lampi_amd/liblampi_csum.so; fi
+  for v in $VARIANTS; do
+    if [ $v = new ]; then L=lampi_amd/liblampi_csum.so; else L=ab/$v.so; fi
     echo "== round $r $v"
     LAMPI_CSUM_LIB=$L timeout -k 10 300 python tools/microbench/msg_bcopy_slots.py 2>&1 | grep -v amdgpu.ids || exit 1
     LAMPI_CSUM_LIB=$L timeout -k 10 300 python bench.py --bcopy --steps 10 --no-cpu-baseline 2>&1 | grep '^{' | \

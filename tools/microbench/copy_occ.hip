@@ -26,15 +26,15 @@ typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
         }                                                       \
     } while (0)
 
-template <int R, int LDS_BYTES, int X>
-__global__ void __launch_bounds__(256) copy_rows(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
-                                                 size_t rows_total, uint32_t *sink) {
+template <int R, int LDS_BYTES, int X, int W = 4>
+__global__ void __launch_bounds__(64 * W) copy_rows(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                    size_t rows_total, uint32_t *sink) {
     __shared__ uint32_t lds[LDS_BYTES / 4];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     // a constant fill of the tables' size (the staging a table-light CRC copy would do)
-    for (uint32_t i = threadIdx.x; i < LDS_BYTES / 16; i += 256)
+    for (uint32_t i = threadIdx.x; i < LDS_BYTES / 16; i += 64 * W)
         reinterpret_cast<u32x4 *>(lds)[i] = u32x4{i, i * 3u, i ^ 7u, i + 11u};
-    const size_t row = ((size_t)blockIdx.x * 4 + wave);  // one row of R KiB per wave
+    const size_t row = ((size_t)blockIdx.x * W + wave);  // one row of R KiB per wave
     if (row * R >= rows_total) return;
     const u32x4 *s = reinterpret_cast<const u32x4 *>(src + row * R * 1024) + lane;
     u32x4 v[R];
@@ -55,25 +55,25 @@ __global__ void __launch_bounds__(256) copy_rows(const uint8_t *__restrict__ src
     if (X > 0 && acc == 0x9E3779B9u) sink[0] = acc;  // keeps the lookups alive
 }
 
-template <int R, int LDS_BYTES, int X>
+template <int R, int LDS_BYTES, int X, int W = 4>
 static void run(const uint8_t *src, uint8_t *dst, size_t bytes, uint32_t *sink, const char *tag) {
     const size_t rows = bytes / 1024;  // 1 KiB units
-    const unsigned grid = (unsigned)((rows / R + 3) / 4);
-    for (int i = 0; i < 3; ++i) copy_rows<R, LDS_BYTES, X><<<grid, 256>>>(src, dst, rows, sink);
+    const unsigned grid = (unsigned)((rows / R + W - 1) / W);
+    for (int i = 0; i < 3; ++i) copy_rows<R, LDS_BYTES, X, W><<<grid, 64 * W>>>(src, dst, rows, sink);
     CK(hipDeviceSynchronize());
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     CK(hipEventRecord(a));
     const int reps = 10;
-    for (int i = 0; i < reps; ++i) copy_rows<R, LDS_BYTES, X><<<grid, 256>>>(src, dst, rows, sink);
+    for (int i = 0; i < reps; ++i) copy_rows<R, LDS_BYTES, X, W><<<grid, 64 * W>>>(src, dst, rows, sink);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, a, b));
     const double gbs = 2.0 * bytes / (ms / reps * 1e-3) / 1e9;
-    std::printf("%-40s R=%d KiB/wave LDS=%6d B (WG/CU<=%2d) X=%d lookups/16B: %7.1f GB/s = %.3f\n", tag, R, LDS_BYTES,
-                LDS_BYTES ? 163840 / LDS_BYTES : 8, X, gbs, gbs / 8000.0);
+    std::printf("%-40s W=%d R=%d KiB/wave LDS=%6d B (WG/CU<=%2d) X=%d lookups/16B: %7.1f GB/s = %.3f\n", tag, W, R,
+                LDS_BYTES, LDS_BYTES ? 163840 / LDS_BYTES : 8, X, gbs, gbs / 8000.0);
     std::fflush(stdout);
 }
 
@@ -87,22 +87,18 @@ int main() {
     CK(hipMemset(src, 0x5A, N));
     uint8_t *d8 = dst + 8;
     for (int pass = 0; pass < 2; ++pass) {
-        run<1, 16, 0>(src, d8, N, sink, "textbook (1 KiB/wave)");
-        run<1, 36864, 0>(src, d8, N, sink, "textbook + 36 KiB LDS");
-        run<1, 36864, 4>(src, d8, N, sink, "textbook + 36 KiB LDS + lookups");
-        run<2, 36864, 0>(src, d8, N, sink, "2 KiB/wave + 36 KiB LDS");
-        run<2, 36864, 4>(src, d8, N, sink, "2 KiB/wave + 36 KiB LDS + lookups");
-        run<4, 16, 0>(src, d8, N, sink, "4 KiB/wave");
-        run<4, 36864, 0>(src, d8, N, sink, "4 KiB/wave + 36 KiB LDS");
         run<4, 36864, 4>(src, d8, N, sink, "4 KiB/wave + 36 KiB LDS + lookups");
-        run<4, 40960, 4>(src, d8, N, sink, "4 KiB/wave + 40 KiB LDS + lookups");
-        run<4, 53248, 4>(src, d8, N, sink, "4 KiB/wave + 52 KiB LDS + lookups");
-        run<4, 81920, 4>(src, d8, N, sink, "4 KiB/wave + 80 KiB LDS + lookups");
-        run<4, 24576, 4>(src, d8, N, sink, "4 KiB/wave + 24 KiB LDS + lookups");
-        run<4, 36864, 8>(src, d8, N, sink, "4 KiB/wave + 36 KiB LDS + 2x lookups");
-        run<1, 16, 0>(src, dst, N, sink, "textbook, aligned dst");
-        run<4, 36864, 4>(src, dst, N, sink, "4 KiB/wave + 36 KiB + lookups, aligned");
+        run<4, 69632, 4, 8>(src, d8, N, sink, "8 waves, 68 KiB LDS (2/CU) + lookups");
+        run<4, 69632, 4, 8>(src, dst, N, sink, "8 waves, 68 KiB LDS, aligned");
+        run<4, 53248, 4, 8>(src, d8, N, sink, "8 waves, 52 KiB LDS (3/CU) + lookups");
+        run<4, 81920, 4, 8>(src, d8, N, sink, "8 waves, 80 KiB LDS (2/CU) + lookups");
+        run<8, 69632, 4, 4>(src, d8, N, sink, "8 KiB/wave, 4 waves, 68 KiB (2/CU)");
+        run<8, 36864, 4, 4>(src, d8, N, sink, "8 KiB/wave, 4 waves, 36 KiB (4/CU)");
+        run<8, 53248, 4, 4>(src, d8, N, sink, "8 KiB/wave, 4 waves, 52 KiB (3/CU)");
     }
+    // (round 3's first pass of this file also measured: textbook 77-81%, textbook + 36 KiB LDS 58%,
+    // 2 KiB/wave + 36 KiB 76% / with lookups 64%, 4 KiB/wave with no LDS 71%, 4 KiB/wave + 24-40 KiB
+    // + lookups 74.4-75.5%, 52 KiB 72%, 80 KiB 50%, 2x lookups 68%: profiles/r03/copy_occ.txt)
     std::printf("done\n");
     return 0;
 }
