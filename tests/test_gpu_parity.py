@@ -420,6 +420,39 @@ def test_host_api_matches_reference_semantics(cuda, oracle):
         assert np.array_equal(d1, d2)
 
 
+def test_host_bcopy_large_pingpong(cuda, oracle):
+    """Host bcopy calls larger than the 8 MiB bounce buffer and not a multiple of its 4 MiB halves:
+    the stage-out ping-pong (the halves alternate through events, lampi_csum.cc) for all three
+    copy-and-checksum entry points, copylen below, equal to and above the checksum length, source
+    and destination at odd offsets.  Destination bytes and checksums vs the oracle."""
+    import lampi_amd as la
+
+    rng = np.random.default_rng(91)
+    big = (9 << 20) + 13
+    data = rng.integers(0, 256, size=big + 4096, dtype=np.uint8)
+    for copylen, clen in [(big, big), (big, 5 << 20), ((5 << 20) + 3, big), ((8 << 20) + 1, (8 << 20) + 1)]:
+        for soff, doff in [(0, 0), (3, 5)]:
+            src = data[soff:soff + max(copylen, clen)]
+            d1 = np.full(copylen + doff + 64, 0xA5, np.uint8)
+            d2 = d1.copy()
+            p = int(rng.integers(0, 2**32))
+            got = la.bcopy_uicrc(src, d1[doff:], copylen, clen, p)
+            assert got == oracle.bcopy_uicrc(src, d2[doff:], copylen, clen, p), (copylen, clen, soff, doff)
+            assert np.array_equal(d1, d2), (copylen, clen, soff, doff)
+            d1[:] = 0x5A
+            d2[:] = 0x5A
+            st = la.PartialState(0x00ABCDEF & 0xFFFF, 2)
+            got = la.bcopy_uicsum(src, d1[doff:], copylen, clen, st)
+            assert (got, st.pint, st.plen) == oracle.bcopy_uicsum(src, d2[doff:], copylen, clen, 0xCDEF, 2)
+            assert np.array_equal(d1, d2), (copylen, clen, soff, doff)
+            d1[:] = 0x3C
+            d2[:] = 0x3C
+            st = la.PartialState64(0x123456, 3)
+            got = la.bcopy_csum(src, d1[doff:], copylen, clen, st)
+            assert (got, st.plong, st.plen) == oracle.bcopy_csum(src, d2[doff:], copylen, clen, 0x123456, 3)
+            assert np.array_equal(d1, d2), (copylen, clen, soff, doff)
+
+
 def test_host_api_chaining(cuda, oracle):
     """Chained pieces (the non-contiguous typemap pattern, src/path/gm/sendFrag.cc:157-217)."""
     import lampi_amd as la
