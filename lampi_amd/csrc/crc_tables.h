@@ -55,13 +55,10 @@ constexpr size_t kImgZero = kImgPow2Cols + 1024;
 constexpr size_t kImgLightNib = kImgZero + 16;
 constexpr int kLightTables = 11;
 constexpr int kLightTableWords = 144;
-//   [kImgTrash, +256)        write-only: 16 bytes per lane that the table-light copy's padding chunks
-//                            are stored to (straight-line stores, so the compiler's waits stay exact)
-constexpr size_t kImgTrash = kImgLightNib + kLightTables * kLightTableWords;
 //   [kImgSliceBasis, +64)    slicing-table basis of table j at 16 j: words 0..4 S_j[1 << b], 5..12 S_j[32 k],
 //                            13..15 zero (S_j is linear in its index; the table-light copy builds its
 //                            tables from these instead of selecting compile-time constants per lane)
-constexpr size_t kImgSliceBasis = kImgTrash + 256;
+constexpr size_t kImgSliceBasis = kImgLightNib + kLightTables * kLightTableWords;
 constexpr size_t kImgWords = kImgSliceBasis + 64;
 constexpr int kChunkBytes = 16;                          // coalesced layout: 16-byte chunks
 constexpr int kChunkStep = kRowBytes / 4 - kChunkBytes;  // 1008 zero bytes between a lane's chunks

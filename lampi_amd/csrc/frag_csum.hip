@@ -38,7 +38,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
 #include <cstdint>
 #include <cstdlib>
 
@@ -2024,6 +2027,7 @@ __global__ void __launch_bounds__(kT) plan_kernel(const lampi_frag_desc *__restr
 // crc_light_join_kernel shifts each past its fragment's later rows and XORs them.
 // Preconditions (launch_msg_bcopy): base and frag_len and msg_len multiples of 16, dst and dst_stride
 // of 4 (a dword-aligned dwordx4 store runs at the aligned rate).
+constexpr int kBufNt = 2;  // buffer instruction cache policy: nt (gfx940+ CPol::NT, the SLC bit)
 constexpr uint32_t kLtNib = 32768;
 constexpr uint32_t kLtTab = 4 * kLightTableWords;  // bytes between the nibble tables
 constexpr uint32_t kLtBytes = kLtNib + kLightTables * kLtTab;
@@ -2074,6 +2078,12 @@ __device__ __forceinline__ uint32_t light_chunk(const uint32_t *lds, uint32_t la
     return xor3(t.t0, t.t1, t.t2) ^ t.t3;
 }
 
+// raw buffer descriptor over [p, p + bytes): loads past either end read zeros, stores there are dropped
+// (gfx9 raw buffers, stride 0: the range check is offset >= num_records, in bytes)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t light_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+}
+
 __global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__restrict__ base, size_t msg_len,
                                                              uint32_t frag_len, uint32_t R, size_t nitems,
                                                              uint32_t partial, uint8_t *__restrict__ dst,
@@ -2081,12 +2091,14 @@ __global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__re
                                                              uint32_t *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    const size_t item = (size_t)blockIdx.x * 4 + (t >> 6);  // (fragment, row) of this wave
+    // (fragment, row) of this wave, wave-uniform: the fragment's source and slot become buffer
+    // descriptors in SGPRs
+    const size_t item = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6);
     const bool live = item < nitems;
     const size_t f = live ? item / R : 0;
     const uint32_t r = live ? (uint32_t)(item - f * R) : 0u;
     const size_t foff = f * frag_len;
-    const uint32_t L = (uint32_t)min((size_t)frag_len, msg_len - foff);
+    const uint32_t L = live ? (uint32_t)min((size_t)frag_len, msg_len - foff) : 0u;
     const uint32_t P = R * (uint32_t)kRowBytes - L;  // frame padding (a multiple of 16)
     // the uniform shift tables from the image (L2) first: vmcnt counts in order, so waiting for this
     // load leaves the row loads issued after it in flight
@@ -2100,30 +2112,29 @@ __global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__re
     u32x4 bs[4];  // the slicing basis of table (t & 7) >> 1
 #pragma unroll
     for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
-    // the row's chunks: frame offset o = 4096r + 1024q + 16l, fragment byte o - P
-    // (unconditional loads -- padding chunks read the image's zero chunk -- so the four are in flight
-    // together: loads under a branch each got their own vmcnt(0) wait, four round trips per row)
+    // the row's chunks: frame offset 4096r + 1024q + 16l, fragment byte o[q] = that - P, through a
+    // buffer descriptor of the fragment's L bytes: the frame padding (o < 0, a huge unsigned offset)
+    // reads as zeros and its stores are dropped by the range check, with no select per chunk.  The
+    // 1024q goes into the VGPR offset (not the instruction's): the check then never sees a wrapped sum.
+    const __amdgpu_buffer_rsrc_t src_rs = light_rsrc(base + foff, L);
+    const __amdgpu_buffer_rsrc_t dst_rs = light_rsrc(dst + f * dst_stride, L);
+    uint32_t o[4];
     u32x4 d[4];
-    int64_t b[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        b[q] = (int64_t)r * kRowBytes + 1024 * q + 16 * lane - P;
-        const u32x4 *a = (live && b[q] >= 0) ? (const u32x4 *)(base + foff + b[q]) : (const u32x4 *)(img + kImgZero);
-        d[q] = __builtin_nontemporal_load(a);
+        o[q] = r * (uint32_t)kRowBytes + 1024u * q + 16u * lane - P;
+        asm volatile("" : "+v"(o[q]));  // (kept whole: the compiler would fold 1024q into the immediate)
+        d[q] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, o[q], 0, kBufNt);
     }
-    // tables: slicing from constants, then the uniform shifts, while the row loads fly
+    // tables: slicing from the basis, then the uniform shifts, while the row loads fly
     build_slices_light(reinterpret_cast<char *>(lds), bs);
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;  // (t >= 140: the last piece again)
     __syncthreads();
     if (!live) return;
-    // the copy: every chunk of the fragment, dword-aligned 16-byte stores; padding chunks go to this
-    // lane's trash slot (stores under a branch made the compiler wait for them to complete before the
-    // CRC: it merges the paths' counters)
-    uint8_t *drow = dst + f * dst_stride;
-    uint8_t *trash = (uint8_t *)(uintptr_t)(img + kImgTrash) + 16 * lane;
+    // the copy: every chunk of the fragment, 16-byte stores (dword-aligned slots run at the aligned rate)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) st16((gwu32x4_a4 *)(b[q] >= 0 ? drow + b[q] : trash), d[q]);
+    for (int q = 0; q < 4; ++q) __builtin_amdgcn_raw_buffer_store_b128(d[q], dst_rs, o[q], 0, kBufNt);
     // the fragment's register enters as data in its first four bytes (frame offset P)
     if ((P >> 12) == r && ((P >> 4) & 63u) == lane) {
         const uint32_t qi = (P >> 10) & 3u, inj = __builtin_bswap32(partial);
@@ -3351,6 +3362,49 @@ static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size
 // a batch of few large fragments to a few workgroups (1 GiB of 4 MiB descriptors: 34% of the roofline).
 // Not the default: the plan launch adds ~10 us to every call (1 x 4 KiB: 7.8 -> 20 us, 4,096 x 4 KiB:
 // 10.6 -> 23 us; profiles/r03/bigdesc_ab.txt).  Larger batches keep the count split.
+// Device scratch for a launch sequence on stream s (the byte-balanced plan, the light copy's group
+// values): one grow-only buffer per (device, stream), reused in stream order -- a call's kernels
+// finish with it before the next call's on the same stream start.  Per-call hipMallocAsync /
+// hipFreeAsync put a ~6 us gap before the next kernel on the stream (profiles/r03/light_join_gap.txt).
+// Growing frees the old buffer with hipFree, which waits for the device.  Kept until process exit.
+// While s is being captured into a graph the graph gets its own allocation (hipMallocAsync; *pooled
+// set: release it with scratch_done), so no replay depends on a buffer a later call may replace.
+static hipError_t stream_scratch(hipStream_t s, size_t bytes, void **out, bool *pooled) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipError_t ce = hipStreamIsCapturing(s, &cs);
+    if (ce != hipSuccess) return ce;
+    *pooled = cs != hipStreamCaptureStatusNone;
+    if (*pooled) return hipMallocAsync(out, bytes, s);
+    static std::mutex mu;
+    static auto *bufs = new std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>>();  // never freed
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    auto &slot = (*bufs)[{dev, s}];
+    if (slot.second < bytes) {
+        if (slot.first) {
+            e = hipFree(slot.first);
+            slot = {nullptr, 0};
+            if (e != hipSuccess) return e;
+        }
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 1u << 20);
+        e = hipMalloc(&slot.first, want);
+        if (e != hipSuccess) {
+            slot = {nullptr, 0};
+            return e;
+        }
+        slot.second = want;
+    }
+    *out = slot.first;
+    return hipSuccess;
+}
+
+static hipError_t scratch_done(hipStream_t s, void *p, bool pooled, hipError_t e) {
+    const hipError_t f = pooled ? hipFreeAsync(p, s) : hipSuccess;
+    return e != hipSuccess ? e : f;
+}
+
 template <bool kSum, int kWv, int kCap>
 static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
                                  hipStream_t s) {
@@ -3361,7 +3415,8 @@ static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *o
     const size_t gmax = 2 + (cap + kPlanF - 1) / kPlanF + gb;                             // workgroups at most
     const size_t seg_bytes = (cap * sizeof(SegDesc) + 255) & ~(size_t)255;
     uint8_t *scratch = nullptr;
-    hipError_t e = hipMallocAsync((void **)&scratch, seg_bytes + (gmax + 2) * sizeof(uint32_t), s);
+    bool pooled = false;
+    hipError_t e = stream_scratch(s, seg_bytes + (gmax + 2) * sizeof(uint32_t), (void **)&scratch, &pooled);
     if (e != hipSuccess) return e;
     SegDesc *segs = (SegDesc *)scratch;
     uint32_t *plan = (uint32_t *)(scratch + seg_bytes);
@@ -3380,8 +3435,7 @@ static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *o
                            dim3(64 * kWv), 0, s, SegSource{segs, d}, cap, 0u, img, out, (const uint32_t *)plan);
         e = hipGetLastError();
     }
-    const hipError_t f = hipFreeAsync(scratch, s);
-    return e != hipSuccess ? e : f;
+    return scratch_done(s, scratch, pooled, e);
 }
 
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
@@ -3592,7 +3646,8 @@ static hipError_t launch_crc_light_copy(const uint8_t *base, size_t msg_len, siz
         return hipGetLastError();
     }
     uint32_t *rows = nullptr;
-    hipError_t e = hipMallocAsync((void **)&rows, items * sizeof(uint32_t), s);
+    bool pooled = false;
+    hipError_t e = stream_scratch(s, items * sizeof(uint32_t), (void **)&rows, &pooled);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(crc_light_copy_kernel, grid, dim3(256), 0, s, base, msg_len, (uint32_t)frag_len, R, items,
                        partial, dst, dst_stride, img, rows);
@@ -3603,8 +3658,7 @@ static hipError_t launch_crc_light_copy(const uint8_t *base, size_t msg_len, siz
                            R, out);
         e = hipGetLastError();
     }
-    const hipError_t fe = hipFreeAsync(rows, s);
-    return e != hipSuccess ? e : fe;
+    return scratch_done(s, rows, pooled, e);
 }
 
 hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, uint8_t *dst,

@@ -89,6 +89,36 @@ def test_message_with_short_last_fragment(cuda, oracle, mode):
         assert np.array_equal(got, want), (msg_len, L)
 
 
+@pytest.mark.parametrize("msg_len,L", [
+    (65456 * 300, 65456),                  # GM payloads: 16-row frames, 80 bytes of front padding
+    (65456 * 300 + 1280, 65456),           # a 1,280-byte last fragment: 15 whole padding rows
+    (((1 << 20) + 48) * 5 + 4096 * 3 + 16, (1 << 20) + 48),  # 257-row frames: 17 groups, joined
+    ((12288 + 80) * 700 + 16, 12288 + 80),  # 4-row frames, P = 4016: the register in row 0, lane 62
+    ((16384 + 1008) * 333, 16384 + 1008),  # P = 3088: lane 48, chunk 1
+    ((12288 * 2 + 16) * 97 + 12288 * 2, 12288 * 2 + 16),  # last fragment exactly 6 rows
+    ((40000 // 16 * 16) * 777 + 4096, 40000 // 16 * 16),
+])
+def test_message_large_ragged_fragments(cuda, oracle, msg_len, L):
+    """lampi_msg_csum CRC of messages of large fragments that are not whole 4 KiB rows (GM payloads,
+    257-row fragments, registers landing in every lane and chunk position of a 4 KiB frame, last
+    fragments of a few rows or exactly whole rows), every fragment vs the oracle, two registers."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(msg_len)
+    buf = torch.empty(msg_len, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=msg_len % 1000)
+    host = buf.cpu().numpy()
+    nf = (msg_len + L - 1) // L
+    offs = np.arange(nf, dtype=np.uint64) * L
+    lens = np.minimum(L, msg_len - offs.astype(np.int64)).astype(np.uint32)
+    for part in (0xFFFFFFFF, int(rng.integers(0, 2**32))):
+        got = dv.as_u32(dv.msg_csum(buf, L, partial=part))
+        want = oracle.desc_batch(host, offs, lens, np.full(nf, part, np.uint32), 0)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (msg_len, L, hex(part), bad[:8].tolist(), nf)
+
+
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 def test_descriptor_batch_edges_and_alignment(cuda, oracle, mode):
     import torch

@@ -20,16 +20,16 @@ for L, n, stride, off in ((4096, 1 << 20, 4096 + 80, 72),   # 4 KiB payloads in 
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     for mode, name in ((dv.CRC32, "crc"), (dv.SUM32, "sum")):
         run = lambda: dv.msg_bcopy(msg, L, dst[off:], stride, mode=mode, out=out)  # noqa: E731
-        for _ in range(5):
+        for _ in range(40):  # past the clocks' transient (a dip over the first ~20 calls: profiles/r03/light_transient.txt)
             run()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(20):
+        for _ in range(30):
             run()
         e1.record()
         torch.cuda.synchronize()
-        s = e0.elapsed_time(e1) / 20 / 1e3
+        s = e0.elapsed_time(e1) / 30 / 1e3
         ok = torch.equal(dst[off:off + n * stride].view(n, stride)[:, :L], msg.view(n, L))
         same = torch.equal(out, dv.msg_csum(msg, L, mode=mode))  # the read-only kernels, an independent path
         print(f"L={L} slot={stride} {name}: {2 * n * L / s / 1e9:.1f} GB/s = {2 * n * L / s / 8e12:.3f} of 8 TB/s, "
