@@ -614,7 +614,7 @@ def run_mixed(args):
     pw_same = bool(torch.equal(pw_out, out))
     achieved = total / kern_avg_s / 1e9
     meta = total + 20 * lens.size  # + the 16-byte descriptor read and the 4-byte result write
-    traffic = read_traffic("crc_configC") if mode == dv.CRC32 else None
+    traffic = read_traffic("crc_configC" if mode == dv.CRC32 else "sum_configC")
     print(json.dumps({
         "metric": METRIC, "value": round(total / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1,
         "steps": args.steps, "warmup": nw, "ms_per_step": round(wall / args.steps * 1e3, 4),
@@ -802,9 +802,21 @@ def run_bcopy(args):
     _, kern_dst1 = timed(lambda: dv.frag_bcopy_batch(descs_d1, n=n - 1, mode=mode, out=out))
     copyd1_ok = bool(torch.equal(src[:(n - 1) * L], dst[1:1 + (n - 1) * L]))
     _, kern_copy = timed(lambda: dst.copy_(src))
+    # GM's own send shape (gm/sendFrag.cc:147-155): 65,456-byte payloads of a 1 GiB message into
+    # 64 KiB ring slots right after the 72-byte header, checksums vs the read-only kernels
+    gm_L, gm_stride, gm_n = 65456, 65536, min(16384, (n * L) // 65536 - 1)
+    gm_msg, gm_dst = src[:gm_n * gm_L], dst[:72 + gm_n * gm_stride]
+    gm_out = torch.empty(gm_n, dtype=torch.int32, device="cuda")
+    gm_run = lambda: dv.msg_bcopy(gm_msg, gm_L, gm_dst[72:], gm_stride, mode=mode, out=gm_out)  # noqa: E731
+    for _ in range(40):  # past the clocks' transient (profiles/r03/light_transient.txt)
+        gm_run()
+    _, kern_gm = timed(gm_run)
+    gm_copy_ok = bool(torch.equal(gm_dst[72:72 + gm_n * gm_stride].view(gm_n, gm_stride)[:, :gm_L],
+                                  gm_msg.view(gm_n, gm_L)))
+    gm_same = bool(torch.equal(gm_out, dv.msg_csum(gm_msg, gm_L, mode=mode)))
     moved = 2.0 * n * L
     achieved = moved / kern / 1e9
-    kname = ("crc_regular_kernel<copy>" if mode == dv.CRC32 else "sum_copy_row_kernel")
+    kname = ("crc_light_copy_kernel" if mode == dv.CRC32 else "sum_copy_row_kernel")
     print(json.dumps({
         "metric": "device-resident fused copy+checksum GiB/s of payload (bcopy); % of HBM roofline",
         "value": round(n * L / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
@@ -836,11 +848,18 @@ def run_bcopy(args):
                                   "kernel_avg_ms": round(kern_dst1 * 1e3, 4),
                                   "frac": round(2.0 * (n - 1) * L / kern_dst1 / 1e9 / HBM_PEAK_GBS, 4),
                                   "copy_ok": copyd1_ok},
+        "gm_send_slots": {"what": f"{gm_n} x {gm_L} B payloads of one message into {gm_stride}-byte slots after "
+                                  f"a 72-byte header (lampi_msg_bcopy, dst % 16 = 8); copy and checksums "
+                                  f"(vs lampi_msg_csum) checked", "kernel": kname if mode == dv.CRC32 else
+                          "sum_copy_row_kernel", "kernel_avg_ms": round(kern_gm * 1e3, 4),
+                          "frac": round(2.0 * gm_n * gm_L / kern_gm / 1e9 / HBM_PEAK_GBS, 4),
+                          "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_bcopy_gm_slots"),
+                          "copy_ok": gm_copy_ok, "checksums_ok": gm_same},
         "copy_reference": {"what": "torch dst.copy_(src), same bytes, no checksum",
                            "kernel_avg_ms": round(kern_copy * 1e3, 4),
                            "achieved_GBs": round(moved / kern_copy / 1e9, 1)},
         "parity": {**parity, "descriptor_batch": parity_desc,
-                   "ok_all": bool(parity["ok"] and parity_desc["ok"])},
+                   "ok_all": bool(parity["ok"] and parity_desc["ok"] and gm_copy_ok and gm_same)},
         "cpu_baseline": None}))
 
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env bash
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
-#   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchD | bcopy | prof | profC | pmc | pmcC | e2e | microbench
+#   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchCsum | benchD | bcopy |
+#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | e2e | microbench
 # Any failure (a test failure, fault, abort, segfault, timeout or kill) ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -42,6 +43,14 @@ for step in "$@"; do
             -- python3 bench.py --config C --steps 20 ;;
     pmcC) run pmcC_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcC_fetch -o run \
             -- python3 bench.py --config C --steps 5 --warmup 1 ;;
+    pmcCsum) run pmcCsum_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcCsum_fetch -o run \
+            -- python3 bench.py --config C --mode sum --steps 5 --warmup 1 ;;
+    pmcDshard) run pmcD0_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcD0_fetch -o run \
+            -- python3 bench.py --config D --shard 0 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmcbcopy) run pmcbcopy_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcbcopy_fetch \
+            -o run -- python3 bench.py --bcopy --steps 5 --warmup 3 &&
+         run pmcbcopy_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcbcopy_write \
+            -o run -- python3 bench.py --bcopy --steps 5 --warmup 3 ;;
     pmcsq) for cfg in B C D; do
              extra="--no-cpu-baseline"; [ $cfg = C ] && extra="--config C"; [ $cfg = D ] && extra="--desc --no-cpu-baseline"
              run pmc_sq$cfg 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
