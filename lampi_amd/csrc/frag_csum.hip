@@ -2200,6 +2200,183 @@ __global__ void __launch_bounds__(256) crc_light_join_kernel(const uint32_t *__r
     if (lane == 0) out[f] = acc;
 }
 
+// ---- CRC fused copy of descriptor batches, table-light (lampi_frag_bcopy_batch, CopyToApp) --------
+// crc_light_copy_kernel's tables and row step for descriptors: one wave per fragment (fragment f of
+// the batch = wave blockIdx.x * 4 + w), its rows walked in order with the next row's loads in flight,
+// the Horner over the 1024-byte step carried from row to row (a lane's last chunk of a row and its
+// first of the next are 1024 bytes apart too), one lane tree per fragment.  Any source and
+// destination alignment, copylen <> csumlen: L = max(copylen, csumlen) bytes are checksummed in a
+// right-aligned frame of R = ceil(L / 4096) rows (front padding P = 4096R - L, any byte count) read
+// through a buffer descriptor of the L source bytes (padding reads zero); the chunk that straddles the
+// fragment's start (P % 16 != 0) is rebuilt from the fragment's first 16 bytes.  The first copylen
+// bytes go out through a buffer descriptor of the destination: whole chunks as 16-byte stores, the
+// (at most two) chunks cut by the copy's start or end byte by byte -- their vector store is aimed out
+// of range.  The register enters as data at frame offset P (any byte offset: two words).  Fragments
+// under 16 bytes: one lane, byte steps on S_3.  Fragments up to 2^32 - 17 bytes.
+__device__ __forceinline__ uint32_t pick4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, int i) {
+    return i == 0 ? a : i == 1 ? b : i == 2 ? c : i == 3 ? d : 0u;
+}
+// 16 bytes (little endian) moved s bytes toward higher addresses, 0 < s < 16, zeros shifted in
+__device__ __forceinline__ u32x4 shl_bytes16(const u32x4 &v, uint32_t s) {
+    const int k = (int)(s >> 2);
+    const uint32_t m = (s & 3u) * 8u;
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t lo = pick4(v.x, v.y, v.z, v.w, i - k);
+        const uint32_t hi = pick4(v.x, v.y, v.z, v.w, i - k - 1);
+        o[i] = m ? (lo << m) | (hi >> (32u - m)) : lo;
+    }
+    return u32x4{o[0], o[1], o[2], o[3]};
+}
+
+template <class Src>
+__global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src, size_t n,
+                                                                  const uint32_t *__restrict__ img,
+                                                                  uint32_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const size_t f = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6);
+    const bool live = f < n;
+    constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
+    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+    const uint32_t t2 = min(256u + t, kNibPieces - 1);
+    const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
+    u32x4 bs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
+    FragInfo fi{nullptr, 0u, 0u, nullptr, 0u};
+    if (live) fi = src.get(f);
+    const uint32_t L = fi.len, R = (uint32_t)(((uint64_t)L + kRowBytes - 1) / kRowBytes);
+    const uint32_t P = R * (uint32_t)kRowBytes - L;  // (L < 2^32 - 16: no overflow)
+    const __amdgpu_buffer_rsrc_t srs = light_rsrc((const void *)fi.addr, L);
+    const __amdgpu_buffer_rsrc_t drs = light_rsrc(fi.dst, fi.copylen);
+    // (ok false: offsets aimed out of range, no memory traffic -- a prefetch past the last row)
+    auto load_row = [&](uint32_t r, bool ok, u32x4 (&d)[4], uint32_t (&o)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            o[q] = ok ? r * (uint32_t)kRowBytes + 1024u * q + 16u * lane - P : 0xFFFFFFF0u;
+            asm volatile("" : "+v"(o[q]));  // whole offsets: padding offsets wrap to huge values, out of range
+            d[q] = __builtin_amdgcn_raw_buffer_load_b128(srs, o[q], 0, kBufNt);
+        }
+    };
+    u32x4 d[4];
+    uint32_t o[4];
+    load_row(0, true, d, o);  // (unconditional: an empty or dead wave's descriptor reads nothing but zeros)
+    // the fragment's first 16 bytes, for the chunk its start cuts (a load here rather than under that
+    // branch: the compiler's merged waits after a branch with a load drained every row's prefetch)
+    const u32x4 head = __builtin_amdgcn_raw_buffer_load_b128(srs, 0u, 0, 0);
+    build_slices_light(reinterpret_cast<char *>(lds), bs);
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
+    __syncthreads();
+    if (!live) return;
+    if (L < 16) {  // short fragments (and empty ones: the register itself)
+        if (lane == 0) {
+            uint32_t C = __builtin_bswap32(fi.partial);
+            for (uint32_t i = 0; i < L; ++i) C = (C >> 8) ^ lds[((C ^ fi.addr[i]) & 255u) * 32u + 24u];
+            emit(src, out, f, __builtin_bswap32(C), fi);
+        }
+        if (lane < fi.copylen) fi.dst[lane] = fi.addr[lane];
+        return;
+    }
+    const uint32_t c8 = (lane & 7u) * 8u;
+    const uint32_t lanec2 = c8 | ((c8 + 64u) << 8) | ((c8 + 128u) << 16) | ((c8 + 192u) << 24);
+    const uint32_t oct = (lane >> 3) & 3u;
+    uint32_t sel[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t j = (uint32_t)q ^ oct;
+        sel[q] = j | ((4u + j) << 8) | 0x0C0C0000u;
+    }
+    const uint32_t grp = lane >> 3;
+    const uint32_t gbase = kLtNib + kLtTab * (4u + min(grp, 6u));
+    const uint32_t kP = P >> 4, sP = P & 15u;   // the chunk holding the fragment's first byte, and where
+    const uint64_t cend = (uint64_t)fi.copylen + P;  // the copy's end in the frame
+    uint32_t acc = 0;
+    auto step = [&](uint32_t r, u32x4 (&dc)[4], const uint32_t (&oc)[4], u32x4 (&dn)[4], uint32_t (&on)[4]) {
+        load_row(r + 1, r + 1 < R, dn, on);
+        if (r == 0 && sP != 0) {  // the chunk cut by the fragment's start: [zeros | first 16 - sP bytes]
+            const u32x4 v = shl_bytes16(head, sP);
+            const bool mine = lane == (kP & 63u);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((uint32_t)q == (kP >> 6) && mine) dc[q] = v;
+        }
+        // the copy: whole chunks of [P, cend) as 16-byte stores (the others aimed out of range)
+        const uint32_t rbase = r * (uint32_t)kRowBytes + 16u * lane;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t x = rbase + 1024u * q;
+            const bool whole = x >= P && x + 16u <= cend;
+            __builtin_amdgcn_raw_buffer_store_b128(dc[q], drs, whole ? oc[q] : 0xFFFFFFF0u, 0, kBufNt);
+        }
+        // chunks cut by the copy's start or end (at most two per fragment): byte stores
+        const uint64_t row0 = (uint64_t)r * kRowBytes;
+        if ((r == 0 && sP != 0) || (cend > row0 && cend < row0 + kRowBytes && (cend & 15u) != 0)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t x = rbase + 1024u * q;
+                if (!(x >= P && x + 16u <= cend) && x < cend && x + 16u > P) {
+                    const uint32_t w[4] = {dc[q].x, dc[q].y, dc[q].z, dc[q].w};
+                    for (uint32_t j = 0; j < 16; ++j)
+                        if (x + j >= P && x + j < cend) fi.dst[x + j - P] = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
+                }
+            }
+        }
+        // the register enters as data at frame offset P: bytes P..P+3 (two words when P % 4 != 0,
+        // chunk kP and, for sP > 12, the next -- in row 1 when kP is row 0's last chunk)
+        if (r == 0 || (r == 1 && kP == 255u)) {
+            const uint32_t inj = __builtin_bswap32(fi.partial);
+            const uint32_t w = sP >> 2, m = (sP & 3u) * 8u;
+            const uint32_t lo = inj << m, hi = m ? inj >> (32u - m) : 0u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t k = 256u * r + lane + 64u * q;
+                const uint32_t a = k == kP ? lo : 0u, b = k == kP ? hi : 0u;
+                const uint32_t c = (k == kP + 1u && w == 3u) ? hi : 0u;
+                dc[q].x ^= (w == 0 ? a : 0u) ^ c;
+                dc[q].y ^= (w == 1 ? a : 0u) ^ (w == 0 ? b : 0u);
+                dc[q].z ^= (w == 2 ? a : 0u) ^ (w == 1 ? b : 0u);
+                dc[q].w ^= (w == 3 ? a : 0u) ^ (w == 2 ? b : 0u);
+            }
+        }
+        const uint32_t c0 = light_chunk(lds, lanec2, sel, dc[0]);
+        const uint32_t c1 = light_chunk(lds, lanec2, sel, dc[1]);
+        const uint32_t c2 = light_chunk(lds, lanec2, sel, dc[2]);
+        const uint32_t c3 = light_chunk(lds, lanec2, sel, dc[3]);
+        const uint32_t v0 = r == 0 ? c0 : light_shift<0>(lds, acc) ^ c0;
+        acc = light_shift<0>(lds, light_shift<0>(lds, light_shift<0>(lds, v0) ^ c1) ^ c2) ^ c3;
+        if (r + 1 == R) {
+            uint32_t v = acc;
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<1>(lds, v), 0x111, 0xF, 0xF, false);
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<2>(lds, v), 0x112, 0xF, 0xF, false);
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<3>(lds, v), 0x114, 0xF, 0xF, false);
+            const uint32_t wv = light_shift_at(lds, gbase, v);
+            v = grp < 7u ? wv : v;
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+            if (lane == 63u) emit(src, out, f, __builtin_bswap32(v), fi);
+        }
+    };
+    u32x4 d2[4];
+    uint32_t o2[4];
+    for (uint32_t r = 0; r < R; r += 2) {
+        step(r, d, o, d2, o2);
+        if (r + 1 >= R) break;
+        step(r + 1, d2, o2, d, o);
+    }
+}
+
+template <class Src>
+static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
+                                             hipStream_t s) {
+    hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n, img,
+                       out);
+    return hipGetLastError();
+}
+
 // ---- CRC fast path: regular batches -------------------------------------------------------
 // Fragment f = base + f*frag_len, frag_len = R*4096, base 16-byte aligned (P = 0, no masks).
 // A wave checksums kChains of its fragments at once (independent lookup chains interleaved:
@@ -3546,10 +3723,8 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
                              hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC)
-    if (mode == LAMPI_CSUM_CRC32)
-        launch_crc_rows_copy(CopySource{d}, n, 1, img, out, s);
-    else
-        launch_sum_copy(CopySource{d}, n, out, s);
+    if (mode == LAMPI_CSUM_CRC32) return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s);
+    launch_sum_copy(CopySource{d}, n, out, s);
     return hipGetLastError();
 }
 
@@ -3562,10 +3737,8 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
     if (!img) return hipErrorInvalidValue;
     const bool crc = mode == LAMPI_CSUM_CRC32;
     const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
-    if (crc)
-        launch_crc_rows_copy(src, n, 1, img, csum, s);
-    else
-        launch_sum_copy(src, n, csum, s);
+    if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s);
+    launch_sum_copy(src, n, csum, s);
     return hipGetLastError();
 }
 
