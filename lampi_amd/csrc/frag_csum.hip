@@ -3844,9 +3844,9 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
         if (light_copy_ok(base, msg_len, frag_len, dst, dst_stride, n))
             return launch_crc_light_copy(base, msg_len, frag_len, partial, dst, dst_stride, n, out, img, s);
         if (regular) return launch_crc_regular_copy(base, n, frag_len, partial, dst, dst_stride, out, img, s);
-        launch_crc_rows_copy(MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n,
-                             (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes), img, out, s, frag_len);
-        return hipGetLastError();
+        // ragged or unaligned messages: one wave per fragment on the same tables (any alignment)
+        return launch_crc_light_frag_copy(MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n, img,
+                                          out, s);
     }
     const uint64_t rpf = (frag_len + kRowBytes - 1) / kRowBytes;
     if (msg_len != 0 && frag_len >= kRowBytes && frag_len % 16 == 0 && msg_len % 16 == 0 &&
