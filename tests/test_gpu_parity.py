@@ -119,6 +119,33 @@ def test_message_large_ragged_fragments(cuda, oracle, msg_len, L):
         assert bad.size == 0, (msg_len, L, hex(part), bad[:8].tolist(), nf)
 
 
+@pytest.mark.parametrize("msg_len,L", [
+    (65456 * 4102 + 1280, 65456),           # GM payloads, >= 256 MiB: the framed regular kernel; the
+                                            # short last fragment's register lands in row 15
+    (39984 * 6800 + 4096 * 3 + 16, 39984),  # 10-row frames, P = 976; last fragment 3 rows + 16 bytes
+    ((131072 - 16) * 2100, 131072 - 16),    # 32-row frames, P = 16
+])
+def test_message_frames_regular_kernel(cuda, oracle, msg_len, L):
+    """lampi_msg_csum CRC of >= 256 MiB messages of 32-128 KiB fragments that are not whole rows
+    (crc_regular_kernel<kFrame>: 4 KiB frames read through buffer descriptors, the register injected
+    at the frame padding's end), every fragment vs the oracle, two registers."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(L)
+    buf = torch.empty(msg_len, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=L % 977)
+    host = buf.cpu().numpy()
+    nf = (msg_len + L - 1) // L
+    offs = np.arange(nf, dtype=np.uint64) * L
+    lens = np.minimum(L, msg_len - offs.astype(np.int64)).astype(np.uint32)
+    for part in (0xFFFFFFFF, int(rng.integers(0, 2**32))):
+        got = dv.as_u32(dv.msg_csum(buf, L, partial=part))
+        want = oracle.desc_batch(host, offs, lens, np.full(nf, part, np.uint32), 0)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (msg_len, L, hex(part), bad[:8].tolist(), nf)
+
+
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 def test_descriptor_batch_edges_and_alignment(cuda, oracle, mode):
     import torch
