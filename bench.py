@@ -932,7 +932,7 @@ def run_recv(args):
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}"),
                      "traffic_source": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}", "source"),
-                     "kernel": "crc_rows_kernel<RecvSource, 8>" if mode == dv.CRC32 else
+                     "kernel": "crc_light_frag_copy_kernel<RecvSource>" if mode == dv.CRC32 else
                                "sum_copy_wg_kernel<RecvSource> (one 128-thread workgroup per fragment)",
                      "kernel_avg_ms": round(kern * 1e3, 4), "algorithmic_bytes_per_launch": int(moved),
                      "note": "algorithmic bytes = payload read + payload written; the 4-byte expected value and "

@@ -2,7 +2,7 @@
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
 #   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchCsum | benchD | bcopy |
-#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | e2e | microbench
+#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | e2e | recv | microbench
 # Any failure (a test failure, fault, abort, segfault, timeout or kill) ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -58,6 +58,8 @@ for step in "$@"; do
                  -d gpurun_out/pmc_sq$cfg -o run -- python3 bench.py --steps 3 --warmup 1 $extra
            done ;;
     e2e) run e2e 600 python bench.py --e2e ;;
+    recv) run recv 600 python bench.py --recv --steps 10 &&
+          run recvsum 600 python bench.py --recv --mode sum --steps 10 ;;
     bcopy) run bcopy 600 python bench.py --bcopy --steps 10 &&
            run bcopysum 600 python bench.py --bcopy --mode sum --steps 10 ;;
     tests_bcopy) run pytest_bcopy 600 python -m pytest tests/test_gpu_bcopy.py -m gpu -x -q ;;
