@@ -327,6 +327,49 @@ def test_descriptor_batch_byte_balanced(cuda, oracle, case, mode):
     assert np.array_equal(dv.as_u32(dv.frag_csum_batch(descs, mode=mode)), got)
 
 
+def test_descriptor_batch_packed_rows(cuda, oracle):
+    """CRC descriptor batches on the regular kernel's shape (crc_list_kernel) pack fragments of whole
+    64-byte pieces up to 1 KiB four to a row and up to 2 KiB two to a row (slot-local combine columns),
+    when one buffer descriptor of < 2^31 bytes spans the workgroup's packable fragments; the rest are
+    right-aligned frames.  The slot edges (64, 1024, 1088, 2048, 2112 bytes), odd lengths beside them,
+    empty fragments, random registers; and a second buffer more than 2 GiB away, so workgroups that
+    mix both fall back to frames.  Every fragment against the oracle."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(64)
+    MiB = 1 << 20
+    a = torch.empty(8 * MiB, dtype=torch.uint8, device=cuda)
+    gap = torch.empty(3 << 30, dtype=torch.uint8, device=cuda)  # pushes b past a's 2 GiB window
+    b = torch.empty(8 * MiB, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(a, seed=61)
+    dv.fill_stream(b, seed=62)
+    far = abs(b.data_ptr() - a.data_ptr()) >= (1 << 31)
+
+    def batch(n):
+        edges = np.array([64, 128, 960, 1024, 1088, 1984, 2048, 2112, 4096, 0, 1000, 2047, 63, 5000], np.uint64)
+        lens = np.where(rng.integers(0, 4, size=n) == 0, rng.choice(edges, size=n),
+                        64 * rng.integers(1, 40, size=n)).astype(np.uint64)
+        offs = rng.integers(0, 8 * MiB - 6000, size=n).astype(np.uint64)
+        offs[rng.integers(0, 3, size=n) > 0] &= ~np.uint64(63)
+        parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+        return lens, offs, parts
+
+    la, oa, pa = batch(24000)
+    lb, ob, pb = batch(24000)
+    # interleave the two buffers in runs, so some workgroups hold fragments of both
+    order = np.argsort(np.concatenate([np.arange(24000) // 5 * 2, np.arange(24000) // 7 * 2 + 1]), kind="stable")
+    descs = torch.cat([dv.make_descs(a, oa, la, pa), dv.make_descs(b, ob, lb, pb)])[torch.from_numpy(order).to(cuda)]
+    want = np.concatenate([oracle.desc_batch(a.cpu().numpy(), oa, la, pa.astype(np.uint32), 0),
+                           oracle.desc_batch(b.cpu().numpy(), ob, lb, pb.astype(np.uint32), 0)])[order]
+    for by_bytes in (False, True):
+        got = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.CRC32, by_bytes=by_bytes))
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (by_bytes, far, bad[:10])
+    del gap
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("n", [30000, 300000])
 def test_descriptor_batch_small_fragments(cuda, oracle, n):
     """Fragments of 16..1024 bytes (multiples of 16, 16-byte aligned) mixed with unaligned,
