@@ -2743,411 +2743,6 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped re-loads before exit
 }
 
-// ---- CRC of descriptor batches on the regular kernel's shape (crc_list_kernel) ---------------------
-// The piece streams (crc_stream_kernel) need 768-thread workgroups of one chain per wave, and that shape
-// reads at ~78% with no CRC work at all (profiles/r02_stream_shape.txt); crc_regular_kernel's shape
-// (256 threads, two chains per wave, the 64 KiB tables, a three-deep asm ring) reads at ~82%.  This
-// kernel runs any descriptor batch on that shape:
-//   * a workgroup owns fpg consecutive descriptors; fragment f is right-aligned in a frame of
-//     R_f = ceil(L_f / 4096) rows (the frame padding P_f = 4096 R_f - L_f reads as zeros through a raw
-//     buffer descriptor of the fragment's L_f bytes, as in kFrame), and the frames of the workgroup's
-//     non-empty fragments, in order, form one stream of T rows;
-//   * chain c (two per wave, eight in all) takes rows [cT/8, (c+1)T/8): every chain within a row of the
-//     others whatever the sizes.  Each chain walks its rows like the regular kernel -- lane l owns bytes
-//     [64l, 64l + 64) of a row, Horner over 4032 bytes between rows, lane_combine + wave_xor at the end
-//     of a fragment -- but its two chains step independently through fragments of any length;
-//   * a fragment cut by a chain boundary is checksummed in parts: each part from a zero register, ending
-//     with the combine at its last row; a part ending before the fragment's last row is shifted past
-//     the rows after it (shift_rows, constant products; at most one per chain, after the loop).  Parts
-//     and whole values are XORed into the workgroup's result slots in LDS (ds_xor) and stored once,
-//     coalesced, at the end (a 4-byte global store inside the load ring sits in the vmcnt order);
-//   * the register enters as lane (P/64)'s starting value when P % 64 == 0 (config C: all fragments),
-//     otherwise as data at frame byte P (two words; the byte past a row end goes to the next row); the
-//     chunk cut by the fragment's start (L % 16 != 0) is rebuilt in the set-up from the fragment's first
-//     L % 16 bytes (byte loads: nothing outside the fragment is read);
-//   * fragments of fewer than 4 bytes get the register's remainder s << 8L XORed into the result.
-// Frame padding costs lookups, not bytes (the padded chunks are never fetched): config C has 1.53M frame
-// rows for 1.05M rows of data; the regular kernel has the LDS and VALU headroom for it (~37% / 34% busy
-// on config B).
-constexpr uint32_t kListMaxF = 128;  // descriptors per workgroup at most
-struct ListEntry {
-    uint64_t addr;
-    uint32_t len, partial;
-    uint32_t R, row0;  // frame rows; the frame's first row in the workgroup's stream
-    uint32_t P, pad;   // frame padding 4096R - len (mod 2^32)
-};
-static_assert(sizeof(ListEntry) == 32, "LDS layout");
-// per chain and ring slot (wave-uniform), packed (SGPR pressure): the row in flight
-struct ListTask {
-    uint32_t jP, rf, partial;  // entry | frame padding (packed rows: slot count) << 8; flags | frame row << 8
-    __device__ uint32_t j() const { return jP & 0xFFu; }
-    __device__ uint32_t P() const { return jP >> 8; }
-    __device__ uint32_t f() const { return rf & 0xFFu; }
-    __device__ uint32_t r() const { return rf >> 8; }
-};
-static_assert(kListMaxF <= 256, "entry index in 8 bits");
-constexpr uint32_t kLtNull = 1u, kLtFirst = 2u, kLtEnd = 4u, kLtOpen = 8u, kLtFix = 16u, kLtShort = 32u,
-                   kLtQuarter = 64u, kLtHalf = 128u;
-constexpr uint32_t kLtBigRows = 1u << 20;  // frames this long wrap the padding's offsets into the fragment
-
-// the workgroup's shared state after the set-up
-struct ListShared {
-    uint32_t lds[kLdsBytes / 4];  // tables
-    ListEntry ents[kListMaxF];    // packed fragments (quarter, half rows) first, then the frames
-    u32x4 heads[kListMaxF];       // the chunk each entry's start cuts (L % 16 != 0)
-    uint32_t sres[kListMaxF];     // values, XORed together from the parts
-    uint32_t cstart[8];           // the entry holding chain c's first row (frames)
-    uint64_t sh[5];
-    uint64_t pmin, pmax;          // the window of the packable fragments
-};
-
-// the row stream: nQ quarter rows (four fragments of <= 1 KiB each), nH half rows (two of <= 2 KiB),
-// then the frames; entries [0, nq) quarters, [nq, nq + nh) halves, the rest frames
-struct ListRows {
-    uint32_t T, nq, nh, nQ, F0;  // rows; quarter and half fragments; quarter rows; the first frame row
-    uint64_t pbase;              // packed rows: one buffer descriptor over [pbase, pbase + pspan)
-    uint32_t pspan;
-};
-
-// The rows of the wave's two chains.  kFix: some frame of the workgroup needs the first-row fix-ups
-// (P % 64 != 0: the register as data, a chunk cut by the start; frames of >= 2^20 rows); without them
-// the register is lane P/64's starting value and the loop carries no fix-up code.
-template <bool kFix>
-__device__ __forceinline__ void list_body(ListShared &S, const ListRows &G, const CombineBasis &cb) {
-    constexpr int K = 2, D = 3;
-    constexpr int kL = 4 * K;  // loads per step
-    const uint32_t lane = threadIdx.x & 63u, wave = uniform(threadIdx.x >> 6);
-    const uint32_t *lds = S.lds;
-    const uint32_t T = G.T, F0 = G.F0;
-    struct Walk {
-        uint32_t rho, left;   // next row of the stream; rows left in the chain, this one included
-        uint32_t j, r;        // frames: entry j, frame row r
-        uint32_t R, P, len, partial;
-        uint64_t addr;
-        bool first;
-    };
-    auto load_entry = [&](Walk &w) {
-        const ListEntry &e = S.ents[w.j];
-        w.addr = uniform64(e.addr);
-        w.len = uniform(e.len);
-        w.partial = uniform(e.partial);
-        w.R = uniform(e.R);
-        w.P = uniform(e.P);
-    };
-    Walk wk[K];
-    uint32_t nsteps = 0;
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        const uint32_t cc = 2u * wave + (uint32_t)c;
-        const uint32_t s = (cc * T) >> 3, e = ((cc + 1u) * T) >> 3;
-        wk[c].rho = s;
-        wk[c].left = e - s;
-        wk[c].first = true;
-        wk[c].j = 0u;
-        wk[c].r = 0u;
-        wk[c].addr = 0ull;
-        wk[c].len = wk[c].R = wk[c].P = wk[c].partial = 0u;
-        if (e > s && s >= F0) {
-            wk[c].j = uniform(S.cstart[cc]);
-            load_entry(wk[c]);
-            wk[c].r = s - uniform(S.ents[wk[c].j].row0);
-        }
-        nsteps = max(nsteps, e - s);
-    }
-    // the task of the chain's next row, its buffer descriptor, the lane's row offset and starting
-    // register; then step the chain
-    auto next_task = [&](Walk &w, ListTask &tk, u32x4 &rs, uint32_t &ol, uint32_t &ci) {
-        if (w.left == 0u) {  // done: a null row (nothing in range, no memory traffic)
-            tk = ListTask{0u, kLtNull, 0u};
-            rs = u32x4{0u, 0u, 0u, 0x00020000u};
-            ol = 0u;
-            ci = 0u;
-            return;
-        }
-        if (w.rho < F0) {  // a packed row: slot g of the lanes holds entry j0 + g, right-aligned
-            const bool quarter = w.rho < G.nQ;
-            const uint32_t j0 = quarter ? 4u * w.rho : G.nq + 2u * (w.rho - G.nQ);
-            const uint32_t cnt = quarter ? min(4u, G.nq - j0) : min(2u, G.nq + G.nh - j0);
-            tk = ListTask{j0 | (cnt << 8), kLtFirst | kLtEnd | (quarter ? kLtQuarter : kLtHalf), 0u};
-            rs = u32x4{(uint32_t)G.pbase, (uint32_t)(G.pbase >> 32) & 0xFFFFu, G.pspan, 0x00020000u};
-            const uint32_t g = quarter ? lane >> 4 : lane >> 5, sl = quarter ? lane & 15u : lane & 31u;
-            const uint32_t slot = quarter ? 1024u : 2048u;
-            ol = 0x80000000u;  // out of range (the window is < 2^31 bytes)
-            ci = 0u;
-            if (g < cnt) {
-                const ListEntry &e = S.ents[j0 + g];
-                const uint32_t Pp = slot - e.len;  // (a multiple of 64)
-                if (sl * (uint32_t)kLaneBytes >= Pp) ol = (uint32_t)(e.addr - G.pbase) - Pp + sl * (uint32_t)kLaneBytes;
-                ci = sl == (Pp >> 6) ? __builtin_bswap32(e.partial) : 0u;
-            }
-            ++w.rho;
-            w.first = false;
-            if (--w.left != 0u && w.rho == F0) {  // on into the frames
-                w.j = G.nq + G.nh;
-                w.r = 0u;
-                load_entry(w);
-            }
-            return;
-        }
-        const bool fend = w.r + 1u == w.R, cend = w.left == 1u;
-        uint32_t f = ((w.first || w.r == 0u) ? kLtFirst : 0u) | ((fend || cend) ? kLtEnd : 0u) |
-                     ((cend && !fend) ? kLtOpen : 0u);
-        const bool fixit = kFix && w.r == 0u && ((w.P & 63u) != 0u || w.R >= kLtBigRows);
-        if (fixit) f |= kLtFix;
-        if (w.len < 4u) f |= kLtShort;
-        tk = ListTask{w.j | (w.P << 8), f | (w.r << 8), w.partial};
-        rs = u32x4{(uint32_t)w.addr, (uint32_t)(w.addr >> 32) & 0xFFFFu, w.len, 0x00020000u};
-        // (frame offsets before P wrap to huge: out of range)
-        ol = uniform(w.r * (uint32_t)kRowBytes - w.P) + lane * (uint32_t)kLaneBytes;
-        // P % 64 == 0: the register is lane P/64's starting value (otherwise fix_first puts it in the data)
-        ci = (w.r == 0u && !fixit && lane == (w.P >> 6)) ? __builtin_bswap32(w.partial) : 0u;
-        ++w.rho;
-        w.first = false;
-        if (--w.left != 0u) {
-            if (w.r + 1u < w.R) {
-                ++w.r;
-            } else {
-                ++w.j;
-                w.r = 0u;
-                load_entry(w);
-            }
-        }
-    };
-    auto issue_step = [&](ListTask (&tk)[K], RowsK<K> &b, uint32_t (&ci)[K]) {
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            u32x4 rs;
-            uint32_t ol;
-            next_task(wk[c], tk[c], rs, ol, ci[c]);
-            rs = u32x4{uniform(rs.x), uniform(rs.y), uniform(rs.z), uniform(rs.w)};  // (SGPR operand)
-            uint32_t o[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = ol + 16u * (uint32_t)q;
-            issue_row_buf(rs, o, b.x[c]);
-        }
-    };
-    ListTask tk[D][K] = {};
-    RowsK<K> ring[D];
-    uint32_t cinit[D][K] = {};
-#pragma unroll
-    for (int q = 0; q < D; ++q) issue_step(tk[q], ring[q], cinit[q]);
-    // the rest of the tables while the first rows fly
-    char *tb = reinterpret_cast<char *>(S.lds);
-    build_horner<false>(tb);
-    build_combine(tb, cb);
-    lds_barrier();
-
-    const CrcLane kl = make_lane((int)lane);
-    uint32_t C[K];
-    uint32_t ov[K], oh[K], oj[K];  // a chain's open part (its last row ends inside a fragment)
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-        C[c] = 0u;
-        oh[c] = 0u;
-        ov[c] = 0u;
-        oj[c] = 0u;
-    }
-    // combine columns of packed rows: lane l of a 16- (32-) lane slot shifts by 64 * (15 - l) (31 - l),
-    // the column of lane 48 + l (32 + l)
-    const uint32_t colq = comb_col(48u + (lane & 15u)), colh = comb_col(32u + (lane & 31u));
-    // the frame's first row: chunks before the fragment zeroed (only frames of >= 2^20 rows read any),
-    // the chunk its start cuts rebuilt, the register XORed in at byte P (two words when P % 4 != 0)
-    auto fix_first = [&](Row &b, const ListTask &x) {
-        const uint32_t P = x.P(), kP = P >> 4;
-        const u32x4 hv = (P & 15u) ? S.heads[x.j()] : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t k = 4u * lane + (uint32_t)q;
-            b.q[q] = k < kP ? u32x4{0u, 0u, 0u, 0u} : ((k == kP && (P & 15u)) ? hv : b.q[q]);
-        }
-        const uint32_t v = __builtin_bswap32(x.partial);
-        const uint32_t l0 = P >> 6, a = (P >> 2) & 15u, sb = P & 3u;
-        const uint32_t m0 = v << (8u * sb), m1 = sb ? (v >> (32u - 8u * sb)) : 0u;
-        const bool own = lane == l0;
-        const uint32_t mA = own ? m0 : 0u, mB = own ? m1 : 0u;
-        const uint32_t mC = (lane == l0 + 1u && a == 15u) ? m1 : 0u;
-#pragma unroll
-        for (uint32_t w = 0; w < 16; ++w) {
-            const uint32_t m = ((w == a) ? mA : ((w == a + 1u) ? mB : 0u)) ^ (w == 0u ? mC : 0u);
-            u32x4 &y = b.q[w >> 2];
-            if ((w & 3u) == 0u) y.x ^= m;
-            if ((w & 3u) == 1u) y.y ^= m;
-            if ((w & 3u) == 2u) y.z ^= m;
-            if ((w & 3u) == 3u) y.w ^= m;
-        }
-    };
-    auto process = [&](RowsK<K> &b, const ListTask (&x)[K], const uint32_t (&ci)[K]) {
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            const uint32_t f = x[c].f();
-            if (f & kLtFirst) {
-                C[c] = ci[c];
-                if (kFix && (f & kLtFix)) fix_first(b.x[c], x[c]);
-            } else if (f & kLtNull) {
-                C[c] = 0u;
-            } else {
-                C[c] = horner_shift(lds, C[c]);
-            }
-            // a register XORed in at frame bytes 4093..4095 spills its last bytes into row 1, lane 0
-            if (kFix && !(f & (kLtNull | kLtQuarter | kLtHalf)) && x[c].r() == 1u && x[c].P() >= 4093u && lane == 0u)
-                b.x[c].q[0].x ^= __builtin_bswap32(x[c].partial) >> (32u - 8u * (x[c].P() & 3u));
-        }
-        crc_pieces<K>(lds, kl, C, b);
-        if ((x[0].rf | x[1].rf) & kLtEnd) {
-            uint32_t v[K];
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                const uint32_t f = x[c].f();
-                const uint32_t col = (f & kLtQuarter) ? colq : ((f & kLtHalf) ? colh : kl.comb_base);
-                v[c] = row16_xor(combine_at(lds, col, C[c]));
-            }
-#pragma unroll
-            for (int c = 0; c < K; ++c) {
-                const uint32_t f = x[c].f();
-                if (!(f & kLtEnd)) continue;
-                const uint32_t s0 = __builtin_amdgcn_readlane(v[c], 0), s1 = __builtin_amdgcn_readlane(v[c], 16);
-                const uint32_t s2 = __builtin_amdgcn_readlane(v[c], 32), s3 = __builtin_amdgcn_readlane(v[c], 48);
-                if (f & (kLtQuarter | kLtHalf)) {  // slot values, one lane per slot
-                    const uint32_t cnt = x[c].P();
-                    const uint32_t y = (f & kLtQuarter) ? (lane == 0u ? s0 : lane == 1u ? s1 : lane == 2u ? s2 : s3)
-                                                        : (lane == 0u ? (s0 ^ s1) : (s2 ^ s3));
-                    if (lane < cnt) atomicXor(&S.sres[x[c].j() + lane], __builtin_bswap32(y));
-                    continue;
-                }
-                uint32_t r = __builtin_bswap32((s0 ^ s1) ^ (s2 ^ s3));
-                if (f & kLtOpen) {  // shifted after the loop (the chain's last row)
-                    ov[c] = r;
-                    oh[c] = uniform(S.ents[x[c].j()].R) - 1u - x[c].r();  // rows of the fragment after it
-                    oj[c] = x[c].j();
-                } else {
-                    if (f & kLtShort) r ^= x[c].partial << (8u * (kRowBytes - x[c].P()));
-                    if (lane == 0u) atomicXor(&S.sres[x[c].j()], r);
-                }
-            }
-        }
-    };
-    uint32_t done = 0;
-#define LAMPI_LIST_STEP(S_)                                 \
-    wait_rows<(D - 1) * kL, K>(ring[S_]);                   \
-    if (done == nsteps) break;                              \
-    process(ring[S_], tk[S_], cinit[S_]);                   \
-    ++done;                                                 \
-    issue_step(tk[S_], ring[S_], cinit[S_]);
-    for (;;) {
-        LAMPI_LIST_STEP(0)
-        LAMPI_LIST_STEP(1)
-        LAMPI_LIST_STEP(2)
-    }
-#undef LAMPI_LIST_STEP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the null rows in flight
-#pragma unroll
-    for (int c = 0; c < K; ++c)
-        if (oh[c] != 0u && lane == 0u) atomicXor(&S.sres[oj[c]], shift_rows(ov[c], oh[c]));
-}
-
-// Src: DescSource (fpg descriptors per workgroup) or SegSource (the byte plan's segments: workgroup i
-// takes segments [plan[1+i], plan[2+i]), each checksummed as a fragment of its own and stored or, for a
-// split fragment, shifted past the fragment's later rows and XORed into out -- as crc_stream_kernel does).
-template <class Src>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
-crc_list_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out,
-                const uint32_t *__restrict__ plan) {
-    __shared__ __attribute__((aligned(16))) ListShared S;
-    const uint32_t t = threadIdx.x;
-    size_t base = (size_t)blockIdx.x * fpg;
-    uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
-    if constexpr (IsSeg<Src>::value) {
-        const uint32_t g = plan[0];
-        if (blockIdx.x >= g) return;  // the launch is sized for the largest plan
-        base = plan[1 + blockIdx.x];
-        nwg = plan[2 + blockIdx.x] - (uint32_t)base;
-    }
-    // ---- set-up: descriptors, the row stream, chain starts -------------------------------------
-    if (t == 0) {
-        S.pmin = ~0ull;
-        S.pmax = 0ull;
-    }
-    FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
-    if (t < nwg) mine = src.get(base + t);
-    CombineBasis cb = issue_combine_basis<false>(img);
-    build_slices(reinterpret_cast<char *>(S.lds));  // (constants: overlaps the descriptor loads)
-    const uint32_t L = mine.len;
-    const uint64_t addr = (uint64_t)(uintptr_t)mine.addr;
-    const bool ne = t < nwg && L != 0u;
-    // packable: whole 64-byte pieces, at most 2 KiB -- a quarter (<= 1 KiB) or half row of its own
-    const bool cand = ne && L <= 2048u && (L & 63u) == 0u;
-    if (cand) {
-        atomicMin((unsigned long long *)&S.pmin, (unsigned long long)addr);
-        atomicMax((unsigned long long *)&S.pmax, (unsigned long long)(addr + L));
-    }
-    __syncthreads();
-    const uint64_t pmin = uniform64(S.pmin), pmax = uniform64(S.pmax);
-    const bool pack = pmax > pmin && pmax - pmin < (1ull << 31);  // one buffer descriptor spans them all
-    const bool isq = pack && cand && L <= 1024u, ish = pack && cand && L > 1024u, isf = ne && !isq && !ish;
-    const uint32_t R = isf ? (uint32_t)(((uint64_t)L + kRowBytes - 1) >> 12) : 0u;
-    const uint32_t P = R * (uint32_t)kRowBytes - L;
-    const uint32_t sP = P & 15u;
-    const bool cut = isf && sP != 0u;
-    u32x4 head{0u, 0u, 0u, 0u};  // the chunk cut by the fragment's start: [sP zeros | the first 16 - sP bytes]
-    if (__builtin_amdgcn_ballot_w64(cut)) {  // (byte loads: nothing outside the fragment is read)
-        uint8_t hb[16];
-#pragma unroll
-        for (uint32_t p = 0; p < 16; ++p) hb[p] = (cut && p >= sP) ? mine.addr[p - sP] : (uint8_t)0;
-        uint32_t w[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            w[k] = (uint32_t)hb[4 * k] | ((uint32_t)hb[4 * k + 1] << 8) | ((uint32_t)hb[4 * k + 2] << 16) |
-                   ((uint32_t)hb[4 * k + 3] << 24);
-        head = u32x4{w[0], w[1], w[2], w[3]};
-    }
-    // one scan: frame rows (bits 0..31), quarter / half / frame counts (bits 32.., 40.., 48..)
-    const uint64_t sv = (uint64_t)R | (isq ? 1ull << 32 : 0ull) | (ish ? 1ull << 40 : 0ull) | (isf ? 1ull << 48 : 0ull);
-    uint64_t tot = 0;
-    const uint64_t ex = block_excl_scan64<256>(sv, S.sh, &tot);
-    ListRows G;
-    G.nq = uniform((uint32_t)(tot >> 32) & 0xFFu);
-    G.nh = uniform((uint32_t)(tot >> 40) & 0xFFu);
-    G.nQ = (G.nq + 3u) >> 2;
-    G.F0 = G.nQ + ((G.nh + 1u) >> 1);
-    G.T = G.F0 + uniform((uint32_t)tot);  // (an LDS sum: the compiler cannot see it is uniform)
-    G.pbase = pmin;
-    G.pspan = (uint32_t)(pmax - pmin);
-    const uint32_t li = isq ? (uint32_t)(ex >> 32) & 0xFFu
-                            : ish ? G.nq + ((uint32_t)(ex >> 40) & 0xFFu) : G.nq + G.nh + ((uint32_t)(ex >> 48) & 0xFFu);
-    const uint32_t row0 = G.F0 + (uint32_t)ex;
-    if (ne) {
-        S.ents[li] = ListEntry{addr, L, mine.partial, R, row0, P, 0u};
-        if (sP != 0u) S.heads[li] = head;
-        S.sres[li] = 0u;
-        if (isf) {
-#pragma unroll
-            for (uint32_t c = 0; c < 8; ++c) {
-                const uint32_t s = (c * G.T) >> 3;
-                if (s >= row0 && s < row0 + R) S.cstart[c] = li;
-            }
-        }
-    }
-    const bool fix = __syncthreads_or(isf && ((P & 63u) != 0u || R >= kLtBigRows)) != 0;
-    // the combine basis arrived long ago (the barriers drained every load): the wait names its registers
-    asm volatile("s_waitcnt vmcnt(0) ; lampi-wait %0 %1" : "+v"(cb.a), "+v"(cb.b) : : "memory");
-    if (fix)
-        list_body<true>(S, G, cb);
-    else
-        list_body<false>(S, G, cb);
-    __syncthreads();
-    if (t >= nwg) return;
-    const uint32_t v = ne ? S.sres[li] : mine.partial;  // uicrc(p, 0, s) == s
-    if constexpr (IsSeg<Src>::value) {  // a segment: its fragment's value, or its part of a split one
-        const SegDesc x = src.s[base + t];
-        if (!(x.rows & kSegSplit))
-            out[x.frag] = v;
-        else
-            atomicXor(out + x.frag, shift_rows(v, x.rows & ~kSegSplit));  // past the fragment's later rows
-    } else {
-        out[base + t] = v;
-    }
-}
-
 // ---- SUM -------------------------------------------------------------------------------
 // SUM fused copies (bcopy_uicsum descriptors, the receive step, ragged message fragments and the
 // rows of longer ones) in the textbook copy shape: one short-lived 128-thread workgroup per
@@ -4071,47 +3666,11 @@ static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *o
                            segs, plan, out);
     e = hipGetLastError();
     if (e == hipSuccess) {
-        if (kSum)
-            hipLaunchKernelGGL((crc_stream_kernel<SegSource, kStreamD, kStreamK, kSum, kWv, kCap>), dim3((unsigned)gmax),
-                               dim3(64 * kWv), 0, s, SegSource{segs, d}, cap, 0u, img, out, (const uint32_t *)plan);
-        else  // CRC segments on the regular kernel's shape
-            hipLaunchKernelGGL(crc_list_kernel<SegSource>, dim3((unsigned)gmax), dim3(kBlock), 0, s, SegSource{segs, d},
-                               cap, 0u, img, out, (const uint32_t *)plan);
+        hipLaunchKernelGGL((crc_stream_kernel<SegSource, kStreamD, kStreamK, kSum, kWv, kCap>), dim3((unsigned)gmax),
+                           dim3(64 * kWv), 0, s, SegSource{segs, d}, cap, 0u, img, out, (const uint32_t *)plan);
         e = hipGetLastError();
     }
     return scratch_done(s, scratch, pooled, e);
-}
-
-// crc_list_kernel: descriptors per workgroup (at most kListMaxF), halved while the grid would have fewer
-// than 2048 workgroups
-static uint32_t g_list_fpg = 64;
-static uint32_t list_frags_per_wg(size_t n) {
-    uint32_t f = g_list_fpg;
-    while (f > 1 && n / f < 2048) f >>= 1;
-    return f;
-}
-
-static hipError_t launch_crc_list(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
-                                  hipStream_t s) {
-    const uint32_t fpg = list_frags_per_wg(n);
-    hipLaunchKernelGGL(crc_list_kernel<DescSource>, frags_grid(n, fpg), dim3(kBlock), 0, s, DescSource{d}, n, fpg, img,
-                       out, nullptr);
-    return hipGetLastError();
-}
-
-static int desc_kernel_choice() {  // A/B switch (LAMPI_DESC_KERNEL=stream|list[:fpg]), read once
-    static int v = [] {
-        const char *e = getenv("LAMPI_DESC_KERNEL");
-        if (!e) return 0;
-        if (e[0] == 'l') {
-            const char *c = e;
-            while (*c && *c != ':') ++c;
-            if (*c == ':') g_list_fpg = (uint32_t)std::min(128, std::max(1, atoi(c + 1)));
-            return 1;
-        }
-        return 0;
-    }();
-    return v;
 }
 
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
@@ -4119,7 +3678,6 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
-    if (desc_kernel_choice() == 1) return launch_crc_list(d, n, out, img, s);
     const uint32_t fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
                        frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);

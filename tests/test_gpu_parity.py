@@ -327,13 +327,11 @@ def test_descriptor_batch_byte_balanced(cuda, oracle, case, mode):
     assert np.array_equal(dv.as_u32(dv.frag_csum_batch(descs, mode=mode)), got)
 
 
-def test_descriptor_batch_packed_rows(cuda, oracle):
-    """CRC descriptor batches on the regular kernel's shape (crc_list_kernel) pack fragments of whole
-    64-byte pieces up to 1 KiB four to a row and up to 2 KiB two to a row (slot-local combine columns),
-    when one buffer descriptor of < 2^31 bytes spans the workgroup's packable fragments; the rest are
-    right-aligned frames.  The slot edges (64, 1024, 1088, 2048, 2112 bytes), odd lengths beside them,
-    empty fragments, random registers; and a second buffer more than 2 GiB away, so workgroups that
-    mix both fall back to frames.  Every fragment against the oracle."""
+def test_descriptor_batch_two_buffers(cuda, oracle):
+    """Fragments from two buffers more than 2 GiB apart, interleaved in runs so workgroups hold both,
+    with lengths at the 64-byte-piece edges that round 3's packed-row experiment (crc_list_kernel,
+    profiles/r03/list_kernel_ab.txt) keyed on (64, 1024, 1088, 2048, 2112 bytes), odd lengths beside them,
+    empty fragments and random registers.  Every fragment against the oracle."""
     import torch
 
     dv = _dv()
