@@ -17,6 +17,13 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lampi_csum.h")
 CRC32 = 0  # enum lampi_csum_mode (include/lampi_csum.h)
 SUM32 = 1
 BY_BYTES = 0x100  # LAMPI_CSUM_BY_BYTES: byte-balanced descriptor batches (OR'ed into the mode)
+
+
+def rows_hint_bits(rows: int) -> int:
+    """LAMPI_CSUM_ROWS_HINT(rows): OR'ed into the mode of the CRC copy batches (0: no hint)."""
+    if not 0 <= int(rows) <= 0xFFF:
+        raise ValueError("rows_hint is 0..4095")
+    return (int(rows) & 0xFFF) << 16
 CRC_POLYNOMIAL = 0x04C11DB7  # ref src/util/MemFunctions.h:36
 CRC_INITIAL_REGISTER = 0xFFFFFFFF  # ref src/util/MemFunctions.h:37
 

@@ -51,6 +51,10 @@
 
 namespace lampi {
 
+// per-stream device scratch (defined with the launchers)
+static hipError_t stream_scratch(hipStream_t s, size_t bytes, void **out, bool *pooled);
+static hipError_t scratch_done(hipStream_t s, void *p, bool pooled, hipError_t e);
+
 namespace {
 
 constexpr uint32_t kLdsHorner = 65536;
@@ -2243,14 +2247,22 @@ __device__ __forceinline__ u32x4 shl_bytes16(const u32x4 &v, uint32_t s) {
     return u32x4{o[0], o[1], o[2], o[3]};
 }
 
+// Row groups (W > 1, LAMPI_CSUM_ROWS_HINT): fragment f runs as W waves, wave g taking rows
+// [g*k, min((g+1)*k, R)) with k = ceil(R / W) -- GM's 16-row payloads one row per wave, the shape of the
+// message copy -- and leaves the groups' values (each from a zero register, the first with the fragment's
+// register in it, the lane tree at the group's last row) in groups[f*W + g]; crc_light_group_join_kernel
+// shifts each past the fragment's later rows, XORs them and emits.  A fragment of one group emits here.
 template <class Src>
 __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src, size_t n,
                                                                   const uint32_t *__restrict__ img,
-                                                                  uint32_t *__restrict__ out) {
+                                                                  uint32_t *__restrict__ out, uint32_t W,
+                                                                  uint32_t *__restrict__ groups) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    const size_t f = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6);
-    const bool live = f < n;
+    const size_t item = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6);
+    const size_t f = item / W;
+    const uint32_t g = (uint32_t)(item - f * W);
+    bool live = f < n;
     constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
     const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
     const uint32_t t2 = min(256u + t, kNibPieces - 1);
@@ -2262,6 +2274,11 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     if (live) fi = src.get(f);
     const uint32_t L = fi.len, R = (uint32_t)(((uint64_t)L + kRowBytes - 1) / kRowBytes);
     const uint32_t P = R * (uint32_t)kRowBytes - L;  // (L < 2^32 - 16: no overflow)
+    // this wave's rows [r0, r1) (all of them for W == 1); a group past the last row has nothing to do
+    const uint32_t k = W > 1 ? (R + W - 1) / W : R;
+    const uint32_t r0 = W > 1 ? min(g * k, R) : 0u, r1 = W > 1 ? min(r0 + k, R) : R;
+    const bool whole = r0 == 0u && r1 == R;  // the fragment's only group: emits its checksum
+    if (W > 1 && g > 0u && r0 >= r1) live = false;
     const __amdgpu_buffer_rsrc_t srs = light_rsrc((const void *)fi.addr, L);
     const __amdgpu_buffer_rsrc_t drs = light_rsrc(fi.dst, fi.copylen);
     // (ok false: offsets aimed out of range, no memory traffic -- a prefetch past the last row)
@@ -2275,7 +2292,7 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     };
     u32x4 d[4];
     uint32_t o[4];
-    load_row(0, true, d, o);  // (unconditional: an empty or dead wave's descriptor reads nothing but zeros)
+    load_row(r0, live, d, o);  // (an empty or dead wave's descriptor reads nothing but zeros)
     // the fragment's first 16 bytes, for the chunk its start cuts (a load here rather than under that
     // branch: the compiler's merged waits after a branch with a load drained every row's prefetch)
     const u32x4 head = __builtin_amdgcn_raw_buffer_load_b128(srs, 0u, 0, 0);
@@ -2308,7 +2325,7 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     const uint64_t cend = (uint64_t)fi.copylen + P;  // the copy's end in the frame
     uint32_t acc = 0;
     auto step = [&](uint32_t r, u32x4 (&dc)[4], const uint32_t (&oc)[4], u32x4 (&dn)[4], uint32_t (&on)[4]) {
-        load_row(r + 1, r + 1 < R, dn, on);
+        load_row(r + 1, r + 1 < r1, dn, on);
         if (r == 0 && sP != 0) {  // the chunk cut by the fragment's start: [zeros | first 16 - sP bytes]
             const u32x4 v = shl_bytes16(head, sP);
             const bool mine = lane == (kP & 63u);
@@ -2358,9 +2375,9 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
         const uint32_t c1 = light_chunk(lds, lanec2, sel, dc[1]);
         const uint32_t c2 = light_chunk(lds, lanec2, sel, dc[2]);
         const uint32_t c3 = light_chunk(lds, lanec2, sel, dc[3]);
-        const uint32_t v0 = r == 0 ? c0 : light_shift<0>(lds, acc) ^ c0;
+        const uint32_t v0 = r == r0 ? c0 : light_shift<0>(lds, acc) ^ c0;
         acc = light_shift<0>(lds, light_shift<0>(lds, light_shift<0>(lds, v0) ^ c1) ^ c2) ^ c3;
-        if (r + 1 == R) {
+        if (r + 1 == r1) {
             uint32_t v = acc;
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<1>(lds, v), 0x111, 0xF, 0xF, false);
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<2>(lds, v), 0x112, 0xF, 0xF, false);
@@ -2370,24 +2387,66 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-            if (lane == 63u) emit(src, out, f, __builtin_bswap32(v), fi);
+            if (lane == 63u) {
+                if (whole)
+                    emit(src, out, f, __builtin_bswap32(v), fi);
+                else
+                    groups[f * W + g] = __builtin_bswap32(v);
+            }
         }
     };
     u32x4 d2[4];
     uint32_t o2[4];
-    for (uint32_t r = 0; r < R; r += 2) {
+    for (uint32_t r = r0; r < r1; r += 2) {
         step(r, d, o, d2, o2);
-        if (r + 1 >= R) break;
+        if (r + 1 >= r1) break;
         step(r + 1, d2, o2, d, o);
     }
 }
 
+// The fragments of more than one row group: value = XOR over the groups of group g shifted past the rows
+// after it (normal domain, constant products), then emit (receive sources: the verdict).  One thread per
+// fragment.
+template <class Src>
+__global__ void __launch_bounds__(256) crc_light_group_join_kernel(const Src src, size_t n, uint32_t W,
+                                                                   const uint32_t *__restrict__ groups,
+                                                                   uint32_t *__restrict__ out) {
+    const size_t f = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (f >= n) return;
+    const FragInfo fi = src.get(f);
+    const uint32_t R = (uint32_t)(((uint64_t)fi.len + kRowBytes - 1) / kRowBytes);
+    if (fi.len < 16u || R <= 1u) return;  // (emitted by its only wave)
+    const uint32_t k = (R + W - 1) / W, ng = (R + k - 1) / k;
+    if (ng <= 1u) return;
+    const uint32_t *p = groups + f * W;
+    uint32_t acc = p[0];
+    for (uint32_t g = 1; g < ng; ++g) acc = shift_rows(acc, min(k, R - g * k)) ^ p[g];
+    emit(src, out, f, acc, fi);
+}
+
+// W: row groups per fragment (1: one wave walks all the fragment's rows)
 template <class Src>
 static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
-                                             hipStream_t s) {
-    hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n, img,
-                       out);
-    return hipGetLastError();
+                                             hipStream_t s, uint32_t W = 1) {
+    while (W > 1 && (size_t)n * W > ((size_t)1 << 26)) W >>= 1;  // (grid: items * 64 threads < 2^32)
+    if (W <= 1) {
+        hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
+                           img, out, 1u, (uint32_t *)nullptr);
+        return hipGetLastError();
+    }
+    uint32_t *groups = nullptr;
+    bool pooled = false;
+    hipError_t e = stream_scratch(s, n * W * sizeof(uint32_t), (void **)&groups, &pooled);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n * W + 3) / 4)), dim3(256), 0, s, src, n, img,
+                       out, W, groups);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(crc_light_group_join_kernel<Src>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, n,
+                           W, groups, out);
+        e = hipGetLastError();
+    }
+    return scratch_done(s, groups, pooled, e);
 }
 
 // ---- CRC fast path: regular batches -------------------------------------------------------
@@ -3802,24 +3861,24 @@ static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t
 }
 
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
-                             hipStream_t s) {
+                             hipStream_t s, uint32_t rows_hint) {
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC)
-    if (mode == LAMPI_CSUM_CRC32) return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s);
+    if (mode == LAMPI_CSUM_CRC32) return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
     launch_sum_copy(CopySource{d}, n, out, s);
     return hipGetLastError();
 }
 
 hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t *expected, size_t exp_stride,
                               int64_t *copied, uint32_t *csum, uint32_t *mask, uint32_t *nbad, int mode,
-                              const uint32_t *img, hipStream_t s) {
+                              const uint32_t *img, hipStream_t s, uint32_t rows_hint) {
     hipError_t e = hipMemsetAsync(nbad, 0, sizeof(uint32_t), s);
     if (e == hipSuccess && n) e = hipMemsetAsync(mask, 0, (n + 31) / 32 * sizeof(uint32_t), s);
     if (e != hipSuccess || n == 0) return e;
     if (!img) return hipErrorInvalidValue;
     const bool crc = mode == LAMPI_CSUM_CRC32;
     const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
-    if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s);
+    if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s, rows_hint);
     launch_sum_copy(src, n, csum, s);
     return hipGetLastError();
 }

@@ -34,8 +34,9 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
 hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
                               const uint32_t *img, int grid, hipStream_t s);
 // Fused copy + checksum (bcopy_uicrc / bcopy_uicsum per descriptor), mode = lampi_csum_mode.
+// rows_hint (LAMPI_CSUM_ROWS_HINT, CRC): row groups per fragment, 1 = one wave walks every row
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
-                             hipStream_t s);
+                             hipStream_t s, uint32_t rows_hint = 1);
 // Fused copy of regular batches: fragment f -> dst + f*dst_stride (dst, dst_stride 4-byte aligned).
 hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint8_t *dst,
                                    size_t dst_stride, uint32_t *out, const uint32_t *img, hipStream_t s);
@@ -45,7 +46,7 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
 // RecvDesc_t::CopyToApp per descriptor (copy min(length, app_len), checksum length, verify).
 hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t *expected, size_t exp_stride,
                               int64_t *copied, uint32_t *csum, uint32_t *mask, uint32_t *nbad, int mode,
-                              const uint32_t *img, hipStream_t s);
+                              const uint32_t *img, hipStream_t s, uint32_t rows_hint = 1);
 // headerChecksum per header / receiver header check / CheckData (mask bit set = corrupt).
 hipError_t launch_header_csum(const uint8_t *hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
                               int mode, const uint32_t *img, uint32_t *out, hipStream_t s);

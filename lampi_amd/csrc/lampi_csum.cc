@@ -584,6 +584,8 @@ int lampi_frag_csum_batch_strided(const lampi_frag_desc *d_descs, size_t n, void
 }
 
 int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
+    const uint32_t rows_hint = std::max(1u, LAMPI_CSUM_ROWS_HINT_OF(mode));
+    mode &= ~LAMPI_CSUM_ROWS_HINT_MASK;
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;
     if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);
@@ -593,12 +595,14 @@ int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d
     const uint32_t *img = nullptr;  // CRC: the tables
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
-    return to_int(launch_bcopy_desc(d_descs, n, d_out, mode, img, (hipStream_t)stream));
+    return to_int(launch_bcopy_desc(d_descs, n, d_out, mode, img, (hipStream_t)stream, rows_hint));
 }
 
 int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void *d_expected, size_t expected_stride,
                             int64_t *d_copied, uint32_t *d_csum, uint32_t *d_mask, uint32_t *d_nbad, int mode,
                             void *stream) {
+    const uint32_t rows_hint = std::max(1u, LAMPI_CSUM_ROWS_HINT_OF(mode));
+    mode &= ~LAMPI_CSUM_ROWS_HINT_MASK;
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (!d_nbad || (n && (!d_descs || !d_expected || !d_copied || !d_csum || !d_mask)) ||
         ((uintptr_t)d_expected & 3u) || (expected_stride & 3u) || n > 0xFFFFFFFFull)
@@ -610,7 +614,7 @@ int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
     return to_int(launch_copy_to_app(d_descs, n, (const uint8_t *)d_expected, expected_stride, d_copied, d_csum, d_mask,
-                                     d_nbad, mode, img, (hipStream_t)stream));
+                                     d_nbad, mode, img, (hipStream_t)stream, rows_hint));
 }
 
 int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t partial, uint32_t *d_out, int mode,

@@ -9,7 +9,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ._lib import BY_BYTES, CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib
+from ._lib import BY_BYTES, CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib, rows_hint_bits
 
 __all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
            "make_descs", "make_copy_descs", "as_u32", "chain_csum_batch", "header_csum_batch", "header_check_batch", "check_data_batch",
@@ -83,8 +83,9 @@ def make_copy_descs(src: torch.Tensor, src_offsets, dst: torch.Tensor, dst_offse
 
 
 def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
-                     stream: torch.cuda.Stream | None = None) -> torch.Tensor:
-    """Fused bcopy_uicrc / bcopy_uicsum per ``lampi_copy_desc``; returns the checksums."""
+                     stream: torch.cuda.Stream | None = None, rows_hint: int = 0) -> torch.Tensor:
+    """Fused bcopy_uicrc / bcopy_uicsum per ``lampi_copy_desc``; returns the checksums.
+    rows_hint: LAMPI_CSUM_ROWS_HINT -- fragments span about that many 4 KiB rows (CRC: row groups)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
     if out is None:
@@ -92,7 +93,8 @@ def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC3
     _require_cuda(out, "out")
     if out.numel() < count:
         raise ValueError("out is too small")
-    check(lib().lampi_frag_bcopy_batch(descs.data_ptr(), count, out.data_ptr(), mode, _stream_handle(stream)),
+    check(lib().lampi_frag_bcopy_batch(descs.data_ptr(), count, out.data_ptr(), mode | rows_hint_bits(rows_hint),
+                                       _stream_handle(stream)),
           "lampi_frag_bcopy_batch")
     return out
 
@@ -315,9 +317,11 @@ def make_recv_descs(frag: torch.Tensor, frag_offsets, app: torch.Tensor, app_off
 
 
 def copy_to_app_batch(descs: torch.Tensor, expected: torch.Tensor, expected_stride: int = 4, expected_offset: int = 0,
-                      n: int | None = None, mode: int = CRC32, stream: torch.cuda.Stream | None = None):
+                      n: int | None = None, mode: int = CRC32, stream: torch.cuda.Stream | None = None,
+                      rows_hint: int = 0):
     """RecvDesc_t::CopyToApp over a batch (src/path/common/BaseDesc.cc:288-342): returns
-    (copied int64[n] -- bytes copied or -1 when corrupt --, csum int32[n], mask, nbad)."""
+    (copied int64[n] -- bytes copied or -1 when corrupt --, csum int32[n], mask, nbad).
+    rows_hint: as for frag_bcopy_batch (GM's 65,456-byte payloads: 16)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
     _records(expected.view(torch.uint8)[expected_offset:] if count else expected, count, expected_stride, "expected")
@@ -325,8 +329,9 @@ def copy_to_app_batch(descs: torch.Tensor, expected: torch.Tensor, expected_stri
     csum = torch.empty(max(count, 1), dtype=torch.int32, device=descs.device)
     mask, nbad = _mask_out(count, descs.device)
     check(lib().lampi_copy_to_app_batch(descs.data_ptr(), count, expected.data_ptr() + expected_offset, expected_stride,
-                                        copied.data_ptr(), csum.data_ptr(), mask.data_ptr(), nbad.data_ptr(), mode,
-                                        _stream_handle(stream)), "lampi_copy_to_app_batch")
+                                        copied.data_ptr(), csum.data_ptr(), mask.data_ptr(), nbad.data_ptr(),
+                                        mode | rows_hint_bits(rows_hint), _stream_handle(stream)),
+          "lampi_copy_to_app_batch")
     return copied[:count], csum[:count], mask, nbad
 
 

@@ -35,7 +35,7 @@ def _layout(totals, copylens, src_align, dst_align):
     return so.astype(np.uint64), do.astype(np.uint64), int(slot_s.sum()), int(slot_d.sum())
 
 
-def _run(cuda, oracle, copylens, csumlens, src_align, dst_align, partials, mode, src_fill=None):
+def _run(cuda, oracle, copylens, csumlens, src_align, dst_align, partials, mode, src_fill=None, rows_hint=0):
     """Run one batch; return (checksums, expected checksums, dst bytes, expected dst bytes)."""
     import torch
 
@@ -58,7 +58,7 @@ def _run(cuda, oracle, copylens, csumlens, src_align, dst_align, partials, mode,
         a, b, n = int(so[i]), int(do[i]), int(cl[i])
         want_dst[b:b + n] = host_src[a:a + n]
     descs = dv.make_copy_descs(src, so, dst, do, cl, sl, partials)
-    got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=mode))
+    got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=mode, rows_hint=rows_hint))
     want = oracle.desc_batch(host_src, so, tot.astype(np.uint32),
                              None if mode == 1 else np.asarray(partials, np.uint64).astype(np.uint32), mode)
     return got, want, dst.cpu().numpy(), want_dst
@@ -105,6 +105,34 @@ def test_bcopy_batch_edges_and_alignment(cuda, oracle, mode):
     parts = rng.integers(0, 2**32, size=len(cl), dtype=np.uint64)
     parts[::4] = 0xFFFFFFFF
     got, want, dgot, dwant = _run(cuda, oracle, cl, sl, sa, da, parts, mode)
+    _assert_same(got, want, dgot, dwant, lambda i: (cl[i], sl[i], sa[i], da[i]))
+
+
+@pytest.mark.parametrize("rows_hint", [2, 3, 16, 64])
+def test_bcopy_batch_row_groups(cuda, oracle, rows_hint):
+    """CRC with LAMPI_CSUM_ROWS_HINT: each fragment's rows run as row groups (ceil(R / hint) rows each)
+    in parallel and are joined afterwards -- edge lengths x alignments x copy =, <, > checksum length,
+    then fragments of up to ~300 KB (more rows than the hint: groups of several rows, a short last
+    group), every checksum and destination byte against the oracle."""
+    rng = np.random.default_rng(900 + rows_hint)
+    cl, sl, sa, da = [], [], [], []
+    for L in EDGE_LENS:
+        for a in range(0, 16, 5):
+            for kind in range(3):
+                short = int(rng.integers(0, L + 1))
+                cl.append(L if kind != 1 else short)
+                sl.append(L if kind != 2 else short)
+                sa.append(a)
+                da.append(int(rng.integers(0, 16)))
+    n = 600
+    big_c = rng.integers(0, 300000, size=n)
+    big_s = np.where(rng.random(n) < 0.3, rng.integers(0, 300000, size=n), big_c)
+    cl += big_c.tolist()
+    sl += big_s.tolist()
+    sa += rng.integers(0, 16, size=n).tolist()
+    da += rng.integers(0, 16, size=n).tolist()
+    parts = rng.integers(0, 2**32, size=len(cl), dtype=np.uint64)
+    got, want, dgot, dwant = _run(cuda, oracle, cl, sl, sa, da, parts, 0, rows_hint=rows_hint)
     _assert_same(got, want, dgot, dwant, lambda i: (cl[i], sl[i], sa[i], da[i]))
 
 

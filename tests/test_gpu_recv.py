@@ -45,7 +45,7 @@ def _batch(rng, n, lengths=None):
     return lengths, app_len
 
 
-def _run_case(cuda, oracle, mode, lengths, app_len, rng, app_misalign=True, corrupt_frac=0.1):
+def _run_case(cuda, oracle, mode, lengths, app_len, rng, app_misalign=True, corrupt_frac=0.1, rows_hint=0):
     import torch
 
     from oracle.oracle import copy_to_app
@@ -86,7 +86,7 @@ def _run_case(cuda, oracle, mode, lengths, app_len, rng, app_misalign=True, corr
     aoff = (np.concatenate([[0], np.cumsum(aslot[:-1])]) + gap).astype(np.int64)
     app = torch.full((int(aslot.sum()) + 64,), 0x5C, dtype=torch.uint8, device=cuda)
     descs = dv.make_recv_descs(nic, poff, app, aoff, lengths, app_len)
-    copied, csum, mask, nbad = _call(dv, descs, nic, soff, slot, n, mode)
+    copied, csum, mask, nbad = _call(dv, descs, nic, soff, slot, n, mode, rows_hint)
     got_copied = copied.cpu().numpy()
     got_csum = csum.cpu().numpy().view(np.uint32)
     want_copied = np.array([r[0] for r in ref], np.int64)
@@ -106,7 +106,7 @@ def _run_case(cuda, oracle, mode, lengths, app_len, rng, app_misalign=True, corr
     return bad_want
 
 
-def _call(dv, descs, nic, soff, slot, n, mode):
+def _call(dv, descs, nic, soff, slot, n, mode, rows_hint=0):
     """Expected checksums read straight out of the NIC buffers' headers: dataChecksum of record i
     at soff[i] + 64.  Uniform slots are one strided array (a GM receive ring); slots of varying
     size are first gathered into an array of 72-byte headers on the device."""
@@ -114,10 +114,11 @@ def _call(dv, descs, nic, soff, slot, n, mode):
 
     if np.all(slot == slot[0]):
         return dv.copy_to_app_batch(descs, nic, expected_stride=int(slot[0]), expected_offset=int(soff[0]) + DCSUM_OFF,
-                                    n=n, mode=mode)
+                                    n=n, mode=mode, rows_hint=rows_hint)
     idx = torch.from_numpy(soff[:, None] + np.arange(HDR)[None, :]).to(nic.device)
     hdrs = nic[idx.reshape(-1)].contiguous()
-    return dv.copy_to_app_batch(descs, hdrs, expected_stride=HDR, expected_offset=DCSUM_OFF, n=n, mode=mode)
+    return dv.copy_to_app_batch(descs, hdrs, expected_stride=HDR, expected_offset=DCSUM_OFF, n=n, mode=mode,
+                                rows_hint=rows_hint)
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
@@ -140,6 +141,25 @@ def test_copy_to_app_edges(cuda, oracle, mode):
             lengths.append(ln)
             app_len.append(a)
     _run_case(cuda, oracle, mode, np.array(lengths), np.array(app_len), rng, corrupt_frac=0.3)
+
+
+@pytest.mark.parametrize("rows_hint", [3, 16])
+def test_copy_to_app_row_groups(cuda, oracle, rows_hint):
+    """CRC receive step with LAMPI_CSUM_ROWS_HINT (GM: 16 for 65,456-byte payloads): row groups joined
+    before the verdict -- the edge cases (AppBufferLen <= 0 .. > length, corrupt and clean), then GM-sized
+    payloads and longer ones (groups of several rows), every copy, checksum and verdict vs the oracle."""
+    rng = np.random.default_rng(31 + rows_hint)
+    L = [0, 1, 3, 4, 5, 63, 64, 65, 1975, 1976, 4095, 4096, 4097, 8192, 65455, 65456, 65536, 200003]
+    lengths, app_len = [], []
+    for ln in L:
+        for a in sorted({-1, 0, 1, ln - 1, ln, ln + 1, 1 << 33}):
+            lengths.append(ln)
+            app_len.append(a)
+    _run_case(cuda, oracle, 0, np.array(lengths), np.array(app_len), rng, corrupt_frac=0.3, rows_hint=rows_hint)
+    n = 300
+    lengths = np.where(rng.random(n) < 0.7, 65456, rng.integers(0, 140000, size=n))
+    bad = _run_case(cuda, oracle, 0, lengths, np.full(n, 1 << 20), rng, corrupt_frac=0.1, rows_hint=rows_hint)
+    assert bad.any() and not bad.all()
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])

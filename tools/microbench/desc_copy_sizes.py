@@ -35,11 +35,16 @@ for L in (1976, 4096, 16384, 65456, 1 << 20):
     offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
     want = dv.msg_csum(src[:n * L], L)
     out = torch.empty(n, dtype=torch.int32, device="cuda")
+    R = (L + 4095) // 4096
+    hints = (0, R) if R > 1 else (0,)  # LAMPI_CSUM_ROWS_HINT: the fragment's rows as parallel row groups
     for tag, doff in (("aligned", 0), ("dst+8", 8)):
         descs = dv.make_copy_descs(src, offs, dst, offs + np.uint64(doff), np.full(n, L), np.full(n, L))
-        s = timed(lambda: dv.frag_bcopy_batch(descs, n=n, out=out))
-        ok = torch.equal(out, want) and torch.equal(dst[doff:doff + n * L], src[:n * L])
-        print(f"bcopy L={L:8d} n={n:7d} {tag:8s} {2 * n * L / s / 8e12:.3f} of 8 TB/s  ok={ok}", flush=True)
+        for h in hints:
+            dst[doff:doff + n * L].zero_()
+            s = timed(lambda: dv.frag_bcopy_batch(descs, n=n, out=out, rows_hint=h))
+            ok = torch.equal(out, want) and torch.equal(dst[doff:doff + n * L], src[:n * L])
+            print(f"bcopy L={L:8d} n={n:7d} {tag:8s} hint={h:4d} {2 * n * L / s / 8e12:.3f} of 8 TB/s  ok={ok}",
+                  flush=True)
     # receive step: payloads at 72 + k * (72 + L + 8) with the expected checksum stamped at 64
     stride = 72 + L + 8
     m = min(n, (dst.numel() - 64) // stride)
@@ -50,9 +55,12 @@ for L in (1976, 4096, 16384, 65456, 1 << 20):
     mo = np.arange(m, dtype=np.uint64)
     rd = dv.make_recv_descs(nic, mo * np.uint64(stride) + np.uint64(72), app, mo * np.uint64(L), np.full(m, L),
                             np.full(m, 1 << 40, dtype=np.int64))
-    run = lambda: dv.copy_to_app_batch(rd, nic, expected_stride=stride, expected_offset=64, n=m)  # noqa: E731
-    s = timed(run)
-    copied, csum, mask, nbad = run()
-    ok = int(nbad.item()) == 0 and torch.equal(app, src[:m * L])
-    print(f"recv  L={L:8d} n={m:7d}          {2 * m * L / s / 8e12:.3f} of 8 TB/s  ok={ok}", flush=True)
+    for h in hints:
+        app.zero_()
+        run = lambda: dv.copy_to_app_batch(rd, nic, expected_stride=stride, expected_offset=64, n=m,  # noqa: E731
+                                           rows_hint=h)
+        s = timed(run)
+        copied, csum, mask, nbad = run()
+        ok = int(nbad.item()) == 0 and torch.equal(app, src[:m * L])
+        print(f"recv  L={L:8d} n={m:7d}          hint={h:4d} {2 * m * L / s / 8e12:.3f} of 8 TB/s  ok={ok}", flush=True)
     del app
