@@ -200,6 +200,32 @@ struct MsgRowCopySource {
     }
 };
 
+// Row group g of fragment f (item v = f * W + g; LAMPI_CSUM_ROWS_HINT, SUM copies): the fragment's bytes
+// [g k 4096, min((g + 1) k 4096, len)) with k = ceil(ceil(len / 4096) / W) -- every group starts on the
+// fragment's word grid -- and the part of the copy inside them; groups past the fragment are empty.
+// The kernel stores each group's sum at out[v] (scratch); sum_group_join_kernel adds them and emits.
+template <class Src>
+struct GroupSource {
+    static constexpr bool kCopy = Src::kCopy;
+    static constexpr bool kPhase = false;
+    Src src;
+    uint32_t W;
+    __device__ FragInfo get(size_t v) const {
+        const size_t f = v / W;
+        const uint32_t g = (uint32_t)(v - f * W);
+        FragInfo fi = src.get(f);
+        const uint64_t R = ((uint64_t)fi.len + kRowBytes - 1) / kRowBytes, k = (R + W - 1) / W;
+        const uint64_t a = min((uint64_t)g * k * kRowBytes, (uint64_t)fi.len);
+        const uint64_t e = min(a + k * kRowBytes, (uint64_t)fi.len);
+        const uint64_t ce = min(e, (uint64_t)fi.copylen);
+        fi.addr += a;
+        fi.len = (uint32_t)(e - a);
+        fi.dst += a;
+        fi.copylen = ce > a ? (uint32_t)(ce - a) : 0u;
+        return fi;
+    }
+};
+
 // One piece of a host call (lampi_uicrc / lampi_uicsum on at most kZeroCopy bytes) by value, so
 // no descriptor is read back over PCIe; its result is followed by the host signal (emit).
 struct HostOneSource {
@@ -2904,6 +2930,20 @@ __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint
     }
 }
 
+// SUM row groups: out[f] = the sum of fragment f's W group sums, then emit (receive sources: the verdict).
+template <class Src>
+__global__ void __launch_bounds__(256) sum_group_join_kernel(const Src src, size_t n, uint32_t W,
+                                                             const uint32_t *__restrict__ groups,
+                                                             uint32_t *__restrict__ out) {
+    const size_t f = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (f >= n) return;
+    const FragInfo fi = src.get(f);
+    const uint32_t *p = groups + f * W;
+    uint32_t sm = 0;
+    for (uint32_t g = 0; g < W; ++g) sm += p[g];
+    emit(src, out, f, sm, fi);
+}
+
 // Acc = uint32_t: uicsum (32-bit words); Acc = uint64_t: csum (64-bit words, ref
 // MemFunctions.cc:142-516, 913-1071).  Phase (kPhase sources) is taken mod the word size.
 template <class Src, class Acc = uint32_t, int kWv = kWaves>
@@ -3860,13 +3900,34 @@ static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t
                        n, out);
 }
 
+// With LAMPI_CSUM_ROWS_HINT (W > 1): each fragment as W row-group workgroups, their sums joined.
+template <class Src>
+static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out, hipStream_t s, uint32_t W) {
+    while (W > 1 && (size_t)n * W > ((size_t)1 << 31)) W >>= 1;
+    if (W <= 1) {
+        launch_sum_copy(src, n, out, s);
+        return hipGetLastError();
+    }
+    uint32_t *groups = nullptr;
+    bool pooled = false;
+    hipError_t e = stream_scratch(s, n * W * sizeof(uint32_t), (void **)&groups, &pooled);
+    if (e != hipSuccess) return e;
+    launch_sum_copy(GroupSource<Src>{src, W}, n * W, groups, s);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(sum_group_join_kernel<Src>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, n, W,
+                           groups, out);
+        e = hipGetLastError();
+    }
+    return scratch_done(s, groups, pooled, e);
+}
+
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                              hipStream_t s, uint32_t rows_hint) {
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC)
     if (mode == LAMPI_CSUM_CRC32) return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
-    launch_sum_copy(CopySource{d}, n, out, s);
-    return hipGetLastError();
+    return launch_sum_copy_groups(CopySource{d}, n, out, s, rows_hint);
 }
 
 hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t *expected, size_t exp_stride,
@@ -3879,8 +3940,7 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
     const bool crc = mode == LAMPI_CSUM_CRC32;
     const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
     if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s, rows_hint);
-    launch_sum_copy(src, n, csum, s);
-    return hipGetLastError();
+    return launch_sum_copy_groups(src, n, csum, s, rows_hint);
 }
 
 hipError_t launch_sum64_desc(const lampi_frag_desc *d, size_t n, uint64_t *out, bool phased, hipStream_t s) {

@@ -34,7 +34,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
 hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
                               const uint32_t *img, int grid, hipStream_t s);
 // Fused copy + checksum (bcopy_uicrc / bcopy_uicsum per descriptor), mode = lampi_csum_mode.
-// rows_hint (LAMPI_CSUM_ROWS_HINT, CRC): row groups per fragment, 1 = one wave walks every row
+// rows_hint (LAMPI_CSUM_ROWS_HINT): row groups per fragment, 1 = one wave (SUM: workgroup) walks every row
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                              hipStream_t s, uint32_t rows_hint = 1);
 // Fused copy of regular batches: fragment f -> dst + f*dst_stride (dst, dst_stride 4-byte aligned).

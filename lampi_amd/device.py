@@ -85,7 +85,7 @@ def make_copy_descs(src: torch.Tensor, src_offsets, dst: torch.Tensor, dst_offse
 def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
                      stream: torch.cuda.Stream | None = None, rows_hint: int = 0) -> torch.Tensor:
     """Fused bcopy_uicrc / bcopy_uicsum per ``lampi_copy_desc``; returns the checksums.
-    rows_hint: LAMPI_CSUM_ROWS_HINT -- fragments span about that many 4 KiB rows (CRC: row groups)."""
+    rows_hint: LAMPI_CSUM_ROWS_HINT -- fragments span about that many 4 KiB rows (row groups)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
     if out is None:

@@ -108,12 +108,14 @@ def test_bcopy_batch_edges_and_alignment(cuda, oracle, mode):
     _assert_same(got, want, dgot, dwant, lambda i: (cl[i], sl[i], sa[i], da[i]))
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 @pytest.mark.parametrize("rows_hint", [2, 3, 16, 64])
-def test_bcopy_batch_row_groups(cuda, oracle, rows_hint):
-    """CRC with LAMPI_CSUM_ROWS_HINT: each fragment's rows run as row groups (ceil(R / hint) rows each)
-    in parallel and are joined afterwards -- edge lengths x alignments x copy =, <, > checksum length,
-    then fragments of up to ~300 KB (more rows than the hint: groups of several rows, a short last
-    group), every checksum and destination byte against the oracle."""
+def test_bcopy_batch_row_groups(cuda, oracle, rows_hint, mode):
+    """LAMPI_CSUM_ROWS_HINT: each fragment's rows run as row groups (ceil(R / hint) rows each) in
+    parallel and are joined afterwards (CRC: shifted and XORed; SUM: added) -- edge lengths x
+    alignments x copy =, <, > checksum length, then fragments of up to ~300 KB (more rows than the
+    hint: groups of several rows, a short last group), every checksum and destination byte against
+    the oracle."""
     rng = np.random.default_rng(900 + rows_hint)
     cl, sl, sa, da = [], [], [], []
     for L in EDGE_LENS:
@@ -132,7 +134,7 @@ def test_bcopy_batch_row_groups(cuda, oracle, rows_hint):
     sa += rng.integers(0, 16, size=n).tolist()
     da += rng.integers(0, 16, size=n).tolist()
     parts = rng.integers(0, 2**32, size=len(cl), dtype=np.uint64)
-    got, want, dgot, dwant = _run(cuda, oracle, cl, sl, sa, da, parts, 0, rows_hint=rows_hint)
+    got, want, dgot, dwant = _run(cuda, oracle, cl, sl, sa, da, parts, mode, rows_hint=rows_hint)
     _assert_same(got, want, dgot, dwant, lambda i: (cl[i], sl[i], sa[i], da[i]))
 
 

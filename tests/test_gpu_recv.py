@@ -143,9 +143,10 @@ def test_copy_to_app_edges(cuda, oracle, mode):
     _run_case(cuda, oracle, mode, np.array(lengths), np.array(app_len), rng, corrupt_frac=0.3)
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 @pytest.mark.parametrize("rows_hint", [3, 16])
-def test_copy_to_app_row_groups(cuda, oracle, rows_hint):
-    """CRC receive step with LAMPI_CSUM_ROWS_HINT (GM: 16 for 65,456-byte payloads): row groups joined
+def test_copy_to_app_row_groups(cuda, oracle, rows_hint, mode):
+    """The receive step with LAMPI_CSUM_ROWS_HINT (GM: 16 for 65,456-byte payloads): row groups joined
     before the verdict -- the edge cases (AppBufferLen <= 0 .. > length, corrupt and clean), then GM-sized
     payloads and longer ones (groups of several rows), every copy, checksum and verdict vs the oracle."""
     rng = np.random.default_rng(31 + rows_hint)
@@ -155,10 +156,10 @@ def test_copy_to_app_row_groups(cuda, oracle, rows_hint):
         for a in sorted({-1, 0, 1, ln - 1, ln, ln + 1, 1 << 33}):
             lengths.append(ln)
             app_len.append(a)
-    _run_case(cuda, oracle, 0, np.array(lengths), np.array(app_len), rng, corrupt_frac=0.3, rows_hint=rows_hint)
+    _run_case(cuda, oracle, mode, np.array(lengths), np.array(app_len), rng, corrupt_frac=0.3, rows_hint=rows_hint)
     n = 300
     lengths = np.where(rng.random(n) < 0.7, 65456, rng.integers(0, 140000, size=n))
-    bad = _run_case(cuda, oracle, 0, lengths, np.full(n, 1 << 20), rng, corrupt_frac=0.1, rows_hint=rows_hint)
+    bad = _run_case(cuda, oracle, mode, lengths, np.full(n, 1 << 20), rng, corrupt_frac=0.1, rows_hint=rows_hint)
     assert bad.any() and not bad.all()
 
 
