@@ -331,6 +331,7 @@ struct SegSource {
     static constexpr bool kPhase = false;
     const SegDesc *s;
     const lampi_frag_desc *d;
+    __device__ SegDesc segment(size_t j) const { return s[j]; }
     __device__ FragInfo get(size_t j) const {
         const SegDesc x = s[j];
         const lampi_frag_desc D = d[x.frag];
@@ -342,6 +343,50 @@ template <class S>
 struct IsSeg : std::false_type {};
 template <>
 struct IsSeg<SegSource> : std::true_type {};
+
+// Row segments (LAMPI_CSUM_ROWS_HINT on lampi_frag_csum_batch): item v = f W + g is segment g of fragment f,
+// its frame rows [g k, min((g + 1) k, R)) with R = ceil(L / 4096), k = ceil(R / W) -- CRC cut from the
+// fragment's end (every segment but the first on a frame row boundary), SUM from its start -- computed on
+// the device from the descriptor, no plan launch.  The launcher zeroes out; split fragments XOR (add) their
+// shifted parts into it as the plan's segments do; items past a fragment's last segment are skipped.
+constexpr uint32_t kSegSkip = 0xFFFFFFFFu;
+struct RowSegSource {
+    static constexpr bool kCopy = false;
+    static constexpr bool kPhase = false;
+    const lampi_frag_desc *d;
+    uint32_t W;
+    int sum;
+    __device__ SegDesc segment(size_t v) const {
+        const size_t f = v / W;
+        const uint32_t g = (uint32_t)(v - f * W);
+        const uint64_t L = d[f].length;
+        const uint64_t R = (L + kRowBytes - 1) / kRowBytes;
+        const uint64_t k = R ? (R + W - 1) / W : 1u, ng = R ? (R + k - 1) / k : 1u;
+        if (g >= ng) return SegDesc{(uint32_t)f, 0u, 0u, kSegSkip};
+        const uint64_t r1 = min((uint64_t)(g + 1) * k, R);
+        uint64_t a, e;
+        if (sum) {
+            a = min((uint64_t)g * k * kRowBytes, L);
+            e = min(r1 * kRowBytes, L);
+        } else {
+            const uint64_t P = R * kRowBytes - L;
+            a = g ? (uint64_t)g * k * kRowBytes - P : 0u;
+            e = r1 * kRowBytes - P;
+        }
+        const uint32_t rows = sum ? 0u : (uint32_t)(R - r1);
+        return SegDesc{(uint32_t)f, (uint32_t)a, (uint32_t)(e - a), rows | (ng > 1 ? kSegSplit : 0u)};
+    }
+    __device__ FragInfo get(size_t v) const {
+        const SegDesc x = segment(v);
+        const lampi_frag_desc D = d[x.frag];
+        return {(gbyte *)(uintptr_t)(D.addr + x.off), x.len, x.off == 0u ? D.partial : 0u, nullptr, 0u};
+    }
+};
+// sources whose items are segments of fragments (the epilogue stores or joins by SegDesc)
+template <class S>
+struct HasSegments : IsSeg<S> {};
+template <>
+struct HasSegments<RowSegSource> : std::true_type {};
 
 // every kernel stores a fragment's checksum through this: receive sources also decide it
 template <class Src, class Acc>
@@ -1906,8 +1951,9 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     if (gown != ~0u) sres[sj[gown]] = kSum ? sjoin[t] : __builtin_bswap32(sjoin[t]);
     __syncthreads();
     if (t >= nwg) return;
-    if constexpr (IsSeg<Src>::value) {  // a segment: its fragment's value, or its part of a split one
-        const SegDesc x = src.s[base + t];
+    if constexpr (HasSegments<Src>::value) {  // a segment: its fragment's value, or its part of a split one
+        const SegDesc x = src.segment(base + t);
+        if (x.rows == kSegSkip) return;
         uint32_t v = sres[t];
         if (!(x.rows & kSegSplit)) {
             out[x.frag] = v;
@@ -3772,11 +3818,39 @@ static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *o
     return scratch_done(s, scratch, pooled, e);
 }
 
+// LAMPI_CSUM_ROWS_HINT(r) on a read-only descriptor batch (fragments of about r rows): the count split
+// sizes workgroups by that length (spread_fpw, as for messages: 16,404 x 65,456 B in workgroups of 6,
+// not 48), and fragments longer than kSegRows rows run as W = ceil(r / kSegRows) row segments each
+// (RowSegSource, out zeroed first: split fragments accumulate into it) -- segments of ~64 KiB, so the
+// per-segment join (a constant-product shift past the later rows) stays small against its rows.
+constexpr uint32_t kSegRows = 16;
+template <bool kSum, int kWv, int kCap>
+static hipError_t launch_row_segments(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
+                                      hipStream_t s, uint32_t rows_hint) {
+    const uint32_t W = (rows_hint + kSegRows - 1) / kSegRows;
+    if (W <= 1) {
+        const size_t frag = (size_t)rows_hint * kRowBytes;
+        const uint32_t fpg = kSum ? sum_frags_per_wg(n, frag) : frags_per_wg(n, frag);
+        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, kSum, kWv, kCap>), frags_grid(n, fpg),
+                           dim3(64 * kWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
+        return hipGetLastError();
+    }
+    const hipError_t e = hipMemsetAsync(out, 0, n * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const size_t items = n * W, seg = (size_t)kSegRows * kRowBytes;
+    const uint32_t fpg = kSum ? sum_frags_per_wg(items, seg) : frags_per_wg(items, seg);
+    hipLaunchKernelGGL((crc_stream_kernel<RowSegSource, kStreamD, kStreamK, kSum, kWv, kCap>), frags_grid(items, fpg),
+                       dim3(64 * kWv), 0, s, RowSegSource{d, W, kSum ? 1 : 0}, items, fpg, img, out, nullptr);
+    return hipGetLastError();
+}
+
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
-                           hipStream_t s, bool plan) {
+                           hipStream_t s, bool plan, uint32_t rows_hint) {  // (defaults: frag_csum_kernels.h)
     (void)grid;
     if (n == 0) return hipSuccess;
     if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
+    if (rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
+        return launch_row_segments<false, kStreamWv, kStreamCap>(d, n, out, img, s, rows_hint);
     const uint32_t fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
                        frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
@@ -3962,10 +4036,12 @@ hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t 
 }
 
 hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
-                           hipStream_t s, bool plan) {
+                           hipStream_t s, bool plan, uint32_t rows_hint) {
     (void)grid;
     if (n == 0) return hipSuccess;
     if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
+    if (img && rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
+        return launch_row_segments<true, kSumWv, kSumCap>(d, n, out, img, s, rows_hint);
     if (img) {  // piece streams (img: the zero chunk)
         const uint32_t fpg = sum_frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, true, kSumWv, kSumCap>),

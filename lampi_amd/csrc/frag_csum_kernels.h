@@ -23,8 +23,9 @@ int crc_grid(int device);
 
 // Descriptor batches; plan (LAMPI_CSUM_BY_BYTES): byte-balanced for n <= 32768, a plan kernel first;
 // otherwise the one-launch count split.
+// rows_hint (LAMPI_CSUM_ROWS_HINT): row segments per fragment (RowSegSource), 1 = none
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
-                           hipStream_t s, bool plan = false);
+                           hipStream_t s, bool plan = false, uint32_t rows_hint = 1);
 // One wavefront per fragment (crc_rows_kernel / sum_rows_kernel), mode = lampi_csum_mode.
 hipError_t launch_desc_per_wave(const lampi_frag_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                                 hipStream_t s);
@@ -72,7 +73,7 @@ hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t 
 // SUM per descriptor / per fragment of a message: piece streams when img (the table image, for its
 // zero chunk) is given, one wavefront per fragment (sum_rows_kernel) otherwise.
 hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
-                           hipStream_t s, bool plan = false);
+                           hipStream_t s, bool plan = false, uint32_t rows_hint = 1);
 hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n, uint32_t *out,
                           const uint32_t *img, int grid, hipStream_t s);
 hipError_t launch_crc_combine(const uint32_t *vals, uint32_t n, const uint32_t *tabs, uint32_t npow,

@@ -536,7 +536,8 @@ int lampi_frag_csum64_batch(const lampi_frag_desc *d_descs, size_t n, uint64_t *
 
 int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
     const bool by_bytes = (mode & LAMPI_CSUM_BY_BYTES) != 0;
-    mode &= ~LAMPI_CSUM_BY_BYTES;
+    const uint32_t rows_hint = std::max(1u, LAMPI_CSUM_ROWS_HINT_OF(mode));
+    mode &= ~(LAMPI_CSUM_BY_BYTES | LAMPI_CSUM_ROWS_HINT_MASK);
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;
     if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);
@@ -547,8 +548,9 @@ int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_
     const uint32_t *img = nullptr;
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
-    if (mode == LAMPI_CSUM_SUM32) return to_int(launch_sum_desc(d_descs, n, d_out, img, crc_grid(dev), s, by_bytes));
-    return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s, by_bytes));
+    if (mode == LAMPI_CSUM_SUM32)
+        return to_int(launch_sum_desc(d_descs, n, d_out, img, crc_grid(dev), s, by_bytes, rows_hint));
+    return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s, by_bytes, rows_hint));
 }
 
 int lampi_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode,
@@ -567,7 +569,7 @@ int lampi_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uin
 
 int lampi_frag_csum_batch_strided(const lampi_frag_desc *d_descs, size_t n, void *d_out, size_t out_stride, int mode,
                                   void *stream) {
-    const int base_mode = mode & ~LAMPI_CSUM_BY_BYTES;
+    const int base_mode = mode & ~(LAMPI_CSUM_BY_BYTES | LAMPI_CSUM_ROWS_HINT_MASK);
     if (base_mode != LAMPI_CSUM_CRC32 && base_mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;
     if (!d_descs || !d_out || ((uintptr_t)d_out & 3u) || (out_stride & 3u) || out_stride < 4 || n > 0xFFFFFFFFull)

@@ -100,9 +100,11 @@ def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC3
 
 
 def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
-                    stream: torch.cuda.Stream | None = None, by_bytes: bool = False) -> torch.Tensor:
+                    stream: torch.cuda.Stream | None = None, by_bytes: bool = False, rows_hint: int = 0) -> torch.Tensor:
     """out[i] = checksum of fragment descs[i] (piece streams: fragments of any size share rows).
-    by_bytes: LAMPI_CSUM_BY_BYTES -- plan the work by bytes (large fragments split across workgroups)."""
+    by_bytes: LAMPI_CSUM_BY_BYTES -- plan the work by bytes (large fragments split across workgroups).
+    rows_hint: LAMPI_CSUM_ROWS_HINT -- fragments span about that many 4 KiB rows: each runs as that many
+    row segments computed on the device (no plan launch)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 16 if n is None else int(n)
     if out is None:
@@ -110,7 +112,8 @@ def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32
     _require_cuda(out, "out")
     if out.numel() < count:
         raise ValueError("out is too small")
-    check(lib().lampi_frag_csum_batch(descs.data_ptr(), count, out.data_ptr(), mode | (BY_BYTES if by_bytes else 0),
+    check(lib().lampi_frag_csum_batch(descs.data_ptr(), count, out.data_ptr(),
+                                      mode | (BY_BYTES if by_bytes else 0) | rows_hint_bits(rows_hint),
                                       _stream_handle(stream)), "lampi_frag_csum_batch")
     return out
 

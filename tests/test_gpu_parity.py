@@ -327,6 +327,84 @@ def test_descriptor_batch_byte_balanced(cuda, oracle, case, mode):
     assert np.array_equal(dv.as_u32(dv.frag_csum_batch(descs, mode=mode)), got)
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_descriptor_batch_row_segments(cuda, oracle, mode):
+    """LAMPI_CSUM_ROWS_HINT on lampi_frag_csum_batch: workgroups sized by the hinted length, and above 16
+    rows ceil(hint / 16) row segments per fragment computed on the device (CRC cut from the end, SUM from
+    the start; split fragments XORed / added into a zeroed out), items past a fragment's last segment
+    skipped -- the edge lengths x alignments with random registers at hints 3, 17, 33 and 49, then
+    random fragments of up to ~300 KB (one to five segments) at hint 70, every fragment against the
+    oracle."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(4242 + mode)
+    base = torch.empty(8 << 20, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=25)
+    host = base.cpu().numpy()
+    lens, offs = [], []
+    for L in EDGE_LENS + [70001, 131072, 200003]:
+        for a in range(0, 17, 4):
+            lens.append(L)
+            offs.append(int(rng.integers(0, (8 << 20) - 210000)) // 64 * 64 + a)
+    lens = np.array(lens, dtype=np.uint64)
+    offs = np.array(offs, dtype=np.uint64)
+    parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
+    descs = dv.make_descs(base, offs, lens, parts)
+    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
+    for hint in (3, 17, 33, 49):
+        got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, rows_hint=hint))
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (hint, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
+    n = 3000
+    lens = rng.integers(0, 300000, size=n).astype(np.uint64)
+    offs = rng.integers(0, (8 << 20) - 300001, size=n).astype(np.uint64)
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    descs = dv.make_descs(base, offs, lens, parts)
+    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
+    out = torch.full((n,), -1, dtype=torch.int32, device=cuda)  # (the launcher zeroes it)
+    got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, out=out, rows_hint=70))
+    assert np.array_equal(got, want)
+
+
+def test_descriptor_batch_row_segments_large(cuda, oracle):
+    """The hint at the sizes it is for: 1 GiB of GM's 65,456-byte fragments (hint 16: workgroups of 6
+    fragments) and of 4 MiB fragments (hint 1024: 64 segments of 16 rows each) and one 2^32 - 1-byte
+    fragment among neighbours (hint 4095: 256 segments of 4,096 rows, shifts past a million rows),
+    against lampi_msg_csum / the plain batch over the same bytes and an oracle sample; both modes."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(77)
+    buf = torch.empty(1 << 30, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=19)
+    for L, hint in ((65456, 16), (4 << 20, 1024)):
+        n = (1 << 30) // L
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+        descs = dv.make_descs(buf, offs, np.full(n, L, np.uint64))
+        idx = rng.choice(n, size=min(n, 12), replace=False)
+        host = buf[:n * L].cpu().numpy()
+        for mode in (dv.CRC32, dv.SUM32):
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, rows_hint=hint))
+            assert np.array_equal(got, dv.as_u32(dv.msg_csum(buf[:n * L], L, mode=mode))), (L, mode)
+            ref = oracle.desc_batch(host, offs[idx], np.full(idx.size, L, np.uint64),
+                                    np.full(idx.size, 0xFFFFFFFF, np.uint32) if mode == dv.CRC32 else None, mode)
+            assert np.array_equal(got[idx], ref), (L, mode)
+    del buf
+    torch.cuda.empty_cache()
+    L = 2**32 - 1
+    base = torch.empty(L + 4096, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=123)
+    descs = dv.make_descs(base, np.array([17, 0, 5], np.uint64), np.array([L, 0, 999], np.uint64),
+                          np.array([0xFFFFFFFF, 7, 0x1234], np.uint64))
+    for mode in (dv.CRC32, dv.SUM32):
+        want = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
+        got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, rows_hint=4095))
+        assert np.array_equal(got, want), mode
+    del base
+    torch.cuda.empty_cache()
+
+
 def test_descriptor_batch_two_buffers(cuda, oracle):
     """Fragments from two buffers more than 2 GiB apart, interleaved in runs so workgroups hold both,
     with lengths at the 64-byte-piece edges that round 3's packed-row experiment (crc_list_kernel,

@@ -1,7 +1,8 @@
 """Descriptor batches of large uniform fragments (lampi_frag_csum_batch), on the default count split and
 with LAMPI_CSUM_BY_BYTES (below 32,768 descriptors: plan_kernel + the piece streams over segments).
 Reports the fraction of the 8 TB/s HBM-read roofline per shape and checks every batch against
-lampi_msg_csum over the same bytes (an independent kernel).
+lampi_msg_csum over the same bytes (an independent kernel).  "rows": LAMPI_CSUM_ROWS_HINT(R), R the
+fragments' row count (row segments computed on the device).
 python tools/microbench/bigdesc_scan.py [crc|sum]"""
 import os
 import sys
@@ -38,9 +39,12 @@ for total, L in ((1 << 30, 65456), (1 << 30, 65536), (1 << 30, 262144), (1 << 30
     d = dv.make_descs(buf, np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, np.uint64))
     out = torch.empty(n, dtype=torch.int32, device="cuda")
     ref = dv.msg_csum(buf[:n * L], L, mode=mode)
-    for by_bytes in (False, True):
-        t = timed(lambda: dv.frag_csum_batch(d, n=n, out=out, mode=mode, by_bytes=by_bytes))
+    R = (L + 4095) // 4096
+    for split, by_bytes, hint in (("count   ", False, 0), ("by_bytes", True, 0), ("rows    ", False, min(R, 4095))):
+        if split.startswith("rows") and R < 2:
+            continue
+        t = timed(lambda: dv.frag_csum_batch(d, n=n, out=out, mode=mode, by_bytes=by_bytes, rows_hint=hint))
         ok = bool(torch.equal(out, ref))
-        print(f"{'crc' if mode == dv.CRC32 else 'sum'} {'by_bytes' if by_bytes else 'count   '} descriptors L={L:8d} "
+        print(f"{'crc' if mode == dv.CRC32 else 'sum'} {split} descriptors L={L:8d} "
               f"n={n:6d} {n * L / 2**20:8.1f} MiB {t * 1e6:9.2f} us  {n * L / t / 8e12:.3f} of 8 TB/s  "
               f"same_as_msg_csum={ok}", flush=True)
