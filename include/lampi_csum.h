@@ -59,7 +59,11 @@ enum lampi_csum_mode {
  * as r row groups in parallel, joined exactly afterwards (a second, small launch) -- the one-row-per-wave
  * shape of the message copy instead of one wave (SUM: one workgroup) walking every row.  Results are
  * identical for any lengths (a longer fragment gets longer groups); r = 0 or 1 is the default walk.
- * Both modes: GM payloads CRC 60 -> 71%, SUM 57 -> 72%; the receive step CRC 59 -> 69%, SUM 56 -> 72%. */
+ * Both modes: GM payloads CRC 60 -> 71%, SUM 57 -> 72%; the receive step CRC 59 -> 69%, SUM 56 -> 72%.
+ * Also accepted by lampi_frag_csum_batch[_strided] (read-only): workgroups are sized by the hinted
+ * length and fragments of more than 16 rows run as ceil(r / 16) row segments computed on the device
+ * (no plan launch; out is zeroed and the parts joined exactly) -- 1 GiB of 4 MiB descriptors CRC
+ * 34 -> 61%, GM payloads CRC 50 -> 62%, SUM 61 -> 75% (LAMPI_CSUM_BY_BYTES takes precedence). */
 #define LAMPI_CSUM_ROWS_HINT(r) ((int)(((unsigned)(r) & 0xFFFu) << 16))
 #define LAMPI_CSUM_ROWS_HINT_MASK LAMPI_CSUM_ROWS_HINT(0xFFFu)
 #define LAMPI_CSUM_ROWS_HINT_OF(mode) ((((unsigned)(mode)) >> 16) & 0xFFFu)
