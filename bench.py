@@ -115,6 +115,9 @@ def parse():
                     help="fused copy + checksum batch (lampi_frag_bcopy_batch) on the config B shape")
     ap.add_argument("--recv", action="store_true",
                     help="batched receive step (lampi_copy_to_app_batch) on the config B shape in GM slots")
+    ap.add_argument("--rows-hint", type=int, default=0,
+                    help="LAMPI_CSUM_ROWS_HINT(r) for the descriptor batches of --desc, --bcopy and --recv: the "
+                         "fragments' 4 KiB rows (e.g. 16 for GM's 65,456-byte payloads); 0 = none")
     ap.add_argument("--desc", action="store_true",
                     help="run the batch through descriptors (lampi_frag_csum_batch, the general kernel) "
                          "instead of the contiguous-message entry point (diagnostic)")
@@ -401,7 +404,7 @@ def run_device(args):
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         if args.desc:
             descs = dv.make_descs(buf, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint64))
-            run = lambda: dv.frag_csum_batch(descs, mode=mode, out=out)  # noqa: E731
+            run = lambda: dv.frag_csum_batch(descs, mode=mode, out=out, rows_hint=args.rows_hint)  # noqa: E731
         else:
             run = lambda: dv.msg_csum(buf, L, mode=mode, out=out)  # noqa: E731
         torch.cuda.synchronize()
@@ -516,6 +519,7 @@ def run_device(args):
             "config": {
                 "workload": workload,
                 "fragments_per_gpu": n, "frag_bytes": L, "bytes_per_gpu": n * L,
+                **({"rows_hint": args.rows_hint} if args.desc and args.rows_hint else {}),
                 "sharding": f"round-robin k = {'g' if args.shard is not None else 'rank'} (mod {kstep}), "
                             f"no collective",
             },
@@ -785,21 +789,21 @@ def run_bcopy(args):
     wall, kern = timed(lambda: dv.msg_bcopy(src, L, dst, L, mode=mode, out=out))
     parity = check("msg_bcopy")
     dst.zero_()
-    _, kern_desc = timed(lambda: dv.frag_bcopy_batch(descs, mode=mode, out=out))
+    _, kern_desc = timed(lambda: dv.frag_bcopy_batch(descs, mode=mode, out=out, rows_hint=args.rows_hint))
     parity_desc = check("frag_bcopy_batch")
     # the GM receive shape: payloads 8 bytes past a 16-byte boundary (after a 72-byte header),
     # destinations aligned -- n-1 fragments of src[8 + k*L, ...)
     descs8 = dv.make_copy_descs(src, offs[:-1] + np.uint64(8), dst, offs[:-1], np.full(n - 1, L), np.full(n - 1, L))
-    _, kern_desc8 = timed(lambda: dv.frag_bcopy_batch(descs8, n=n - 1, mode=mode, out=out))
+    _, kern_desc8 = timed(lambda: dv.frag_bcopy_batch(descs8, n=n - 1, mode=mode, out=out, rows_hint=args.rows_hint))
     copy8_ok = bool(torch.equal(src[8:8 + (n - 1) * L], dst[:(n - 1) * L]))
     # the GM send shape: payloads gathered into ring slots right after the 72-byte header --
     # destinations 8 bytes past a 16-byte boundary, sources aligned
     descs_d8 = dv.make_copy_descs(src, offs[:-1], dst, offs[:-1] + np.uint64(8), np.full(n - 1, L), np.full(n - 1, L))
-    _, kern_dst8 = timed(lambda: dv.frag_bcopy_batch(descs_d8, n=n - 1, mode=mode, out=out))
+    _, kern_dst8 = timed(lambda: dv.frag_bcopy_batch(descs_d8, n=n - 1, mode=mode, out=out, rows_hint=args.rows_hint))
     copyd8_ok = bool(torch.equal(src[:(n - 1) * L], dst[8:8 + (n - 1) * L]))
     # byte-misaligned destinations (dst + 1)
     descs_d1 = dv.make_copy_descs(src, offs[:-1], dst, offs[:-1] + np.uint64(1), np.full(n - 1, L), np.full(n - 1, L))
-    _, kern_dst1 = timed(lambda: dv.frag_bcopy_batch(descs_d1, n=n - 1, mode=mode, out=out))
+    _, kern_dst1 = timed(lambda: dv.frag_bcopy_batch(descs_d1, n=n - 1, mode=mode, out=out, rows_hint=args.rows_hint))
     copyd1_ok = bool(torch.equal(src[:(n - 1) * L], dst[1:1 + (n - 1) * L]))
     _, kern_copy = timed(lambda: dst.copy_(src))
     # GM's own send shape (gm/sendFrag.cc:147-155): 65,456-byte payloads of a 1 GiB message into
@@ -825,7 +829,7 @@ def run_bcopy(args):
         "data": f"synthetic: splitmix64 stream seed {args.seed} (SURVEY.md 8(d)), generated on device",
         "config": {"workload": f"{n} x {L} B fragments copied into a staging array with the "
                                f"{'CRC' if mode == dv.CRC32 else 'sum'} fused (lampi_msg_bcopy)",
-                   "fragments": n, "frag_bytes": L},
+                   "fragments": n, "frag_bytes": L, "rows_hint": args.rows_hint},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_bcopy_{n}x{L}"),
@@ -893,7 +897,8 @@ def run_recv(args):
     offs = np.arange(n, dtype=np.uint64)
     descs = dv.make_recv_descs(nic, offs * np.uint64(stride) + np.uint64(72), app, offs * np.uint64(L),
                                np.full(n, L), np.full(n, 1 << 40, dtype=np.int64))
-    run = lambda: dv.copy_to_app_batch(descs, nic, expected_stride=stride, expected_offset=64, n=n, mode=mode)  # noqa
+    run = lambda: dv.copy_to_app_batch(descs, nic, expected_stride=stride, expected_offset=64, n=n, mode=mode,  # noqa
+                                       rows_hint=args.rows_hint)
     for _ in range(args.warmup):
         res = run()
     torch.cuda.synchronize()
@@ -927,7 +932,7 @@ def run_recv(args):
         "config": {"workload": f"{n} x {L} B fragments, 72-byte gmHeaderData + payload slots (stride {stride}), "
                                f"{'CRC' if mode == dv.CRC32 else 'sum'} verified against dataChecksum, delivered "
                                "into one application buffer (lampi_copy_to_app_batch)", "fragments": n,
-                   "frag_bytes": L},
+                   "frag_bytes": L, "rows_hint": args.rows_hint},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}"),

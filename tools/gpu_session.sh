@@ -2,7 +2,7 @@
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
 #   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchCsum | benchD | bcopy |
-#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | e2e | recv | microbench
+#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | e2e | recv | gm | microbench
 # Any failure (a test failure, fault, abort, segfault, timeout or kill) ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -62,6 +62,12 @@ for step in "$@"; do
           run recvsum 600 python bench.py --recv --mode sum --steps 10 ;;
     bcopy) run bcopy 600 python bench.py --bcopy --steps 10 &&
            run bcopysum 600 python bench.py --bcopy --mode sum --steps 10 ;;
+    gm) for m in crc sum; do  # GM's 65,456-byte payloads, with and without LAMPI_CSUM_ROWS_HINT(16)
+          for h in 0 16; do
+            run gm_recv_${m}_h$h 600 python bench.py --recv --mode $m --frags 16384 --frag-bytes 65456 --rows-hint $h --steps 10 &&
+            run gm_desc_${m}_h$h 600 python bench.py --desc --mode $m --frags 16404 --frag-bytes 65456 --rows-hint $h --steps 10 --no-cpu-baseline
+          done
+        done ;;
     tests_bcopy) run pytest_bcopy 600 python -m pytest tests/test_gpu_bcopy.py -m gpu -x -q ;;
     tests_chain) run pytest_chain 600 python -m pytest tests/test_gpu_chain.py -m gpu -x -q ;;
     tests_csum64) run pytest_csum64 600 python -m pytest tests/test_gpu_csum64.py -m gpu -x -q ;;
