@@ -238,3 +238,24 @@ int main(void) {
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", inc, str(c_src), "-o", str(tmp_path / "cc")],
                    check=True)
     assert subprocess.run([str(tmp_path / "cc")]).returncode == 0
+
+
+def test_mode_flag_macros_match_the_binding(tmp_path):
+    """The header's mode flags (LAMPI_CSUM_BY_BYTES, LAMPI_CSUM_ROWS_HINT) as a C caller sees them equal
+    what the Python binding ORs into `mode`, and the hint field does not overlap the mode or BY_BYTES."""
+    from lampi_amd._lib import BY_BYTES, CRC32, SUM32, rows_hint_bits
+
+    prog = tmp_path / "flags.c"
+    prog.write_text('#include "lampi_csum.h"\n#include <stdio.h>\n'
+                    'int main(void) { printf("%d %d %u %u %u\\n", LAMPI_CSUM_BY_BYTES, LAMPI_CSUM_ROWS_HINT(16), '
+                    'LAMPI_CSUM_ROWS_HINT_OF(LAMPI_CSUM_ROWS_HINT(4095) | LAMPI_CSUM_BY_BYTES | 1), '
+                    '(unsigned)LAMPI_CSUM_ROWS_HINT_MASK, LAMPI_CSUM_ROWS_HINT_OF(-1)); return 0; }\n')
+    exe = tmp_path / "flags"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.dirname(HEADER), str(prog), "-o", str(exe)],
+                   check=True)
+    by_bytes, hint16, back, mask, of_all = (int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                                           text=True).stdout.split())
+    assert by_bytes == BY_BYTES and hint16 == rows_hint_bits(16) and back == 4095
+    assert mask & (BY_BYTES | CRC32 | SUM32) == 0 and of_all == 4095
+    with pytest.raises(ValueError):
+        rows_hint_bits(4096)
