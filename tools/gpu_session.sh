@@ -64,8 +64,8 @@ for step in "$@"; do
            run bcopysum 600 python bench.py --bcopy --mode sum --steps 10 ;;
     gm) for m in crc sum; do  # GM's 65,456-byte payloads, with and without LAMPI_CSUM_ROWS_HINT(16)
           for h in 0 16; do
-            run gm_recv_${m}_h$h 600 python bench.py --recv --mode $m --frags 16384 --frag-bytes 65456 --rows-hint $h --steps 10 &&
-            run gm_desc_${m}_h$h 600 python bench.py --desc --mode $m --frags 16404 --frag-bytes 65456 --rows-hint $h --steps 10 --no-cpu-baseline
+            run gm_recv_${m}_h$h 600 python bench.py --recv --mode $m --frags 16384 --frag-bytes 65456 --rows-hint $h --steps 20 --warmup 60 &&
+            run gm_desc_${m}_h$h 600 python bench.py --desc --mode $m --frags 16404 --frag-bytes 65456 --rows-hint $h --steps 20 --warmup 60 --no-cpu-baseline
           done
         done ;;
     tests_bcopy) run pytest_bcopy 600 python -m pytest tests/test_gpu_bcopy.py -m gpu -x -q ;;
