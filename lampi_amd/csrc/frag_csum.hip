@@ -2324,6 +2324,11 @@ __device__ __forceinline__ u32x4 shl_bytes16(const u32x4 &v, uint32_t s) {
 // message copy -- and leaves the groups' values (each from a zero register, the first with the fragment's
 // register in it, the lane tree at the group's last row) in groups[f*W + g]; crc_light_group_join_kernel
 // shifts each past the fragment's later rows, XORs them and emits.  A fragment of one group emits here.
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
+
 template <class Src>
 __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src, size_t n,
                                                                   const uint32_t *__restrict__ img,
@@ -2345,7 +2350,10 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     FragInfo fi{nullptr, 0u, 0u, nullptr, 0u};
     if (live) fi = src.get(f);
     const uint32_t L = fi.len, R = (uint32_t)(((uint64_t)L + kRowBytes - 1) / kRowBytes);
-    const uint32_t P = R * (uint32_t)kRowBytes - L;  // (L < 2^32 - 16: no overflow)
+    // fragments of at most 2 KiB take a half frame: chunks q = 0, 1 of the row (its first 2 KiB), half the
+    // lookups of a 4 KiB frame (IB's 1,976-byte payloads were 52% padding)
+    const bool half = R == 1u && L <= (uint32_t)kRowBytes / 2u;
+    const uint32_t P = (half ? (uint32_t)kRowBytes / 2u : R * (uint32_t)kRowBytes) - L;  // (L < 2^32 - 16)
     // this wave's rows [r0, r1) (all of them for W == 1); a group past the last row has nothing to do
     const uint32_t k = W > 1 ? (R + W - 1) / W : R;
     const uint32_t r0 = W > 1 ? min(g * k, R) : 0u, r1 = W > 1 ? min(r0 + k, R) : R;
@@ -2354,17 +2362,18 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     const __amdgpu_buffer_rsrc_t srs = light_rsrc((const void *)fi.addr, L);
     const __amdgpu_buffer_rsrc_t drs = light_rsrc(fi.dst, fi.copylen);
     // (ok false: offsets aimed out of range, no memory traffic -- a prefetch past the last row)
-    auto load_row = [&](uint32_t r, bool ok, u32x4 (&d)[4], uint32_t (&o)[4]) {
+    // (hf: a half frame's row, chunks q = 0, 1 only)
+    auto load_row = [&](uint32_t r, bool ok, u32x4 (&d)[4], uint32_t (&o)[4], bool hf = false) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            o[q] = ok ? r * (uint32_t)kRowBytes + 1024u * q + 16u * lane - P : 0xFFFFFFF0u;
+            o[q] = (ok && (!hf || q < 2)) ? r * (uint32_t)kRowBytes + 1024u * q + 16u * lane - P : 0xFFFFFFF0u;
             asm volatile("" : "+v"(o[q]));  // whole offsets: padding offsets wrap to huge values, out of range
             d[q] = __builtin_amdgcn_raw_buffer_load_b128(srs, o[q], 0, kBufNt);
         }
     };
     u32x4 d[4];
     uint32_t o[4];
-    load_row(r0, live, d, o);  // (an empty or dead wave's descriptor reads nothing but zeros)
+    load_row(r0, live, d, o, half);  // (an empty or dead wave's descriptor reads nothing but zeros)
     // the fragment's first 16 bytes, for the chunk its start cuts (a load here rather than under that
     // branch: the compiler's merged waits after a branch with a load drained every row's prefetch)
     const u32x4 head = __builtin_amdgcn_raw_buffer_load_b128(srs, 0u, 0, 0);
@@ -2396,7 +2405,9 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     const uint32_t kP = P >> 4, sP = P & 15u;   // the chunk holding the fragment's first byte, and where
     const uint64_t cend = (uint64_t)fi.copylen + P;  // the copy's end in the frame
     uint32_t acc = 0;
-    auto step = [&](uint32_t r, u32x4 (&dc)[4], const uint32_t (&oc)[4], u32x4 (&dn)[4], uint32_t (&on)[4]) {
+    // (hf: BoolC<true> for a half frame -- its own copy of the body, kept out of the row loop)
+    auto step = [&](auto hf, uint32_t r, u32x4 (&dc)[4], const uint32_t (&oc)[4], u32x4 (&dn)[4],
+                    uint32_t (&on)[4]) {
         load_row(r + 1, r + 1 < r1, dn, on);
         if (r == 0 && sP != 0) {  // the chunk cut by the fragment's start: [zeros | first 16 - sP bytes]
             const u32x4 v = shl_bytes16(head, sP);
@@ -2445,10 +2456,14 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
         }
         const uint32_t c0 = light_chunk(lds, lanec2, sel, dc[0]);
         const uint32_t c1 = light_chunk(lds, lanec2, sel, dc[1]);
-        const uint32_t c2 = light_chunk(lds, lanec2, sel, dc[2]);
-        const uint32_t c3 = light_chunk(lds, lanec2, sel, dc[3]);
-        const uint32_t v0 = r == r0 ? c0 : light_shift<0>(lds, acc) ^ c0;
-        acc = light_shift<0>(lds, light_shift<0>(lds, light_shift<0>(lds, v0) ^ c1) ^ c2) ^ c3;
+        if constexpr (decltype(hf)::value) {  // (one row: r == r0 == 0; chunks 2, 3 lie past the frame)
+            acc = light_shift<0>(lds, c0) ^ c1;
+        } else {
+            const uint32_t c2 = light_chunk(lds, lanec2, sel, dc[2]);
+            const uint32_t c3 = light_chunk(lds, lanec2, sel, dc[3]);
+            const uint32_t v0 = r == r0 ? c0 : light_shift<0>(lds, acc) ^ c0;
+            acc = light_shift<0>(lds, light_shift<0>(lds, light_shift<0>(lds, v0) ^ c1) ^ c2) ^ c3;
+        }
         if (r + 1 == r1) {
             uint32_t v = acc;
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<1>(lds, v), 0x111, 0xF, 0xF, false);
@@ -2469,10 +2484,14 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     };
     u32x4 d2[4];
     uint32_t o2[4];
+    if (half) {
+        step(BoolC<true>{}, 0u, d, o, d2, o2);
+        return;
+    }
     for (uint32_t r = r0; r < r1; r += 2) {
-        step(r, d, o, d2, o2);
+        step(BoolC<false>{}, r, d, o, d2, o2);
         if (r + 1 >= r1) break;
-        step(r + 1, d2, o2, d, o);
+        step(BoolC<false>{}, r + 1, d2, o2, d, o);
     }
 }
 

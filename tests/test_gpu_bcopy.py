@@ -14,8 +14,10 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-EDGE_LENS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 63, 64, 65, 127, 1023, 1024, 1025, 1976, 4092, 4095, 4096, 4097,
-             4098, 4099, 4111, 4113, 8191, 8192, 8193, 8194, 12289, 16384, 16385, 65455, 65456]
+EDGE_LENS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 63, 64, 65, 127, 1023, 1024, 1025, 1976, 2031, 2047, 2048, 2049,
+             4092, 4095, 4096, 4097, 4098, 4099, 4111, 4113, 8191, 8192, 8193, 8194, 12289, 16384, 16385, 65455,
+             65456]
+# (16-2048: the CRC copy's half frame -- 2 KiB, two chunks per lane; 2049 the first full-frame length)
 # (4097-4099, 8193, 8194, 12289: a 4 KiB frame's padding leaves the fragment's first bytes -- and the
 # register injected there -- in the last chunk of a row, spilling into the next row's first chunk)
 

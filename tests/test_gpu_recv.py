@@ -134,7 +134,7 @@ def test_copy_to_app_edges(cuda, oracle, mode):
     """Zero-length fragments, AppBufferLen <= 0 / == 1 / == length - 1 / == length / > length,
     lengths around the 64-byte piece and 4 KiB row edges, corrupt and clean."""
     rng = np.random.default_rng(7 + mode)
-    L = [0, 1, 3, 4, 5, 63, 64, 65, 1975, 1976, 4095, 4096, 4097, 8192, 65455, 65456, 65536]
+    L = [0, 1, 3, 4, 5, 63, 64, 65, 1975, 1976, 2047, 2048, 2049, 4095, 4096, 4097, 8192, 65455, 65456, 65536]
     lengths, app_len = [], []
     for ln in L:
         for a in sorted({-1, 0, 1, ln - 1, ln, ln + 1, 1 << 33}):
@@ -150,7 +150,7 @@ def test_copy_to_app_row_groups(cuda, oracle, rows_hint, mode):
     before the verdict -- the edge cases (AppBufferLen <= 0 .. > length, corrupt and clean), then GM-sized
     payloads and longer ones (groups of several rows), every copy, checksum and verdict vs the oracle."""
     rng = np.random.default_rng(31 + rows_hint)
-    L = [0, 1, 3, 4, 5, 63, 64, 65, 1975, 1976, 4095, 4096, 4097, 8192, 65455, 65456, 65536, 200003]
+    L = [0, 1, 3, 4, 5, 63, 64, 65, 1975, 1976, 2047, 2048, 2049, 4095, 4096, 4097, 8192, 65455, 65456, 65536, 200003]
     lengths, app_len = [], []
     for ln in L:
         for a in sorted({-1, 0, 1, ln - 1, ln, ln + 1, 1 << 33}):
