@@ -493,6 +493,12 @@ def run_device(args):
         cfg_key = f"{'crc' if crc else 'sum'}_{'desc_' if args.desc else ''}{n}x{L}"
         traffic = None if args.dry_run else read_traffic(cfg_key)
         kernel = ("none (dry run)" if args.dry_run else
+                  "crc_light_frag_copy_kernel<DescSource> (read-only, row groups + crc_light_group_join_kernel)"
+                  if args.desc and crc and args.rows_hint >= 8 else
+                  "crc_stream_kernel<RowSegSource> (descriptors, 16-row segments)"
+                  if args.desc and crc and args.rows_hint > 1 else
+                  "crc_stream_kernel<RowSegSource, kSum> (descriptors, 16-row segments)"
+                  if args.desc and args.rows_hint > 16 else
                   "crc_stream_kernel (descriptors)" if args.desc and crc else
                   "crc_stream_kernel<kSum> (descriptors)" if args.desc else
                   "crc_regular_kernel" if crc else "crc_regular_kernel (kSum: uicsum on the same schedule)")
@@ -500,7 +506,7 @@ def run_device(args):
                     if args.shard is not None else
                     f"{n} x {L} B fragments per GPU, device-resident, "
                     f"{'CRC-32/MPEG-2 (uicrc)' if crc else 'uicsum'}, "
-                    f"{'one descriptor per fragment (piece streams)' if args.desc else 'uniform fragments (regular kernel schedule)'}")
+                    f"{('one descriptor per fragment, LAMPI_CSUM_ROWS_HINT(%d)' % args.rows_hint) if args.desc and args.rows_hint > 1 else 'one descriptor per fragment (piece streams)' if args.desc else 'uniform fragments (regular kernel schedule)'}")
         result = {
             "metric": METRIC,
             "value": round(value, 2),

@@ -60,10 +60,11 @@ enum lampi_csum_mode {
  * shape of the message copy instead of one wave (SUM: one workgroup) walking every row.  Results are
  * identical for any lengths (a longer fragment gets longer groups); r = 0 or 1 is the default walk.
  * Both modes: GM payloads CRC 60 -> 71%, SUM 57 -> 72%; the receive step CRC 59 -> 69%, SUM 56 -> 72%.
- * Also accepted by lampi_frag_csum_batch[_strided] (read-only): workgroups are sized by the hinted
- * length and fragments of more than 16 rows run as ceil(r / 16) row segments computed on the device
- * (no plan launch; out is zeroed and the parts joined exactly) -- 1 GiB of 4 MiB descriptors CRC
- * 34 -> 61%, GM payloads CRC 50 -> 62%, SUM 61 -> 75% (LAMPI_CSUM_BY_BYTES takes precedence). */
+ * Also accepted by lampi_frag_csum_batch[_strided] (read-only; LAMPI_CSUM_BY_BYTES first): CRC with
+ * r >= 8 walks each fragment's rows in one wave of the table-light kernel (above 16 rows, one wave per
+ * 8 rows, joined exactly) -- 1 GiB of GM payloads CRC 56 -> 80%, of 1 MiB / 4 MiB descriptors 57 / 34
+ * -> 80%; smaller r and SUM size workgroups by the hinted length and cut fragments of more than 16
+ * rows into 16-row segments on the device (out zeroed, parts joined exactly): SUM 61 -> 74%. */
 #define LAMPI_CSUM_ROWS_HINT(r) ((int)(((unsigned)(r) & 0xFFFu) << 16))
 #define LAMPI_CSUM_ROWS_HINT_MASK LAMPI_CSUM_ROWS_HINT(0xFFFu)
 #define LAMPI_CSUM_ROWS_HINT_OF(mode) ((((unsigned)(mode)) >> 16) & 0xFFFu)

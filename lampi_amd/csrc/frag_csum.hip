@@ -2388,7 +2388,8 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
             for (uint32_t i = 0; i < L; ++i) C = (C >> 8) ^ lds[((C ^ fi.addr[i]) & 255u) * 32u + 24u];
             emit(src, out, f, __builtin_bswap32(C), fi);
         }
-        if (lane < fi.copylen) fi.dst[lane] = fi.addr[lane];
+        if constexpr (Src::kCopy)
+            if (lane < fi.copylen) fi.dst[lane] = fi.addr[lane];
         return;
     }
     const uint32_t c8 = (lane & 7u) * 8u;
@@ -2422,11 +2423,13 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
         for (int q = 0; q < 4; ++q) {
             const uint64_t x = rbase + 1024u * q;
             const bool whole = x >= P && x + 16u <= cend;
-            __builtin_amdgcn_raw_buffer_store_b128(dc[q], drs, whole ? oc[q] : 0xFFFFFFF0u, 0, kBufNt);
+            if constexpr (Src::kCopy)
+                __builtin_amdgcn_raw_buffer_store_b128(dc[q], drs, whole ? oc[q] : 0xFFFFFFF0u, 0, kBufNt);
         }
         // chunks cut by the copy's start or end (at most two per fragment): byte stores
         const uint64_t row0 = (uint64_t)r * kRowBytes;
-        if ((r == 0 && sP != 0) || (cend > row0 && cend < row0 + kRowBytes && (cend & 15u) != 0)) {
+        if (Src::kCopy &&
+            ((r == 0 && sP != 0) || (cend > row0 && cend < row0 + kRowBytes && (cend & 15u) != 0))) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint64_t x = rbase + 1024u * q;
@@ -2496,23 +2499,27 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
 }
 
 // The fragments of more than one row group: value = XOR over the groups of group g shifted past the rows
-// after it (normal domain, constant products), then emit (receive sources: the verdict).  One thread per
-// fragment.
+// after it (normal domain, constant products), then emit (receive sources: the verdict).  G = min(64,
+// pow2 >= W) lanes per fragment, lane j taking groups j, j + G, ... (each shift independent of the
+// others: one thread walking 64 groups by Horner waited on 64 dependent rounds, ~25 us for 4 MiB
+// fragments of 16-row groups; a whole wave per fragment of 4 groups cost 16 KiB copies 4 points).
 template <class Src>
-__global__ void __launch_bounds__(256) crc_light_group_join_kernel(const Src src, size_t n, uint32_t W,
+__global__ void __launch_bounds__(256) crc_light_group_join_kernel(const Src src, size_t n, uint32_t W, uint32_t G,
                                                                    const uint32_t *__restrict__ groups,
                                                                    uint32_t *__restrict__ out) {
-    const size_t f = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (f >= n) return;
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x, f = i / G;
+    const uint32_t j = (uint32_t)(i & (G - 1u));
+    if (f >= n) return;  // (the G lanes of a fragment leave or stay together)
     const FragInfo fi = src.get(f);
     const uint32_t R = (uint32_t)(((uint64_t)fi.len + kRowBytes - 1) / kRowBytes);
     if (fi.len < 16u || R <= 1u) return;  // (emitted by its only wave)
     const uint32_t k = (R + W - 1) / W, ng = (R + k - 1) / k;
     if (ng <= 1u) return;
     const uint32_t *p = groups + f * W;
-    uint32_t acc = p[0];
-    for (uint32_t g = 1; g < ng; ++g) acc = shift_rows(acc, min(k, R - g * k)) ^ p[g];
-    emit(src, out, f, acc, fi);
+    uint32_t acc = 0;
+    for (uint32_t g = j; g < ng; g += G) acc ^= shift_rows(p[g], R - min((g + 1u) * k, R));
+    for (uint32_t o = G >> 1; o >= 1u; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, (int)o);
+    if (j == 0) emit(src, out, f, acc, fi);
 }
 
 // W: row groups per fragment (1: one wave walks all the fragment's rows)
@@ -2533,8 +2540,10 @@ static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uin
                        out, W, groups);
     e = hipGetLastError();
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(crc_light_group_join_kernel<Src>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, n,
-                           W, groups, out);
+        uint32_t G = 1;
+        while (G < W && G < 64u) G <<= 1;
+        hipLaunchKernelGGL(crc_light_group_join_kernel<Src>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, s, src,
+                           n, W, G, groups, out);
         e = hipGetLastError();
     }
     return scratch_done(s, groups, pooled, e);
@@ -3842,7 +3851,12 @@ static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *o
 // not 48), and fragments longer than kSegRows rows run as W = ceil(r / kSegRows) row segments each
 // (RowSegSource, out zeroed first: split fragments accumulate into it) -- segments of ~64 KiB, so the
 // per-segment join (a constant-product shift past the later rows) stays small against its rows.
+#ifndef LAMPI_LDR
+#define LAMPI_LDR 8
+#endif
 constexpr uint32_t kSegRows = 16;
+constexpr uint32_t kLightDescRows = LAMPI_LDR;
+constexpr uint32_t kLightRoRows = 8;
 template <bool kSum, int kWv, int kCap>
 static hipError_t launch_row_segments(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
                                       hipStream_t s, uint32_t rows_hint) {
@@ -3868,6 +3882,9 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
+    if (rows_hint >= kLightDescRows)  // one wave per kSegRows rows of a fragment, read-only
+        return launch_crc_light_frag_copy(DescSource{d}, n, img, out, s,
+                                          rows_hint <= kSegRows ? 1u : (rows_hint + kLightRoRows - 1) / kLightRoRows);
     if (rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<false, kStreamWv, kStreamCap>(d, n, out, img, s, rows_hint);
     const uint32_t fpg = frags_per_wg(n);

@@ -33,6 +33,10 @@ CASES = [
     (2, 1048576, 16384, 0, (1,)),          # --frags 1048576 --frag-bytes 16384
     (2, 1048576, 16384, 1, (1,)),
     (1, 1048576, 1024, 0, (1,)),           # config A shape
+    (2, 16404, 65456, 0, (1,)),            # --desc: GM's payloads (--rows-hint 16), 1 GiB
+    (2, 16404, 65456, 1, (1,)),
+    (2, 1024, 1048576, 0, (1,)),           # --desc --rows-hint 256 / 1024: 1 MiB and 4 MiB fragments
+    (2, 256, 4194304, 0, (1,)),
 ]
 # config D per-GPU shards: (seed, n_total, L, mode, nshard)
 SHARD_CASES = [(3, 33554432, 16384, 0, 8), (3, 33554432, 16384, 1, 8)]

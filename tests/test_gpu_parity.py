@@ -332,9 +332,10 @@ def test_descriptor_batch_row_segments(cuda, oracle, mode):
     """LAMPI_CSUM_ROWS_HINT on lampi_frag_csum_batch: workgroups sized by the hinted length, and above 16
     rows ceil(hint / 16) row segments per fragment computed on the device (CRC cut from the end, SUM from
     the start; split fragments XORed / added into a zeroed out), items past a fragment's last segment
-    skipped -- the edge lengths x alignments with random registers at hints 3, 17, 33 and 49, then
-    random fragments of up to ~300 KB (one to five segments) at hint 70, every fragment against the
-    oracle."""
+    skipped; CRC from hint 8 on: the read-only table-light kernel, one wave per 8 rows (up to 16 rows:
+    one wave per fragment, however long), groups joined by crc_light_group_join_kernel -- the edge
+    lengths x alignments with random registers at hints 3, 8, 12, 17, 33 and 49, then random fragments
+    of up to ~300 KB at hint 70, every fragment against the oracle."""
     import torch
 
     dv = _dv()
@@ -352,7 +353,7 @@ def test_descriptor_batch_row_segments(cuda, oracle, mode):
     parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
     descs = dv.make_descs(base, offs, lens, parts)
     want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
-    for hint in (3, 17, 33, 49):
+    for hint in (3, 8, 12, 17, 33, 49):
         got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, rows_hint=hint))
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (hint, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
@@ -369,8 +370,9 @@ def test_descriptor_batch_row_segments(cuda, oracle, mode):
 
 def test_descriptor_batch_row_segments_large(cuda, oracle):
     """The hint at the sizes it is for: 1 GiB of GM's 65,456-byte fragments (hint 16: workgroups of 6
-    fragments) and of 4 MiB fragments (hint 1024: 64 segments of 16 rows each) and one 2^32 - 1-byte
-    fragment among neighbours (hint 4095: 256 segments of 4,096 rows, shifts past a million rows),
+    fragments) and of 4 MiB fragments (hint 1024: 64 segments of 16 rows each; CRC 128 groups of 8)
+    and one 2^32 - 1-byte fragment among neighbours (hint 4095: 256 segments of 4,096 rows, CRC 512
+    groups of 2,048; shifts past a million rows),
     against lampi_msg_csum / the plain batch over the same bytes and an oracle sample; both modes."""
     import torch
 

@@ -2,7 +2,7 @@
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
 #   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchCsum | benchD | bcopy |
-#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | e2e | recv | gm | microbench
+#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | e2e | recv | gm | bigdesc | microbench
 # Any failure (a test failure, fault, abort, segfault, timeout or kill) ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -68,6 +68,14 @@ for step in "$@"; do
             run gm_desc_${m}_h$h 600 python bench.py --desc --mode $m --frags 16404 --frag-bytes 65456 --rows-hint $h --steps 20 --warmup 60 --no-cpu-baseline
           done
         done ;;
+    bigdesc) for spec in 16404:65456:16 1024:1048576:256 256:4194304:1024; do  # read-only, LAMPI_CSUM_ROWS_HINT
+               IFS=: read -r nf fb h <<< "$spec"
+               run desc_${fb}_h$h 600 python bench.py --desc --frags $nf --frag-bytes $fb --rows-hint $h --steps 20 --warmup 60 --no-cpu-baseline
+             done &&
+             run prof_desc_gm 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_desc_gm -o run \
+               -- python3 bench.py --desc --frags 16404 --frag-bytes 65456 --rows-hint 16 --steps 20 --warmup 60 --no-cpu-baseline &&
+             run pmc_desc_gm_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_desc_gm_fetch -o run \
+               -- python3 bench.py --desc --frags 16404 --frag-bytes 65456 --rows-hint 16 --steps 5 --warmup 1 --no-cpu-baseline ;;
     tests_bcopy) run pytest_bcopy 600 python -m pytest tests/test_gpu_bcopy.py -m gpu -x -q ;;
     tests_chain) run pytest_chain 600 python -m pytest tests/test_gpu_chain.py -m gpu -x -q ;;
     tests_csum64) run pytest_csum64 600 python -m pytest tests/test_gpu_csum64.py -m gpu -x -q ;;
