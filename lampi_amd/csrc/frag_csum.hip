@@ -2526,6 +2526,7 @@ __global__ void __launch_bounds__(256) crc_light_group_join_kernel(const Src src
 template <class Src>
 static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
                                              hipStream_t s, uint32_t W = 1) {
+    W = min(W, 4096u);  // (the join: at most 64 groups per lane)
     while (W > 1 && (size_t)n * W > ((size_t)1 << 26)) W >>= 1;  // (grid: items * 64 threads < 2^32)
     if (W <= 1) {
         hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
@@ -3851,6 +3852,9 @@ static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *o
 // not 48), and fragments longer than kSegRows rows run as W = ceil(r / kSegRows) row segments each
 // (RowSegSource, out zeroed first: split fragments accumulate into it) -- segments of ~64 KiB, so the
 // per-segment join (a constant-product shift past the later rows) stays small against its rows.
+#ifndef LAMPI_MSG_LIGHT
+#define LAMPI_MSG_LIGHT 1
+#endif
 #ifndef LAMPI_LDR
 #define LAMPI_LDR 8
 #endif
@@ -3936,6 +3940,16 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
+    // the read-only table-light kernel (tools/microbench/msg_light.py, profiles/r03/msg_light_ab.txt):
+    // fragments of 8-16 rows (GM's 65,456-byte payloads, 64 KiB) one wave each -- 4 GiB of 64 KiB
+    // fragments 67.7 -> 78.4%, of 65,456 B 76.9 -> 78.3% -- and longer ones in messages up to 2 GiB
+    // (crc_light_msg) as 8-row groups: 1 GiB of 1 MiB fragments 40% on the regular kernel, whose
+    // chains are fragments; larger messages keep the framed regular kernel (131,056 B at 4 GiB
+    // 76.8% against 75.7%)
+    const size_t R = (frag_len + kRowBytes - 1) / kRowBytes;
+    if (LAMPI_MSG_LIGHT && crc_light_msg(frag_len, msg_len))
+        return launch_crc_light_frag_copy(MsgSource{base, msg_len, frag_len, partial}, n, img, out, s,
+                                          R <= kSegRows ? 1u : (uint32_t)((R + kLightRoRows - 1) / kLightRoRows));
     if (frame_ok(base, msg_len, frag_len, n)) return launch_crc_frames(base, msg_len, frag_len, partial, n, out, img, s);
     const uint32_t fpg = frags_per_wg(n, frag_len);
     hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,

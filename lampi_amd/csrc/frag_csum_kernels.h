@@ -18,6 +18,13 @@ inline bool regular_msg_frag(size_t frag_len, bool sum) {
     return sum ? (frag_len <= (32u << 10) || frag_len > (64u << 10)) : frag_len != (64u << 10);
 }
 
+// CRC messages whose fragments run on the read-only table-light kernel (launch_crc_msg): 8-16 rows,
+// or longer in messages of at most 2 GiB (row groups; the regular kernel keeps the larger ones)
+inline bool crc_light_msg(size_t frag_len, size_t msg_len) {
+    const size_t rows = (frag_len + 4095) / 4096;
+    return rows >= 8 && (rows <= 16 || (msg_len <= ((size_t)1 << 31) && rows < ((size_t)1 << 32)));
+}
+
 // Workgroups for the persistent CRC kernel on `device` (one 1024-thread WG per CU).
 int crc_grid(int device);
 

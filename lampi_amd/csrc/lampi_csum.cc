@@ -72,7 +72,8 @@ hipError_t launch_msg_csum(const uint8_t *base, size_t msg_len, size_t frag_len,
     const int grid = crc_grid(dev);
     if (mode == LAMPI_CSUM_SUM32) return launch_sum_msg(base, msg_len, frag_len, n, out, img, grid, s);
     const bool regular = msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 &&
-                         regular_msg_frag(frag_len, false) && ((uintptr_t)base & 15u) == 0;
+                         regular_msg_frag(frag_len, false) && ((uintptr_t)base & 15u) == 0 &&
+                         !crc_light_msg(frag_len, msg_len);
     if (regular) return launch_crc_regular(base, n, frag_len, partial, out, img, grid, s);
     return launch_crc_msg(base, msg_len, frag_len, partial, n, out, img, grid, s);
 }

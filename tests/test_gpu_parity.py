@@ -97,11 +97,15 @@ def test_message_with_short_last_fragment(cuda, oracle, mode):
     ((16384 + 1008) * 333, 16384 + 1008),  # P = 3088: lane 48, chunk 1
     ((12288 * 2 + 16) * 97 + 12288 * 2, 12288 * 2 + 16),  # last fragment exactly 6 rows
     ((40000 // 16 * 16) * 777 + 4096, 40000 // 16 * 16),
+    ((1 << 20) * 6, 1 << 20),                 # whole-row fragments, 256 rows: 32 groups of 8 rows
+    ((1 << 20) * 3 + 4096 * 5 + 7, 1 << 20),  # ... and a last fragment of 5 rows + 7 bytes
+    ((131072 - 16) * 40 + 999, 131072 - 16),  # 32 rows, P = 16: 4 groups, the register in group 0
 ])
 def test_message_large_ragged_fragments(cuda, oracle, msg_len, L):
-    """lampi_msg_csum CRC of messages of large fragments that are not whole 4 KiB rows (GM payloads,
-    257-row fragments, registers landing in every lane and chunk position of a 4 KiB frame, last
-    fragments of a few rows or exactly whole rows), every fragment vs the oracle, two registers."""
+    """lampi_msg_csum CRC of messages of large fragments (GM payloads, 257-row fragments, registers
+    landing in every lane and chunk position of a 4 KiB frame, last fragments of a few rows or exactly
+    whole rows; from 8 rows the read-only table-light kernel, above 16 rows as 8-row groups joined),
+    every fragment vs the oracle, two registers."""
     import torch
 
     dv = _dv()
@@ -120,15 +124,18 @@ def test_message_large_ragged_fragments(cuda, oracle, msg_len, L):
 
 
 @pytest.mark.parametrize("msg_len,L", [
-    (65456 * 4102 + 1280, 65456),           # GM payloads, >= 256 MiB: the framed regular kernel; the
+    (65456 * 4102 + 1280, 65456),           # GM payloads, >= 256 MiB (the table-light kernel); the
                                             # short last fragment's register lands in row 15
     (39984 * 6800 + 4096 * 3 + 16, 39984),  # 10-row frames, P = 976; last fragment 3 rows + 16 bytes
-    ((131072 - 16) * 2100, 131072 - 16),    # 32-row frames, P = 16
+    ((131072 - 16) * 2100, 131072 - 16),    # 32-row frames, P = 16 (8-row groups)
+    (24592 * 11000 + 4096 + 32, 24592),     # 7-row frames (P = 4080): the framed regular kernel
+    (20480 * 13200 + 48, 20480 - 16),       # 5-row frames, P = 16, ragged end: the same
 ])
 def test_message_frames_regular_kernel(cuda, oracle, msg_len, L):
-    """lampi_msg_csum CRC of >= 256 MiB messages of 32-128 KiB fragments that are not whole rows
-    (crc_regular_kernel<kFrame>: 4 KiB frames read through buffer descriptors, the register injected
-    at the frame padding's end), every fragment vs the oracle, two registers."""
+    """lampi_msg_csum CRC of >= 256 MiB messages of 20-128 KiB fragments that are not whole rows
+    (under 8 rows crc_regular_kernel<kFrame>: 4 KiB frames read through buffer descriptors, the
+    register injected at the frame padding's end; from 8 rows the table-light kernel), every fragment
+    vs the oracle, two registers."""
     import torch
 
     dv = _dv()
