@@ -66,6 +66,8 @@ constexpr int kWaves = kBlock / 64;  // waves per workgroup
 // Global-address-space byte pointer: keeps loads as global_load_* (flat loads would force
 // vmcnt(0) + lgkmcnt(0) waits and defeat the prefetch).
 typedef __attribute__((address_space(1))) const uint8_t gbyte;
+typedef __attribute__((address_space(1))) uint8_t gbyte_w;  // global byte stores (not flat: a flat store
+                                                            // pending makes every LDS wait lgkmcnt(0))
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 typedef __attribute__((address_space(1))) const uint32_t guint;
@@ -2389,7 +2391,7 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
             emit(src, out, f, __builtin_bswap32(C), fi);
         }
         if constexpr (Src::kCopy)
-            if (lane < fi.copylen) fi.dst[lane] = fi.addr[lane];
+            if (lane < fi.copylen) ((gbyte_w *)fi.dst)[lane] = fi.addr[lane];
         return;
     }
     const uint32_t c8 = (lane & 7u) * 8u;
@@ -2436,7 +2438,8 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
                 if (!(x >= P && x + 16u <= cend) && x < cend && x + 16u > P) {
                     const uint32_t w[4] = {dc[q].x, dc[q].y, dc[q].z, dc[q].w};
                     for (uint32_t j = 0; j < 16; ++j)
-                        if (x + j >= P && x + j < cend) fi.dst[x + j - P] = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
+                        if (x + j >= P && x + j < cend)
+                            ((gbyte_w *)fi.dst)[x + j - P] = (uint8_t)(w[j >> 2] >> (8u * (j & 3u)));
                 }
             }
         }
