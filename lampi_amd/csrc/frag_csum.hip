@@ -3855,14 +3855,8 @@ static hipError_t launch_planned(const lampi_frag_desc *d, size_t n, uint32_t *o
 // not 48), and fragments longer than kSegRows rows run as W = ceil(r / kSegRows) row segments each
 // (RowSegSource, out zeroed first: split fragments accumulate into it) -- segments of ~64 KiB, so the
 // per-segment join (a constant-product shift past the later rows) stays small against its rows.
-#ifndef LAMPI_MSG_LIGHT
-#define LAMPI_MSG_LIGHT 1
-#endif
-#ifndef LAMPI_LDR
-#define LAMPI_LDR 8
-#endif
 constexpr uint32_t kSegRows = 16;
-constexpr uint32_t kLightDescRows = LAMPI_LDR;
+constexpr uint32_t kLightDescRows = 8;  // read-only CRC with LAMPI_CSUM_ROWS_HINT(r >= 8): table-light kernel
 constexpr uint32_t kLightRoRows = 8;
 template <bool kSum, int kWv, int kCap>
 static hipError_t launch_row_segments(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
@@ -3950,7 +3944,7 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     // chains are fragments; larger messages keep the framed regular kernel (131,056 B at 4 GiB
     // 76.8% against 75.7%)
     const size_t R = (frag_len + kRowBytes - 1) / kRowBytes;
-    if (LAMPI_MSG_LIGHT && crc_light_msg(frag_len, msg_len))
+    if (crc_light_msg(frag_len, msg_len))
         return launch_crc_light_frag_copy(MsgSource{base, msg_len, frag_len, partial}, n, img, out, s,
                                           R <= kSegRows ? 1u : (uint32_t)((R + kLightRoRows - 1) / kLightRoRows));
     if (frame_ok(base, msg_len, frag_len, n)) return launch_crc_frames(base, msg_len, frag_len, partial, n, out, img, s);
@@ -4053,7 +4047,8 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
                              hipStream_t s, uint32_t rows_hint) {
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC)
-    if (mode == LAMPI_CSUM_CRC32) return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
+    if (mode == LAMPI_CSUM_CRC32)
+        return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
     return launch_sum_copy_groups(CopySource{d}, n, out, s, rows_hint);
 }
 
