@@ -664,7 +664,7 @@ def run_e2e(args):
     import numpy as np
     import torch
 
-    from lampi_amd import shard
+    from lampi_amd import _lib, shard
     from lampi_amd._lib import check, lib as _clib
 
     torch.cuda.set_device(0)
@@ -689,11 +689,25 @@ def run_e2e(args):
             fn()
         return (time.perf_counter() - t0) / reps
 
-    # raw PCIe rates of this box: pinned H2D and D2H of the whole message (torch copies)
+    # raw PCIe rates of this box: pinned H2D and D2H of the whole message (torch copies), and both at
+    # once on two streams (the receive path moves every byte both ways: ring -> HBM -> application)
     t_h2d = timed(lambda: (staged.copy_(pinned, non_blocking=True), torch.cuda.synchronize()))
     t_d2h = timed(lambda: (pinned.copy_(staged, non_blocking=True), torch.cuda.synchronize()))
-    del staged
+    back = torch.empty(msg_bytes, dtype=torch.uint8).pin_memory()
+    staged2 = torch.empty_like(staged)
+    s_up, s_down = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def duplex():
+        with torch.cuda.stream(s_up):
+            staged2.copy_(pinned, non_blocking=True)
+        with torch.cuda.stream(s_down):
+            back.copy_(staged, non_blocking=True)
+        torch.cuda.synchronize()
+
+    t_duplex = timed(duplex)
+    del staged, staged2, back
     h2d, d2h = msg_bytes / GIB / t_h2d, msg_bytes / GIB / t_d2h
+    duplex_rate = msg_bytes / GIB / t_duplex  # bytes per direction / time, both directions busy
     res = {}
     ok_all = True
     for L in (4096, 16384, 65456):
@@ -734,13 +748,61 @@ def run_e2e(args):
                 "GiB_per_s": round(msg_bytes / GIB / t, 2), "ms": round(t * 1e3, 3),
                 "frac_of_min_h2d_d2h": round(msg_bytes / GIB / t / min(h2d, d2h), 4),
                 "slot_stride": stride, "bit_exact_and_copied": bool(ok)}
-        del ring
+        # the receive side: the fragments now sit in the pinned ring (payload at +72 of each slot, its CRC
+        # from the send call as the header's dataChecksum); one lampi_host_copy_to_app_batch call delivers
+        # them all into an application buffer (ring order: one D2H per chunk) and verifies every checksum
+        lens = np.full(nfr, L, dtype=np.uint32)
+        lens[-1] = msg_bytes - (nfr - 1) * L
+        frags = (_lib.HostRecvFrag * nfr)()
+        fr = np.ctypeslib.as_array(ctypes.cast(frags, ctypes.POINTER(ctypes.c_uint8)), shape=(nfr * 32,)).view(
+            np.dtype([("frag_off", "<u8"), ("app", "<u8"), ("app_len", "<i8"), ("length", "<u4"),
+                      ("expected", "<u4")]))
+        fr["frag_off"] = 72 + np.arange(nfr, dtype=np.uint64) * stride
+        fr["app_len"] = lens
+        fr["length"] = lens
+        fr["expected"] = out
+        copied = np.empty(nfr, np.int64)
+        csums = np.empty(nfr, np.uint32)
+        mask = np.empty((nfr + 31) // 32, np.uint32)
+        nbad = ctypes.c_uint32(0)
+        app_pin = torch.empty(msg_bytes, dtype=torch.uint8).pin_memory()
+        app_pg = np.empty(msg_bytes, dtype=np.uint8)
+        ring_pg[:] = ring.numpy()
+        for ring_kind, ring_base, app_kind, app_arr, app_ptr in (
+                ("pinned", ring.data_ptr(), "pinned", app_pin.numpy(), app_pin.data_ptr()),
+                ("pinned", ring.data_ptr(), "pageable", app_pg, app_pg.ctypes.data),
+                ("pageable", ring_pg.ctypes.data, "pageable", app_pg, app_pg.ctypes.data)):
+            fr["app"] = app_ptr + np.arange(nfr, dtype=np.uint64) * L
+            app_arr.fill(0)
+            t = timed(lambda: check(c.lampi_host_copy_to_app_batch(ring_base, nfr * stride, ctypes.addressof(frags), nfr,
+                                                                   copied.ctypes.data, csums.ctypes.data,
+                                                                   mask.ctypes.data, ctypes.byref(nbad), 0),
+                                    "lampi_host_copy_to_app_batch"))
+            ok = (nbad.value == 0 and np.array_equal(copied, lens.astype(np.int64)) and np.array_equal(csums, out)
+                  and not mask.any() and shard.digest(csums, ks) == (g["crc_xor"], g["crc_wsum"])
+                  and np.array_equal(app_arr, pageable))
+            ok_all &= ok
+            row[f"recv_{ring_kind}_ring_{app_kind}_app"] = {
+                "GiB_per_s": round(msg_bytes / GIB / t, 2), "ms": round(t * 1e3, 3),
+                "frac_of_duplex": round(msg_bytes / GIB / t / duplex_rate, 4),
+                "frac_of_min_h2d_d2h": round(msg_bytes / GIB / t / min(h2d, d2h), 4),
+                "bit_exact_and_delivered": bool(ok)}
+        # the receiver's header check over the same ring (72-byte headers, GM residue; the headers hold no
+        # stamped checksum here, so every one is reported -- this leg is timed, not checked)
+        offs = np.arange(nfr, dtype=np.uint64) * stride
+        t = timed(lambda: check(c.lampi_host_header_check_batch(ring.data_ptr(), nfr * stride, offs.ctypes.data, nfr,
+                                                                72, 18, 68, mask.ctypes.data, ctypes.byref(nbad), 0),
+                                "lampi_host_header_check_batch"))
+        row["header_check_pinned_ring"] = {"headers_per_s": round(nfr / t), "ms": round(t * 1e3, 3),
+                                           "nbad": int(nbad.value)}
+        del ring, app_pin
         res[str(L)] = row
     print(json.dumps({"metric": "end-to-end host-memory fragment-CRC (config E: 256 MiB message in host memory, "
-                                "one lampi_host_msg_csum / lampi_host_msg_bcopy call per message)",
+                                "one lampi_host_msg_csum / lampi_host_msg_bcopy call per message; the receive "
+                                "side one lampi_host_copy_to_app_batch call per message)",
                       "unit": "GiB/s", "results": res, "pinned_h2d_GiB_per_s": round(h2d, 2),
-                      "pinned_d2h_GiB_per_s": round(d2h, 2), "reps": reps,
-                      "parity_ok": bool(ok_all)}), flush=True)
+                      "pinned_d2h_GiB_per_s": round(d2h, 2), "duplex_GiB_per_s_per_direction": round(duplex_rate, 2),
+                      "reps": reps, "parity_ok": bool(ok_all)}), flush=True)
 
 
 def run_bcopy(args):

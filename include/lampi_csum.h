@@ -125,7 +125,8 @@ unsigned long lampi_bcopy_csum(const void *src, void *dst, unsigned long copylen
  * message and write the slots in place, page-locked or pageable (the runtime stages pageable
  * H2D at the pinned rate; pageable slots halve the D2H rate: register NIC rings with
  * lampi_host_register).  Synchronous: everything is written when the call returns.  Returns 0 or a hipError_t
- * (invalid arguments: hipErrorInvalidValue; nothing is written then).
+ * (invalid arguments -- frag_len 0 or above 1 GiB among them -- hipErrorInvalidValue; nothing is written
+ * then; after a failure nothing is left in flight).
  * ---------------------------------------------------------------------------------- */
 
 /* Checksum-only: what the sender stores in dataChecksum for each fragment of the range --
@@ -144,6 +145,70 @@ int lampi_host_msg_csum(const void *h_msg, size_t msg_len, size_t frag_len, size
  * is touched.  h_ring must not overlap h_msg. */
 int lampi_host_msg_bcopy(const void *h_msg, size_t msg_len, size_t frag_len, size_t k_first, size_t k_count,
                          void *h_ring, size_t slot_stride, uint32_t partial, uint32_t *h_out, int mode);
+
+/* ------------------------------------------------------------------------------------
+ * Host-memory receive path: a batch of received fragments in one call.
+ * The reference's receive loop drains every pending NIC event (gmPath::receive,
+ * src/path/gm/path.cc:286-313; ibPath::receive, src/path/ib/path.cc:630-741), checks each
+ * header (gm/path.cc:364-393, ib/path.cc:652-680), matches the fragment to a posted receive and
+ * delivers it with RecvDesc_t::CopyToApp (src/path/common/BaseDesc.cc:288-342).  These entry
+ * points take the drained batch at once: the fragments sit anywhere in a host NIC ring
+ * [h_ring, h_ring + ring_bytes) (page-locked or pageable; every byte of it may be read by the
+ * DMA engines, so it must be one readable range), the application buffers anywhere in host
+ * memory (they must not overlap the ring).  Synchronous, on the calling thread's own streams (the
+ * pipeline of the send path): when the call returns every result and delivered byte is in place.
+ * Return 0 or a hipError_t; invalid arguments return hipErrorInvalidValue before anything is
+ * written.  Masks hold one bit per fragment, bit (i % 32) of word i / 32, SET when fragment i
+ * FAILS; *h_nbad receives the number of failures.
+ * ---------------------------------------------------------------------------------- */
+
+/* One received fragment to deliver (32 bytes, little-endian): offset 0 frag_off, 8 app, 16 app_len,
+ * 24 length, 28 expected. */
+typedef struct lampi_host_recv_frag {
+    uint64_t frag_off;  /* the payload's offset in the ring (BaseRecvFragDesc_t::addr_m - h_ring) */
+    void    *app;       /* host address it is delivered to: RecvDesc_t::addr_m + dataOffset() */
+    int64_t  app_len;   /* room left in the posted buffer at that offset: posted_m.length_m - Offset
+                           (ref BaseDesc.cc:307); may be <= 0 */
+    uint32_t length;    /* bytes received, length_m (GM: event length - sizeof(gmHeader)); all of them are
+                           checksummed */
+    uint32_t expected;  /* the sender's checksum from the fragment's header: gmHeader_m->data.dataChecksum
+                           (gm/recvFrag.h:233), msg_m->header.dataChecksum (ib/recvFrag.cc:233) */
+} lampi_host_recv_frag;
+
+/* RecvDesc_t::CopyToApp for every fragment of the batch, as lampi_copy_to_app_batch does on the device
+ * (CopyFunction gm/recvFrag.h:165-182 / ib/recvFrag.cc:182-200 fused with CheckData gm/recvFrag.h:213-257
+ * / ib/recvFrag.cc:229-245):
+ *   lengthToCopy = app_len <= 0 ? 0 : min(length, app_len);
+ *   lengthToCopy > 0:  lengthToCopy bytes ring -> app, the checksum over all `length` bytes compared with
+ *                      `expected` (the bytes are delivered either way, as bcopy_uicrc does before CheckData);
+ *   lengthToCopy == 0: nothing read, copied or checksummed; DataOK.
+ * h_copied[i] = lengthToCopy, or -1 when the checksum differs (CopyToApp's return value); h_csum[i] = the
+ * calculated checksum (CRC_INITIAL_REGISTER / 0 when nothing was checksummed); h_mask (ceil(n/32) words,
+ * overwritten) and *h_nbad as above.  The fragments' ring bytes move to the GPU in as few DMA transfers as
+ * their layout allows (dense runs one copy, a constant slot pitch one 2D copy), the delivered bytes come
+ * back in one copy per run of fragments contiguous in the application buffer.  `mode` may carry
+ * LAMPI_CSUM_ROWS_HINT(r) to override the row-group count the library derives from the fragments' mean
+ * length.  Fragments up to 1 GiB. */
+int lampi_host_copy_to_app_batch(const void *h_ring, size_t ring_bytes, const lampi_host_recv_frag *h_frags,
+                                 size_t n, int64_t *h_copied, uint32_t *h_csum, uint32_t *h_mask, uint32_t *h_nbad,
+                                 int mode);
+
+/* The GM receiver's header check over a batch of received headers at h_ring + h_hdr_offs[i]
+ * (gmPath::receive, ref src/path/gm/path.cc:364-393), as lampi_header_check_batch does on the device:
+ * header i fails unless CRC mode: uicrc(hdr_i, hdr_bytes) == 0; SUM mode: the sum of word_count words ==
+ * 2 x the stored checksum at csum_offset (4-byte aligned).  Headers may sit at any byte offset; each is
+ * read once (its bytes gathered into pinned staging, the checks run on the GPU). */
+int lampi_host_header_check_batch(const void *h_ring, size_t ring_bytes, const uint64_t *h_hdr_offs, size_t n,
+                                  uint32_t hdr_bytes, uint32_t word_count, uint32_t csum_offset, uint32_t *h_mask,
+                                  uint32_t *h_nbad, int mode);
+
+/* The IB receiver's header check over the same kind of batch (ibPath::receive, ref
+ * src/path/ib/path.cc:652-680), as lampi_header_compare_batch: header i fails unless the 32-bit value at
+ * csum_offset equals uicrc(hdr_i, crclen) / uicsum(hdr_i, crclen) (e.g. crclen 68, csum_offset 68 for an
+ * ibDataHdr_t). */
+int lampi_host_header_compare_batch(const void *h_ring, size_t ring_bytes, const uint64_t *h_hdr_offs, size_t n,
+                                    uint32_t crclen, uint32_t csum_offset, uint32_t *h_mask, uint32_t *h_nbad,
+                                    int mode);
 
 /* Page-lock [h_ptr, h_ptr+len) for direct DMA by the host paths (hipHostRegister) and undo it:
  * the analogue of registering NIC buffers with the network (GM gm_register_memory).  Return 0
@@ -327,14 +392,18 @@ int lampi_fill_stream(void *d_dst, size_t nbytes, uint64_t seed, uint64_t byte_o
 int lampi_fill_stream_frags(void *d_dst, size_t n, size_t frag_len, uint64_t seed, uint64_t k0,
                             uint64_t kstep, void *stream);
 
-/* Release the calling thread's staging resources of the host entry points (stream, device
- * buffers, pinned bounce buffer).  They are also released automatically when the thread exits
+/* Release the calling thread's staging resources of the host entry points (streams, device
+ * buffers, pinned bounce buffer) and its device scratch of the batched entry points.  They are also released automatically when the thread exits
  * or switches to another device; the next host call on the thread allocates them again. */
 void lampi_host_release(void);
 
 /* Bytes of page-locked host memory the library's host paths hold right now, over all threads
  * (bounce buffers, result words, staging): a leak check for callers with short-lived threads. */
 int64_t lampi_host_pinned_bytes(void);
+
+/* Bytes of device scratch the library holds right now, over all threads (the per-thread, per-stream
+ * buffers of the row-group joins and byte plans): freed at thread exit and by lampi_host_release(). */
+int64_t lampi_device_scratch_bytes(void);
 
 /* Version string of the engine and the gfx target it was built for. */
 const char *lampi_csum_version(void);

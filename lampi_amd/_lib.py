@@ -56,6 +56,15 @@ class RecvDesc(ctypes.Structure):
 
 assert ctypes.sizeof(RecvDesc) == 32
 
+class HostRecvFrag(ctypes.Structure):
+    """struct lampi_host_recv_frag (32 bytes): frag_off u64, app ptr, app_len i64, length u32, expected u32."""
+
+    _fields_ = [("frag_off", ctypes.c_uint64), ("app", ctypes.c_void_p), ("app_len", ctypes.c_int64),
+                ("length", ctypes.c_uint32), ("expected", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(HostRecvFrag) == 32
+
 _lock = threading.Lock()
 _lib = None
 
@@ -104,6 +113,14 @@ PROTOTYPES = {
                                            c_void_p, ctypes.c_int]),
     "lampi_host_msg_bcopy": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_size_t, c_size_t, c_void_p, c_size_t,
                                             ctypes.c_uint32, c_void_p, ctypes.c_int]),
+    "lampi_host_copy_to_app_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p,
+                                                    c_void_p, c_void_p, ctypes.c_int]),
+    "lampi_host_header_check_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.c_uint32,
+                                                     ctypes.c_uint32, ctypes.c_uint32, c_void_p, c_void_p,
+                                                     ctypes.c_int]),
+    "lampi_host_header_compare_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.c_uint32,
+                                                       ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_int]),
+    "lampi_device_scratch_bytes": (ctypes.c_int64, []),
     "lampi_host_register": (ctypes.c_int, [c_void_p, c_size_t]),
     "lampi_host_unregister": (ctypes.c_int, [c_void_p]),
     "lampi_csum_version": (ctypes.c_char_p, []),

@@ -38,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <type_traits>
@@ -3775,42 +3776,95 @@ static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size
 // Not the default: the plan launch adds ~10 us to every call (1 x 4 KiB: 7.8 -> 20 us, 4,096 x 4 KiB:
 // 10.6 -> 23 us; profiles/r03/bigdesc_ab.txt).  Larger batches keep the count split.
 // Device scratch for a launch sequence on stream s (the byte-balanced plan, the light copy's group
-// values): one grow-only buffer per (device, stream), reused in stream order -- a call's kernels
-// finish with it before the next call's on the same stream start.  Per-call hipMallocAsync /
-// hipFreeAsync put a ~6 us gap before the next kernel on the stream (profiles/r03/light_join_gap.txt).
-// Growing frees the old buffer with hipFree, which waits for the device.  Kept until process exit.
+// values): one grow-only buffer per (calling thread, device, stream), reused in stream order -- a
+// call's kernels finish with it before the same thread's next call on that stream starts.  Keyed by
+// thread as well, so two threads calling on one stream (torch's default stream, handle 0) never share
+// a buffer: their producer and join launches may interleave on the stream, each pair reading only its
+// own values.  Per-call hipMallocAsync / hipFreeAsync put a ~6 us gap before the next kernel on the
+// stream (profiles/r03/light_join_gap.txt).  Growing first synchronizes s (this thread's earlier
+// launches on it are the only users of the old buffer), then frees it.  The thread's buffers are
+// freed at thread exit, by lampi_host_release() and, per stream, when the host pipeline destroys its
+// streams (release_stream_scratch); lampi_device_scratch_bytes() counts them for leak checks.
 // While s is being captured into a graph the graph gets its own allocation (hipMallocAsync; *pooled
 // set: release it with scratch_done), so no replay depends on a buffer a later call may replace.
+namespace {
+std::atomic<int64_t> g_scratch_bytes{0};
+
+struct ScratchTable {
+    struct Slot {
+        void *p = nullptr;
+        size_t cap = 0;
+    };
+    std::map<std::pair<int, hipStream_t>, Slot> slots;
+    ScratchTable() = default;
+    ScratchTable(const ScratchTable &) = delete;
+    ScratchTable &operator=(const ScratchTable &) = delete;
+    ~ScratchTable() { release_if([](const std::pair<int, hipStream_t> &) { return true; }); }
+
+    // Free the slots whose key satisfies pred, each on its own device after its stream drained;
+    // errors are ignored (this also runs at thread exit).
+    template <class Pred>
+    void release_if(Pred pred) {
+        int cur = -1;
+        const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+        int set = cur;
+        for (auto it = slots.begin(); it != slots.end();) {
+            if (!pred(it->first)) {
+                ++it;
+                continue;
+            }
+            if (it->first.first != set && hipSetDevice(it->first.first) == hipSuccess) set = it->first.first;
+            (void)hipStreamSynchronize(it->first.second);
+            (void)hipFree(it->second.p);
+            g_scratch_bytes.fetch_sub((int64_t)it->second.cap, std::memory_order_relaxed);
+            it = slots.erase(it);
+        }
+        if (have_cur && set != cur) (void)hipSetDevice(cur);
+    }
+};
+thread_local ScratchTable t_scratch;
+}  // namespace
+
 static hipError_t stream_scratch(hipStream_t s, size_t bytes, void **out, bool *pooled) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     hipError_t ce = hipStreamIsCapturing(s, &cs);
     if (ce != hipSuccess) return ce;
     *pooled = cs != hipStreamCaptureStatusNone;
     if (*pooled) return hipMallocAsync(out, bytes, s);
-    static std::mutex mu;
-    static auto *bufs = new std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>>();  // never freed
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
-    std::lock_guard<std::mutex> g(mu);
-    auto &slot = (*bufs)[{dev, s}];
-    if (slot.second < bytes) {
-        if (slot.first) {
-            e = hipFree(slot.first);
-            slot = {nullptr, 0};
-            if (e != hipSuccess) return e;
+    ScratchTable::Slot &slot = t_scratch.slots[{dev, s}];
+    if (slot.cap < bytes) {
+        if (slot.p) {
+            e = hipStreamSynchronize(s);  // this thread's earlier launches on s still read the old buffer
+            if (e == hipSuccess) e = hipFree(slot.p);
+            if (e != hipSuccess) return e;  // the old buffer stays in the slot, still valid
+            g_scratch_bytes.fetch_sub((int64_t)slot.cap, std::memory_order_relaxed);
+            slot = {};
         }
         const size_t want = std::max<size_t>(bytes + bytes / 4, 1u << 20);
-        e = hipMalloc(&slot.first, want);
+        e = hipMalloc(&slot.p, want);
         if (e != hipSuccess) {
-            slot = {nullptr, 0};
+            slot = {};
             return e;
         }
-        slot.second = want;
+        slot.cap = want;
+        g_scratch_bytes.fetch_add((int64_t)want, std::memory_order_relaxed);
     }
-    *out = slot.first;
+    *out = slot.p;
     return hipSuccess;
 }
+
+void release_stream_scratch(hipStream_t s) {
+    t_scratch.release_if([s](const std::pair<int, hipStream_t> &k) { return k.second == s; });
+}
+
+void release_thread_scratch() {
+    t_scratch.release_if([](const std::pair<int, hipStream_t> &) { return true; });
+}
+
+int64_t device_scratch_bytes() { return g_scratch_bytes.load(std::memory_order_relaxed); }
 
 static hipError_t scratch_done(hipStream_t s, void *p, bool pooled, hipError_t e) {
     const hipError_t f = pooled ? hipFreeAsync(p, s) : hipSuccess;

@@ -95,4 +95,10 @@ hipError_t launch_fill_frags(uint64_t *dst, size_t n, uint64_t frag_words, uint6
 hipError_t launch_fill_stream(uint8_t *dst, size_t nbytes, uint64_t seed, uint64_t byte_off, int grid,
                               hipStream_t s);
 
+// The calling thread's device scratch (stream_scratch, frag_csum.hip): free its buffer for stream s
+// (before s is destroyed) or all of its buffers (lampi_host_release); bytes held over all threads.
+void release_stream_scratch(hipStream_t s);
+void release_thread_scratch();
+int64_t device_scratch_bytes();
+
 }  // namespace lampi

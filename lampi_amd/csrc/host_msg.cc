@@ -26,29 +26,12 @@
 #include <cstring>
 
 #include "../../include/lampi_csum.h"
+#include "frag_csum_kernels.h"
 #include "host_internal.h"
+#include "host_pipe.h"
 
 namespace lampi {
 namespace {
-
-constexpr int kBufs = 3;                    // device chunks in flight
-// Bytes per chunk (whole fragments; at least one).  Back-to-back 16 MiB H2D copies ran at 51.3-51.5
-// GiB/s against 52.9-53.3 for 64 MiB ones (profiles/r03/pcie_duplex_run*.txt), and every chunk adds
-// cross-stream waits; three 64 MiB chunks are 192 MiB of HBM.
-constexpr size_t kChunkTarget = 64u << 20;
-
-// Everything a thread's pipeline holds; a plain aggregate, so release() can reset it.
-struct PipeState {
-    int dev = -1;
-    hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
-    hipEvent_t in_done[kBufs] = {}, k_done[kBufs] = {}, out_done[kBufs] = {};
-    uint8_t *dchunk = nullptr;  // kBufs chunks of chunk_bytes
-    size_t chunk_bytes = 0;
-    uint32_t *dres = nullptr;  // per-fragment results of the call
-    size_t res_cap = 0;
-    uint32_t *hres = nullptr;  // pinned landing place of the results (then copied to the caller's array)
-    size_t hres_cap = 0;
-};
 
 struct PipeCtx {
     PipeState st;
@@ -67,9 +50,10 @@ struct PipeCtx {
         if (have_cur && cur != p.dev) (void)hipSetDevice(p.dev);
         for (hipStream_t s : {p.s_in, p.s_k, p.s_out})
             if (s) (void)hipStreamSynchronize(s);
-        if (p.dchunk) (void)hipFree(p.dchunk);
-        if (p.dres) (void)hipFree(p.dres);
-        pinned_free(p.hres, p.hres_cap * sizeof(uint32_t));
+        if (p.s_k) release_stream_scratch(p.s_k);  // the light copies' group values of this thread on s_k
+        for (uint8_t *d : {p.dchunk, p.dout, p.dmeta})
+            if (d) (void)hipFree(d);
+        pinned_free(p.hmeta, p.hmeta_cap);
         for (int b = 0; b < kBufs; ++b)
             for (hipEvent_t e : {p.in_done[b], p.k_done[b], p.out_done[b]})
                 if (e) (void)hipEventDestroy(e);
@@ -82,11 +66,22 @@ struct PipeCtx {
 
 thread_local PipeCtx t_pipe;
 
-#define TRY(call)                                   \
-    do {                                            \
-        const hipError_t e_ = (call);               \
-        if (e_ != hipSuccess) return e_;            \
-    } while (0)
+#define TRY LAMPI_TRY
+
+hipError_t grow_device(uint8_t *&ptr, size_t &cap, size_t want, PipeState &p) {
+    if (cap >= want) return hipSuccess;
+    if (ptr) {
+        for (hipStream_t s : {p.s_in, p.s_k, p.s_out}) TRY(hipStreamSynchronize(s));
+        TRY(hipFree(ptr));
+        ptr = nullptr;
+        cap = 0;
+    }
+    TRY(hipMalloc((void **)&ptr, want));
+    cap = want;
+    return hipSuccess;
+}
+
+}  // namespace
 
 hipError_t pipe_ctx(PipeState **out) {
     int dev = 0;
@@ -104,41 +99,40 @@ hipError_t pipe_ctx(PipeState **out) {
     return hipSuccess;
 }
 
-// Capacity helpers: grow only (a device buffer is freed after the streams drained).
+// every chunk starts 256-byte aligned
 hipError_t ensure_chunks(PipeState &p, size_t chunk) {
-    chunk = (chunk + 255) & ~(size_t)255;  // every chunk starts 256-byte aligned
+    chunk = align_up(chunk, 256);
     if (p.chunk_bytes >= chunk) return hipSuccess;
-    if (p.dchunk) {
-        for (hipStream_t s : {p.s_in, p.s_k, p.s_out}) TRY(hipStreamSynchronize(s));
-        TRY(hipFree(p.dchunk));
-        p.dchunk = nullptr;
-        p.chunk_bytes = 0;
-    }
-    TRY(hipMalloc((void **)&p.dchunk, kBufs * chunk));
+    size_t cap = 0;
+    TRY(grow_device(p.dchunk, cap, kBufs * chunk, p));
     p.chunk_bytes = chunk;
     return hipSuccess;
 }
 
-hipError_t ensure_results(PipeState &p, size_t n) {
-    if (p.res_cap < n) {
-        if (p.dres) {
-            TRY(hipStreamSynchronize(p.s_k));
-            TRY(hipFree(p.dres));
-            p.dres = nullptr;
-            p.res_cap = 0;
-        }
-        TRY(hipMalloc((void **)&p.dres, n * sizeof(uint32_t)));
-        p.res_cap = n;
-    }
-    if (p.hres_cap < n) {
-        pinned_free(p.hres, p.hres_cap * sizeof(uint32_t));
-        p.hres = nullptr;
-        p.hres_cap = 0;
-        TRY(pinned_alloc((void **)&p.hres, n * sizeof(uint32_t), hipHostMallocDefault));
-        p.hres_cap = n;
+hipError_t ensure_out_chunks(PipeState &p, size_t chunk) {
+    chunk = align_up(chunk, 256);
+    if (p.out_bytes >= chunk) return hipSuccess;
+    size_t cap = 0;
+    TRY(grow_device(p.dout, cap, kBufs * chunk, p));
+    p.out_bytes = chunk;
+    return hipSuccess;
+}
+
+hipError_t ensure_meta(PipeState &p, size_t bytes) {
+    bytes = align_up(std::max<size_t>(bytes, 4096), 4096);
+    TRY(grow_device(p.dmeta, p.dmeta_cap, bytes, p));
+    if (p.hmeta_cap < bytes) {
+        // the previous call synchronized before it returned: nothing reads the old image
+        pinned_free(p.hmeta, p.hmeta_cap);
+        p.hmeta = nullptr;
+        p.hmeta_cap = 0;
+        TRY(pinned_alloc((void **)&p.hmeta, bytes, hipHostMallocDefault));
+        p.hmeta_cap = bytes;
     }
     return hipSuccess;
 }
+
+namespace {
 
 struct Range {
     size_t frag_len, nfrag, last;  // fragments of the call, bytes of its last fragment
@@ -175,17 +169,19 @@ hipError_t host_msg(const uint8_t *h_msg, size_t msg_len, size_t frag_len, size_
     const size_t fpc = std::max<size_t>(1, kChunkTarget / frag_len);  // fragments per chunk
     const size_t cb = fpc * frag_len;
     TRY(ensure_chunks(p, cb));
-    TRY(ensure_results(p, k_count));
+    TRY(ensure_meta(p, k_count * sizeof(uint32_t)));
+    uint32_t *dres = (uint32_t *)p.dmeta, *hres = (uint32_t *)p.hmeta;
     const bool copy = h_ring != nullptr;
 
+    PipeDrain drain(p);  // any early return below leaves nothing in flight
     const size_t nchunks = (k_count + fpc - 1) / fpc;
     for (size_t i = 0; i < nchunks; ++i) {
         const int b = (int)(i % kBufs);
         const size_t f0 = i * fpc, nf = std::min(fpc, k_count - f0);
         const size_t off = b0 + f0 * frag_len, nb = std::min(nf * frag_len, b1 - off);
         uint8_t *d = p.dchunk + (size_t)b * p.chunk_bytes;
-        // chunk b is free once chunk i - kBufs was checksummed and copied out (the previous call
-        // drained both streams before it returned)
+        // chunk b is free once chunk i - kBufs was checksummed and copied out (every call, failed
+        // ones included, drains the streams before it returns)
         if (i >= (size_t)kBufs) {
             TRY(hipStreamWaitEvent(p.s_in, p.k_done[b], 0));
             if (copy) TRY(hipStreamWaitEvent(p.s_in, p.out_done[b], 0));
@@ -193,17 +189,18 @@ hipError_t host_msg(const uint8_t *h_msg, size_t msg_len, size_t frag_len, size_
         TRY(hipMemcpyAsync(d, h_msg + off, nb, hipMemcpyHostToDevice, p.s_in));
         TRY(hipEventRecord(p.in_done[b], p.s_in));
         TRY(hipStreamWaitEvent(p.s_k, p.in_done[b], 0));
-        TRY(launch_msg_csum(d, nb, frag_len, partial, p.dres + f0, mode, dev, img, p.s_k));
+        TRY(launch_msg_csum(d, nb, frag_len, partial, dres + f0, mode, dev, img, p.s_k));
         TRY(hipEventRecord(p.k_done[b], p.s_k));
         if (!copy) continue;
         TRY(hipStreamWaitEvent(p.s_out, p.in_done[b], 0));
         TRY(copy_out(p, h_ring, stride, d, f0, nf, r));
         TRY(hipEventRecord(p.out_done[b], p.s_out));
     }
-    TRY(hipMemcpyAsync(p.hres, p.dres, k_count * sizeof(uint32_t), hipMemcpyDeviceToHost, p.s_k));
+    TRY(hipMemcpyAsync(hres, dres, k_count * sizeof(uint32_t), hipMemcpyDeviceToHost, p.s_k));
     TRY(hipStreamSynchronize(p.s_k));
     if (copy) TRY(hipStreamSynchronize(p.s_out));
-    std::memcpy(h_out, p.hres, k_count * sizeof(uint32_t));
+    drain.armed = false;
+    std::memcpy(h_out, hres, k_count * sizeof(uint32_t));
     return hipSuccess;
 }
 
@@ -212,7 +209,7 @@ int check_args(const void *h_msg, size_t msg_len, size_t frag_len, size_t k_firs
                uint32_t *h_out, int mode, bool *done, uint32_t partial) {
     *done = false;
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return (int)hipErrorInvalidValue;
-    if (frag_len == 0 || frag_len > 0xFFFFFFFFull) return (int)hipErrorInvalidValue;
+    if (frag_len == 0 || frag_len > kHostMaxFrag) return (int)hipErrorInvalidValue;
     const size_t nfr = msg_len ? (msg_len - 1) / frag_len + 1 : 1;
     if (k_first > nfr || k_count > nfr - k_first) return (int)hipErrorInvalidValue;
     if (k_count == 0) {

@@ -1,0 +1,516 @@
+// host_recv.cc -- the receive half of the host-memory path of liblampi_csum.so
+// (lampi_host_copy_to_app_batch, lampi_host_header_check_batch, lampi_host_header_compare_batch;
+// include/lampi_csum.h).
+//
+// LA-MPI's receive loop drains every pending NIC event in one call (gmPath::receive, ref
+// src/path/gm/path.cc:286-313; IB src/path/ib/path.cc:630-741).  Per fragment it checks the header
+// (gm/path.cc:364-393; IB recompute-and-compare, ib/path.cc:652-680), matches it to a posted
+// receive and delivers the payload: RecvDesc_t::CopyToApp (src/path/common/BaseDesc.cc:288-342)
+// copies min(length_m, AppBufferLen) bytes into the application buffer with the checksum of all
+// length_m bytes fused (CopyFunction, gm/recvFrag.h:165-182: bcopy_uicrc / bcopy_uicsum with
+// copylen < csumlen; IB recvFrag.cc:182-200) and compares it with the header's dataChecksum
+// (CheckData, gm/recvFrag.h:213-257; IB recvFrag.cc:229-245).
+//
+// Here the caller hands over the whole batch of drained fragments at once: payloads anywhere in a
+// host NIC ring (page-locked or pageable), the application bytes go to host addresses.  The
+// per-thread pipeline of host_msg.cc carries it:
+//
+//   s_in : H2D of chunk i -- the ring bytes under its fragments, coalesced into as few DMA
+//          transfers as the layout allows: a dense run of fragments (gaps <= 1/16 of the payload,
+//          e.g. GM's payloads 80 bytes apart, IB's 112) is one 1D copy, fragments at a constant
+//          slot pitch with wide gaps (4 KiB payloads in 64 KiB slots) one 2D copy, anything else
+//          one copy each
+//   s_k  : the fused CopyToApp kernel over the chunk (launch_copy_to_app, the device path's own
+//          kernel; the row-group count comes from the fragments' mean length, which the host knows)
+//          into per-fragment results, the delivered bytes packed into an output chunk so that every
+//          run of fragments contiguous in the application buffer goes back in one D2H
+//   s_out: D2H of those runs straight into the application buffers
+//
+// Results come back in one D2H at the end.  No payload byte is touched by the CPU; it reads only the
+// descriptors the caller built.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "../../include/lampi_csum.h"
+#include "crc_tables.h"
+#include "frag_csum_kernels.h"
+#include "host_internal.h"
+#include "host_pipe.h"
+
+namespace lampi {
+namespace {
+
+#define TRY LAMPI_TRY
+
+// A DMA transfer host -> chunk (rows == 1: 1D of width bytes) or chunk -> application buffer.
+struct InXfer {
+    size_t hoff;    // ring offset of the first byte
+    size_t width;   // bytes per row
+    size_t rows;
+    size_t hpitch;  // ring bytes between rows (2D)
+    size_t doff;    // offset in the input chunk
+    size_t dpitch;
+};
+struct OutXfer {
+    uint8_t *h;
+    size_t doff;  // offset in the output chunk
+    size_t bytes;
+};
+struct ChunkPlan {
+    size_t f0 = 0, f1 = 0;        // fragments [f0, f1)
+    size_t xi0 = 0, xi1 = 0;      // its H2D transfers
+    size_t xo0 = 0, xo1 = 0;      // its D2H transfers
+    size_t in_used = 0, out_used = 0;
+    uint64_t payload = 0;         // bytes checksummed
+    size_t ncopy = 0;             // fragments with bytes to deliver
+    size_t mask_word0 = 0;        // its mask words in the call's mask scratch
+};
+
+uint32_t to_copy(const lampi_host_recv_frag &x) {
+    return x.app_len <= 0 ? 0u : (x.app_len < (int64_t)x.length ? (uint32_t)x.app_len : x.length);
+}
+
+// Dense 1D runs may carry gaps of at most this many bytes each and 1/16 of their payload in all.
+constexpr size_t kDenseGap = 4096;
+
+// The open run of ring bytes being coalesced into one H2D transfer.
+struct InRun {
+    enum Kind { kNone, kOne, kDense, kPitch } kind = kNone;
+    size_t lo = 0, end = 0;        // ring range [lo, end) (1D kinds)
+    size_t last = 0, pitch = 0;    // the last member's offset, the slot pitch (kPitch)
+    size_t width = 0;              // the widest member (kPitch rows)
+    size_t gaps = 0, payload = 0;  // gap and payload bytes (kDense)
+    size_t rows = 0;               // members
+    size_t size() const {          // device bytes it needs
+        if (kind == kNone) return 0;
+        if (kind == kPitch) return rows * align_up(width, 16);
+        return end - lo;
+    }
+    // The run with fragment [o, o + len) appended, or kind kNone if it cannot take it.
+    InRun extended(size_t o, size_t len, size_t ring_bytes) const {
+        InRun r = *this;
+        switch (kind) {
+            case kNone:
+                break;
+            case kOne:
+                if (o >= end && o - end <= kDenseGap && (o - end) * 16 <= payload + len) {
+                    r.kind = kDense;
+                    r.gaps = o - end;
+                    r.payload += len;
+                    r.end = o + len;
+                    r.last = o;
+                    r.rows = 2;
+                    return r;
+                }
+                if (o > last && o - last >= std::max(width, len) && o + std::max(width, len) <= ring_bytes) {
+                    r.kind = kPitch;
+                    r.pitch = o - last;
+                    r.width = std::max(width, len);
+                    r.last = o;
+                    r.rows = 2;
+                    return r;
+                }
+                break;
+            case kDense:
+                if (o >= end && o - end <= kDenseGap && (gaps + o - end) * 16 <= payload + len) {
+                    r.gaps += o - end;
+                    r.payload += len;
+                    r.end = o + len;
+                    r.last = o;
+                    ++r.rows;
+                    return r;
+                }
+                break;
+            case kPitch:
+                if (o > last && o - last == pitch && len <= pitch && o + std::max(width, len) <= ring_bytes) {
+                    r.width = std::max(width, len);
+                    r.last = o;
+                    ++r.rows;
+                    return r;
+                }
+                break;
+        }
+        r.kind = kNone;
+        return r;
+    }
+    static InRun single(size_t o, size_t len) {
+        InRun r;
+        r.kind = kOne;
+        r.lo = r.last = o;
+        r.end = o + len;
+        r.width = r.payload = len;
+        r.rows = 1;
+        return r;
+    }
+};
+
+// The whole call's plan: chunks, transfers and every fragment's place in its chunk.
+struct RecvPlan {
+    std::vector<ChunkPlan> chunks;
+    std::vector<InXfer> in;
+    std::vector<OutXfer> out;
+    std::vector<size_t> din, dout;  // per fragment: offsets in its input / output chunk
+    size_t in_need = 0, out_need = 0, mask_words = 0;
+};
+
+class Planner {
+  public:
+    Planner(const lampi_host_recv_frag *f, size_t n, size_t ring_bytes, RecvPlan &p)
+        : f_(f), n_(n), ring_(ring_bytes), p_(p) {
+        p_.din.assign(n, 0);
+        p_.dout.assign(n, 0);
+    }
+
+    void run() {
+        ChunkPlan c;
+        for (size_t j = 0; j < n_; ++j) {
+            const uint32_t cj = to_copy(f_[j]);
+            if (cj == 0) continue;  // nothing to move: its result is decided without its bytes
+            const size_t o = f_[j].frag_off, len = f_[j].length;
+            uint8_t *app = (uint8_t *)f_[j].app;
+            // where j would go: extending the open runs, or opening new ones
+            const InRun ext = in_.extended(o, len, ring_);
+            const bool in_ext = ext.kind != InRun::kNone;
+            const size_t in_total = in_ext ? in_base_ + ext.size() : align_up(in_base_ + in_.size(), 256) + len;
+            const bool out_ext = out_open_ && app == out_end_;
+            const size_t out_total = out_ext ? out_used_ + cj : align_up(out_used_, 256) + cj;
+            if (c.ncopy > 0 && (in_total > kChunkTarget || out_total > kChunkTarget)) {
+                close_chunk(c, j);  // j opens the next chunk
+                c = ChunkPlan{};
+                c.f0 = j;
+                c.xi0 = p_.in.size();
+                c.xo0 = p_.out.size();
+                open_in(j, o, len);
+                open_out(j, app, cj);
+            } else {
+                if (in_ext) {
+                    in_ = ext;
+                    members_.push_back(j);
+                } else {
+                    close_in();
+                    open_in(j, o, len);
+                }
+                if (out_ext) {
+                    p_.dout[j] = out_cur_ + (size_t)(app - out_start_);
+                    out_end_ = app + cj;
+                    out_used_ += cj;
+                } else {
+                    close_out();
+                    open_out(j, app, cj);
+                }
+            }
+            c.payload += len;
+            ++c.ncopy;
+        }
+        close_chunk(c, n_);
+    }
+
+  private:
+    void open_in(size_t j, size_t o, size_t len) {
+        in_base_ = align_up(in_base_, 256);
+        in_ = InRun::single(o, len);
+        members_.assign(1, j);
+    }
+    // the open input run becomes a transfer; its members get their chunk offsets
+    void close_in() {
+        if (in_.kind == InRun::kNone) return;
+        InXfer x{};
+        x.doff = in_base_;
+        x.hoff = in_.lo;
+        if (in_.kind == InRun::kPitch) {
+            x.width = in_.width;
+            x.rows = in_.rows;
+            x.hpitch = in_.pitch;
+            x.dpitch = align_up(in_.width, 16);
+            for (size_t r = 0; r < members_.size(); ++r) p_.din[members_[r]] = x.doff + r * x.dpitch;
+        } else {
+            x.width = in_.end - in_.lo;
+            x.rows = 1;
+            x.hpitch = x.dpitch = x.width;
+            for (size_t m : members_) p_.din[m] = x.doff + (f_[m].frag_off - in_.lo);
+        }
+        p_.in.push_back(x);
+        in_base_ += in_.size();
+        in_ = InRun{};
+        members_.clear();
+    }
+    void open_out(size_t j, uint8_t *app, uint32_t cj) {
+        out_cur_ = align_up(out_used_, 256);
+        out_used_ = out_cur_ + cj;
+        out_start_ = app;
+        out_end_ = app + cj;
+        out_open_ = true;
+        p_.dout[j] = out_cur_;
+    }
+    void close_out() {
+        if (!out_open_) return;
+        p_.out.push_back(OutXfer{out_start_, out_cur_, (size_t)(out_end_ - out_start_)});
+        out_open_ = false;
+    }
+    void close_chunk(ChunkPlan &c, size_t f1) {
+        close_in();
+        close_out();
+        c.f1 = f1;
+        c.in_used = in_base_;
+        c.out_used = out_used_;
+        c.xi1 = p_.in.size();
+        c.xo1 = p_.out.size();
+        c.mask_word0 = p_.mask_words;
+        p_.mask_words += (c.f1 - c.f0 + 31) / 32;
+        p_.in_need = std::max(p_.in_need, c.in_used);
+        p_.out_need = std::max(p_.out_need, c.out_used);
+        p_.chunks.push_back(c);
+        in_base_ = 0;
+        out_used_ = 0;
+    }
+
+    const lampi_host_recv_frag *f_;
+    size_t n_, ring_;
+    RecvPlan &p_;
+    InRun in_;
+    std::vector<size_t> members_;
+    size_t in_base_ = 0;  // input chunk bytes used before the open run
+    size_t out_used_ = 0, out_cur_ = 0;
+    uint8_t *out_start_ = nullptr, *out_end_ = nullptr;
+    bool out_open_ = false;
+};
+
+// Rows per fragment for the row-group schedule of the chunk's copy kernel: the fragments' mean
+// length in 4 KiB rows (GM's 65,456-byte payloads: 16 -> 69-70% of read + write against 59%
+// walking the rows in one wave); 1 for fragments of about a row or less.
+uint32_t chunk_rows_hint(const ChunkPlan &c) {
+    if (c.ncopy == 0) return 1;
+    const uint64_t mean = c.payload / c.ncopy;
+    const uint64_t rows = (mean + kRowBytes - 1) / kRowBytes;
+    return rows >= 2 ? (uint32_t)std::min<uint64_t>(rows, 0xFFF) : 1u;
+}
+
+hipError_t host_recv(const uint8_t *h_ring, size_t ring_bytes, const lampi_host_recv_frag *f, size_t n,
+                     int64_t *h_copied, uint32_t *h_csum, uint32_t *h_mask, uint32_t *h_nbad, int mode,
+                     uint32_t hint_override) {
+    RecvPlan plan;
+    Planner(f, n, ring_bytes, plan).run();
+    PipeState *pp = nullptr;
+    TRY(pipe_ctx(&pp));
+    PipeState &p = *pp;
+    const uint32_t *img = nullptr;
+    TRY(device_tables(p.dev, &img));
+    TRY(ensure_chunks(p, std::max<size_t>(plan.in_need, 256)));
+    TRY(ensure_out_chunks(p, std::max<size_t>(plan.out_need, 256)));
+
+    // the call's descriptors and results, in one device block and its pinned image:
+    // [descs | expected] go up in one H2D, [copied | csum | mask | nbad] come back in one D2H
+    const size_t nch = plan.chunks.size();
+    const size_t o_exp = align_up(n * sizeof(lampi_recv_desc), 256);
+    const size_t o_copied = align_up(o_exp + n * sizeof(uint32_t), 256);
+    const size_t o_csum = align_up(o_copied + n * sizeof(int64_t), 256);
+    const size_t o_mask = align_up(o_csum + n * sizeof(uint32_t), 256);
+    const size_t o_nbad = align_up(o_mask + plan.mask_words * sizeof(uint32_t), 256);
+    const size_t total = o_nbad + nch * sizeof(uint32_t);
+    TRY(ensure_meta(p, total));
+    lampi_recv_desc *hd = (lampi_recv_desc *)p.hmeta;
+    uint32_t *he = (uint32_t *)(p.hmeta + o_exp);
+    for (size_t c = 0; c < nch; ++c) {
+        const ChunkPlan &k = plan.chunks[c];
+        const int b = (int)(c % kBufs);
+        const uint64_t in = (uint64_t)(uintptr_t)(p.dchunk + (size_t)b * p.chunk_bytes);
+        const uint64_t out = (uint64_t)(uintptr_t)(p.dout + (size_t)b * p.out_bytes);
+        for (size_t j = k.f0; j < k.f1; ++j) {
+            const bool moves = to_copy(f[j]) != 0;  // others read and write nothing: any valid address
+            hd[j] = lampi_recv_desc{moves ? in + plan.din[j] : in, moves ? out + plan.dout[j] : out, f[j].app_len,
+                                    f[j].length, 0u};
+            he[j] = f[j].expected;
+        }
+    }
+    uint8_t *dm = p.dmeta;
+
+    PipeDrain drain(p);  // any early return below leaves nothing in flight
+    TRY(hipMemcpyAsync(dm, p.hmeta, o_copied, hipMemcpyHostToDevice, p.s_in));
+    for (size_t c = 0; c < nch; ++c) {
+        const ChunkPlan &k = plan.chunks[c];
+        const int b = (int)(c % kBufs);
+        uint8_t *din = p.dchunk + (size_t)b * p.chunk_bytes;
+        uint8_t *dout = p.dout + (size_t)b * p.out_bytes;
+        // chunk b's buffers are free once chunk c - kBufs was copied to the app and sent back
+        if (c >= (size_t)kBufs) {
+            TRY(hipStreamWaitEvent(p.s_in, p.k_done[b], 0));
+            TRY(hipStreamWaitEvent(p.s_in, p.out_done[b], 0));
+        }
+        for (size_t x = k.xi0; x < k.xi1; ++x) {
+            const InXfer &t = plan.in[x];
+            if (t.rows == 1)
+                TRY(hipMemcpyAsync(din + t.doff, h_ring + t.hoff, t.width, hipMemcpyHostToDevice, p.s_in));
+            else
+                TRY(hipMemcpy2DAsync(din + t.doff, t.dpitch, h_ring + t.hoff, t.hpitch, t.width, t.rows,
+                                     hipMemcpyHostToDevice, p.s_in));
+        }
+        TRY(hipEventRecord(p.in_done[b], p.s_in));
+        TRY(hipStreamWaitEvent(p.s_k, p.in_done[b], 0));
+        const uint32_t hint = hint_override ? hint_override : chunk_rows_hint(k);
+        TRY(launch_copy_to_app((const lampi_recv_desc *)dm + k.f0, k.f1 - k.f0, dm + o_exp + k.f0 * sizeof(uint32_t),
+                               sizeof(uint32_t), (int64_t *)(dm + o_copied) + k.f0, (uint32_t *)(dm + o_csum) + k.f0,
+                               (uint32_t *)(dm + o_mask) + k.mask_word0, (uint32_t *)(dm + o_nbad) + c, mode, img, p.s_k,
+                               hint));
+        TRY(hipEventRecord(p.k_done[b], p.s_k));
+        TRY(hipStreamWaitEvent(p.s_out, p.k_done[b], 0));
+        for (size_t x = k.xo0; x < k.xo1; ++x) {
+            const OutXfer &t = plan.out[x];
+            TRY(hipMemcpyAsync(t.h, dout + t.doff, t.bytes, hipMemcpyDeviceToHost, p.s_out));
+        }
+        TRY(hipEventRecord(p.out_done[b], p.s_out));
+    }
+    TRY(hipMemcpyAsync(p.hmeta + o_copied, dm + o_copied, total - o_copied, hipMemcpyDeviceToHost, p.s_k));
+    TRY(hipStreamSynchronize(p.s_k));
+    TRY(hipStreamSynchronize(p.s_out));
+    drain.armed = false;
+
+    std::memcpy(h_copied, p.hmeta + o_copied, n * sizeof(int64_t));
+    std::memcpy(h_csum, p.hmeta + o_csum, n * sizeof(uint32_t));
+    std::memset(h_mask, 0, (n + 31) / 32 * sizeof(uint32_t));
+    const uint32_t *hm = (const uint32_t *)(p.hmeta + o_mask), *hn = (const uint32_t *)(p.hmeta + o_nbad);
+    uint32_t nbad = 0;
+    for (size_t c = 0; c < nch; ++c) {  // chunk masks start at bit 0 of their own words
+        const ChunkPlan &k = plan.chunks[c];
+        nbad += hn[c];
+        if (hn[c] == 0) continue;
+        for (size_t i = 0; i < k.f1 - k.f0; ++i)
+            if ((hm[k.mask_word0 + i / 32] >> (i % 32)) & 1u) h_mask[(k.f0 + i) / 32] |= 1u << ((k.f0 + i) % 32);
+    }
+    *h_nbad = nbad;
+    return hipSuccess;
+}
+
+// The header checks of a batch of received fragments: each header's first `need` bytes are gathered
+// from the ring into pinned records (the CPU moves header bytes only), checked on the device a chunk
+// at a time, and the chunk's mask words and failure count come back.
+enum class HdrKind { kResidue, kCompare };
+struct HdrArgs {
+    HdrKind kind;
+    uint32_t hdr_bytes, word_count, crclen, csum_offset;
+};
+constexpr size_t kHdrChunkBytes = 4u << 20;
+
+hipError_t host_headers(const uint8_t *ring, const uint64_t *offs, size_t n, size_t need, const HdrArgs &a,
+                        uint32_t *h_mask, uint32_t *h_nbad, int mode) {
+    const size_t rec = align_up(std::max<size_t>(need, 4), 4);
+    const size_t per = std::max<size_t>(64, (kHdrChunkBytes / rec) & ~(size_t)63);  // whole mask words
+    const size_t nch = (n + per - 1) / per;
+    PipeState *pp = nullptr;
+    TRY(pipe_ctx(&pp));
+    PipeState &p = *pp;
+    const uint32_t *img = nullptr;
+    TRY(device_tables(p.dev, &img));
+    const size_t slot = align_up(std::min(n, per) * rec, 256);
+    TRY(ensure_chunks(p, slot));
+    const size_t mwords = (n + 31) / 32;
+    const size_t o_res = kBufs * slot, o_nbad = o_res + align_up(mwords * sizeof(uint32_t), 256);
+    const size_t total = o_nbad + nch * sizeof(uint32_t);
+    TRY(ensure_meta(p, total));  // pinned: kBufs gather slots, then the results; device: the results
+    uint8_t *dres = p.dmeta;     // [mask words | nbad per chunk] at device offset 0
+    const size_t d_nbad = o_nbad - o_res;
+
+    PipeDrain drain(p);
+    for (size_t c = 0; c < nch; ++c) {
+        const int b = (int)(c % kBufs);
+        const size_t i0 = c * per, m = std::min(per, n - i0);
+        uint8_t *hs = p.hmeta + (size_t)b * slot;
+        uint8_t *ds = p.dchunk + (size_t)b * p.chunk_bytes;
+        if (c >= (size_t)kBufs) {
+            TRY(hipEventSynchronize(p.in_done[b]));  // the pinned slot's last H2D is done
+            TRY(hipStreamWaitEvent(p.s_in, p.k_done[b], 0));
+        }
+        for (size_t i = 0; i < m; ++i) std::memcpy(hs + i * rec, ring + offs[i0 + i], need);
+        TRY(hipMemcpyAsync(ds, hs, m * rec, hipMemcpyHostToDevice, p.s_in));
+        TRY(hipEventRecord(p.in_done[b], p.s_in));
+        TRY(hipStreamWaitEvent(p.s_k, p.in_done[b], 0));
+        uint32_t *mk = (uint32_t *)dres + i0 / 32, *nb = (uint32_t *)(dres + d_nbad) + c;
+        if (a.kind == HdrKind::kResidue)
+            TRY(launch_header_check(ds, m, rec, a.hdr_bytes, a.word_count, a.csum_offset, mode, img, mk, nb, p.s_k));
+        else
+            TRY(launch_header_compare(ds, m, rec, a.crclen, a.csum_offset, mode, img, mk, nb, p.s_k));
+        TRY(hipEventRecord(p.k_done[b], p.s_k));
+    }
+    TRY(hipMemcpyAsync(p.hmeta + o_res, dres, total - o_res, hipMemcpyDeviceToHost, p.s_k));
+    TRY(hipStreamSynchronize(p.s_k));
+    drain.armed = false;
+    std::memcpy(h_mask, p.hmeta + o_res, mwords * sizeof(uint32_t));
+    uint32_t nbad = 0;
+    for (size_t c = 0; c < nch; ++c) nbad += ((const uint32_t *)(p.hmeta + o_nbad))[c];
+    *h_nbad = nbad;
+    return hipSuccess;
+}
+
+int check_headers_args(const void *h_ring, size_t ring_bytes, const uint64_t *offs, size_t n, size_t need,
+                       uint32_t csum_offset, uint32_t *h_mask, uint32_t *h_nbad, int mode) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return (int)hipErrorInvalidValue;
+    if (!h_nbad || (csum_offset & 3u) || n > 0xFFFFFFFFull) return (int)hipErrorInvalidValue;
+    if (n && (!h_ring || !offs || !h_mask)) return (int)hipErrorInvalidValue;
+    for (size_t i = 0; i < n; ++i)
+        if (offs[i] > ring_bytes || need > ring_bytes - offs[i]) return (int)hipErrorInvalidValue;
+    return 0;
+}
+
+}  // namespace
+}  // namespace lampi
+
+using namespace lampi;
+
+extern "C" {
+
+int lampi_host_copy_to_app_batch(const void *h_ring, size_t ring_bytes, const lampi_host_recv_frag *h_frags, size_t n,
+                                 int64_t *h_copied, uint32_t *h_csum, uint32_t *h_mask, uint32_t *h_nbad, int mode) {
+    const uint32_t hint = LAMPI_CSUM_ROWS_HINT_OF(mode);
+    mode &= ~LAMPI_CSUM_ROWS_HINT_MASK;
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return (int)hipErrorInvalidValue;
+    if (!h_nbad || n > 0xFFFFFFFFull) return (int)hipErrorInvalidValue;
+    if (n == 0) {
+        *h_nbad = 0;
+        return 0;
+    }
+    if (!h_frags || !h_copied || !h_csum || !h_mask) return (int)hipErrorInvalidValue;
+    for (size_t j = 0; j < n; ++j) {
+        const lampi_host_recv_frag &x = h_frags[j];
+        if (to_copy(x) == 0) continue;  // its bytes are never read: no constraint on frag_off / app
+        if (!h_ring || !x.app || x.length > kHostMaxFrag || x.frag_off > ring_bytes ||
+            x.length > ring_bytes - x.frag_off)
+            return (int)hipErrorInvalidValue;
+    }
+    return (int)host_recv((const uint8_t *)h_ring, ring_bytes, h_frags, n, h_copied, h_csum, h_mask, h_nbad, mode,
+                          hint);
+}
+
+int lampi_host_header_check_batch(const void *h_ring, size_t ring_bytes, const uint64_t *h_hdr_offs, size_t n,
+                                  uint32_t hdr_bytes, uint32_t word_count, uint32_t csum_offset, uint32_t *h_mask,
+                                  uint32_t *h_nbad, int mode) {
+    // CRC mode reads the whole header (the stored checksum included); SUM mode word_count words and
+    // the stored checksum
+    const size_t need = mode == LAMPI_CSUM_CRC32 ? (size_t)hdr_bytes
+                                                 : std::max<size_t>(4 * (size_t)word_count, (size_t)csum_offset + 4);
+    const int rc = check_headers_args(h_ring, ring_bytes, h_hdr_offs, n, need, csum_offset, h_mask, h_nbad, mode);
+    if (rc) return rc;
+    if (n == 0) {
+        *h_nbad = 0;
+        return 0;
+    }
+    const HdrArgs a{HdrKind::kResidue, hdr_bytes, word_count, 0u, csum_offset};
+    return (int)host_headers((const uint8_t *)h_ring, h_hdr_offs, n, need, a, h_mask, h_nbad, mode);
+}
+
+int lampi_host_header_compare_batch(const void *h_ring, size_t ring_bytes, const uint64_t *h_hdr_offs, size_t n,
+                                    uint32_t crclen, uint32_t csum_offset, uint32_t *h_mask, uint32_t *h_nbad,
+                                    int mode) {
+    const size_t need = std::max<size_t>(crclen, (size_t)csum_offset + 4);
+    const int rc = check_headers_args(h_ring, ring_bytes, h_hdr_offs, n, need, csum_offset, h_mask, h_nbad, mode);
+    if (rc) return rc;
+    if (n == 0) {
+        *h_nbad = 0;
+        return 0;
+    }
+    const HdrArgs a{HdrKind::kCompare, 0u, 0u, crclen, csum_offset};
+    return (int)host_headers((const uint8_t *)h_ring, h_hdr_offs, n, need, a, h_mask, h_nbad, mode);
+}
+
+}  // extern "C"

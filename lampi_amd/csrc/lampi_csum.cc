@@ -763,9 +763,12 @@ int lampi_fill_stream_frags(void *d_dst, size_t n, size_t frag_len, uint64_t see
 void lampi_host_release(void) {
     t_ctx.release();
     release_pipeline();
+    release_thread_scratch();
 }
 
 int64_t lampi_host_pinned_bytes(void) { return g_pinned_bytes.load(std::memory_order_relaxed); }
+
+int64_t lampi_device_scratch_bytes(void) { return device_scratch_bytes(); }
 
 int lampi_host_register(void *h_ptr, size_t len) {
     if (!h_ptr || !len) return to_int(hipErrorInvalidValue);

@@ -87,6 +87,9 @@ def test_native_host_staging_does_not_leak(cuda):
     assert f["pinned_before"] > 0
     assert f["pinned_after_threads"] == f["pinned_before"], r.stdout
     assert f["pinned_after_release"] == 0, r.stdout
+    # per-thread device scratch (row-group joins of the receive path): gone with each thread, and
+    # after the main thread's release (it was kept per stream until process exit)
+    assert f["scratch_after_threads"] == 0 and f["scratch_after_release"] == 0, r.stdout
 
 
 def test_native_host_message_path_matches_oracle(cuda):
@@ -104,3 +107,26 @@ def test_native_host_message_path_matches_oracle(cuda):
     # 7 shapes x 2 modes x 2 sources x 4 ranges x 3 calls, on 2 threads + the main thread, + 1
     assert len(lines) == 7 * 2 * 2 * 4 * 3 * (2 + 1) + 1
     assert "pinned_after_release 0" in out
+
+
+def test_native_host_receive_path_matches_oracle(cuda):
+    """lampi_host_header_check_batch / _compare_batch and lampi_host_copy_to_app_batch from a native C++
+    caller (tests/native/host_recv_caller.cc): GM rings of 64 KiB buffers with 65,456-byte and 4 KiB
+    payloads, IB rings of 2,048-byte buffers behind a 40-byte GRH; ~1% corrupted headers (incl. the
+    reference's |= 0xA4A4), ~2% corrupted data checksums, ~1% corrupted payloads; AppBufferLen <= 0 / < /
+    = / >; ragged and empty fragments; ring-order and shuffled batches; pinned and pageable rings; both
+    modes; two threads at once, then the main thread.  Every verdict, checksum, copied count and
+    application byte is checked against the oracle inside the program."""
+    r = subprocess.run([_bin("host_recv_caller"), "2"], capture_output=True, text=True, timeout=600)
+    out = r.stdout
+    assert r.returncode == 0, out[-4000:] + r.stderr[-2000:]
+    assert out.strip().endswith("bad 0 done"), out[-2000:]
+    lines = [ln for ln in out.splitlines() if ln.startswith(("headers ", "copy_to_app ", "invalid", "empty",
+                                                                "nothing"))]
+    assert lines and all(ln.endswith(" ok") for ln in lines)
+    # 3 shapes x 2 modes x 2 rings x 2 orders x (headers + copy) on 2 threads + main, + 4 edge lines
+    assert len(lines) == 3 * 2 * 2 * 2 * 2 * (2 + 1) + 4
+    # the batches really held corrupt fragments of every kind
+    assert any(" nbad 0 " not in ln and ln.startswith("headers ") for ln in lines)
+    assert any(ln.startswith("copy_to_app ") and " nbad 0 " not in ln for ln in lines)
+    assert "pinned_after_release 0 scratch_after_release 0" in out
