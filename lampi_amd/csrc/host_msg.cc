@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/lampi_csum.h"
@@ -99,6 +100,14 @@ hipError_t pipe_ctx(PipeState **out) {
     return hipSuccess;
 }
 
+size_t chunk_target(bool duplex) {
+    if (const char *e = std::getenv("LAMPI_HOST_CHUNK_BYTES")) {
+        const unsigned long long v = std::strtoull(e, nullptr, 0);
+        if (v >= 4096) return (size_t)v;
+    }
+    return duplex ? kChunkDuplex : kChunkTarget;
+}
+
 // every chunk starts 256-byte aligned
 hipError_t ensure_chunks(PipeState &p, size_t chunk) {
     chunk = align_up(chunk, 256);
@@ -166,7 +175,7 @@ hipError_t host_msg(const uint8_t *h_msg, size_t msg_len, size_t frag_len, size_
     const size_t b0 = k_first * frag_len;
     const size_t b1 = std::min(msg_len, (k_first + k_count) * frag_len);
     const Range r{frag_len, k_count, b1 - (b0 + (k_count - 1) * frag_len)};
-    const size_t fpc = std::max<size_t>(1, kChunkTarget / frag_len);  // fragments per chunk
+    const size_t fpc = std::max<size_t>(1, chunk_target(h_ring != nullptr) / frag_len);  // fragments per chunk
     const size_t cb = fpc * frag_len;
     TRY(ensure_chunks(p, cb));
     TRY(ensure_meta(p, k_count * sizeof(uint32_t)));

@@ -10,9 +10,17 @@
 namespace lampi {
 
 constexpr int kBufs = 3;  // device chunks in flight
-// Payload bytes per chunk.  Back-to-back 16 MiB H2D copies ran at 51.3-51.5 GiB/s against 52.9-53.3
-// for 64 MiB ones (profiles/r03/pcie_duplex_run*.txt), and every chunk adds cross-stream waits.
+// Payload bytes per chunk.  A call's time is about (chunks + 1) pipeline stages: the first chunk's H2D
+// and the last one's D2H run alone.  Checksum-only calls (H2D only): 64 MiB chunks, 51.2-51.7 GiB/s
+// for 256 MiB messages against 49.1-50.7 at 32 MiB and 45-48 at 16 MiB; calls moving bytes both ways
+// (host_msg bcopy, the receive path): 32 MiB, bcopy 36.3-37.7 -> 39.9-40.2 GiB/s and receive 34.8-37.1
+// -> 36.8-39.4 against 64 MiB; 16 MiB about the same as 32 for bcopy, noisier for receive; 8 MiB
+// receive 16 GiB/s (profiles/r04/chunk_ab.txt, one box).
 constexpr size_t kChunkTarget = 64u << 20;
+constexpr size_t kChunkDuplex = 32u << 20;
+// The chunk size for a call (duplex: it also moves bytes back); LAMPI_HOST_CHUNK_BYTES overrides it
+// for A/B runs.
+size_t chunk_target(bool duplex);
 // Largest fragment the host paths take (a chunk holds whole fragments, so kBufs x this is the most
 // staging HBM a call can ask for: 3 GiB of the 288 GB).  The transports' fragments are at most
 // 64 KiB (GM), 2 KiB (IB); larger ones are refused with hipErrorInvalidValue.

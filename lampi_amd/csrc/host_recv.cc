@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstring>
 #include <vector>
 
@@ -60,13 +61,10 @@ struct OutXfer {
     size_t bytes;
 };
 struct ChunkPlan {
-    size_t f0 = 0, f1 = 0;        // fragments [f0, f1)
-    size_t xi0 = 0, xi1 = 0;      // its H2D transfers
-    size_t xo0 = 0, xo1 = 0;      // its D2H transfers
+    size_t f0 = 0, f1 = 0;  // fragments [f0, f1)
     size_t in_used = 0, out_used = 0;
-    uint64_t payload = 0;         // bytes checksummed
-    size_t ncopy = 0;             // fragments with bytes to deliver
-    size_t mask_word0 = 0;        // its mask words in the call's mask scratch
+    uint64_t payload = 0;   // bytes checksummed
+    size_t ncopy = 0;       // fragments with bytes to deliver
 };
 
 uint32_t to_copy(const lampi_host_recv_frag &x) {
@@ -147,94 +145,119 @@ struct InRun {
     }
 };
 
-// The whole call's plan: chunks, transfers and every fragment's place in its chunk.
-struct RecvPlan {
-    std::vector<ChunkPlan> chunks;
-    std::vector<InXfer> in;
-    std::vector<OutXfer> out;
-    std::vector<size_t> din, dout;  // per fragment: offsets in its input / output chunk
-    size_t in_need = 0, out_need = 0, mask_words = 0;
-};
-
+// Plans the call one chunk at a time (next()), so the first chunk's DMA starts while the later ones
+// are still being planned: the fragments' ring bytes coalesced into transfers, their delivered bytes
+// into runs contiguous in the application buffers, and each fragment's offsets in its input / output
+// chunk (din / dout).
 class Planner {
   public:
-    Planner(const lampi_host_recv_frag *f, size_t n, size_t ring_bytes, RecvPlan &p)
-        : f_(f), n_(n), ring_(ring_bytes), p_(p) {
-        p_.din.assign(n, 0);
-        p_.dout.assign(n, 0);
+    Planner(const lampi_host_recv_frag *f, size_t n, size_t ring_bytes, size_t *din, size_t *dout)
+        : f_(f), n_(n), ring_(ring_bytes), din_(din), dout_(dout) {
+        uint64_t total = 0, ncopy = 0, maxlen = 0, maxc = 0, sumc = 0;
+        for (size_t j = 0; j < n; ++j) {
+            const uint32_t c = to_copy(f[j]);
+            if (!c) continue;
+            total += f[j].length;
+            sumc += c;
+            ++ncopy;
+            maxlen = std::max<uint64_t>(maxlen, f[j].length);
+            maxc = std::max<uint64_t>(maxc, c);
+        }
+        cap_ = chunk_target(true);
+        (void)total;
+        // a chunk of several fragments stays within cap_ (each fragment brings at most its length, 4 KiB
+        // of dense-run gap, a 2D row's padding and 256 bytes of alignment); a chunk of one holds just it
+        in_need_ = std::max<uint64_t>(maxlen, std::min<uint64_t>(cap_, ncopy * (maxlen + 4096 + 272)));
+        out_need_ = std::max<uint64_t>(maxc, std::min<uint64_t>(cap_, sumc + ncopy * 256));
     }
+    size_t in_need() const { return in_need_; }
+    size_t out_need() const { return out_need_; }
 
-    void run() {
-        ChunkPlan c;
-        for (size_t j = 0; j < n_; ++j) {
+    // The next chunk (fragments [c.f0, c.f1), its transfers), or false after the last one.
+    bool next(ChunkPlan &c, std::vector<InXfer> &in, std::vector<OutXfer> &out) {
+        if (done_) return false;  // (a batch with nothing to move still gets one chunk, empty of transfers)
+        in.clear();
+        out.clear();
+        in_ = &in;
+        out_ = &out;
+        c = ChunkPlan{};
+        c.f0 = first_;
+        if (pending_) {  // the fragment that closed the last chunk opens this one
+            pending_ = false;
+            const size_t j = j_++;
+            const lampi_host_recv_frag &x = f_[j];
+            open_in(j, x.frag_off, x.length);
+            open_out(j, (uint8_t *)x.app, to_copy(x));
+            c.payload += x.length;
+            ++c.ncopy;
+        }
+        for (; j_ < n_; ++j_) {
+            const size_t j = j_;
             const uint32_t cj = to_copy(f_[j]);
             if (cj == 0) continue;  // nothing to move: its result is decided without its bytes
             const size_t o = f_[j].frag_off, len = f_[j].length;
             uint8_t *app = (uint8_t *)f_[j].app;
             // where j would go: extending the open runs, or opening new ones
-            const InRun ext = in_.extended(o, len, ring_);
+            const InRun ext = run_.extended(o, len, ring_);
             const bool in_ext = ext.kind != InRun::kNone;
-            const size_t in_total = in_ext ? in_base_ + ext.size() : align_up(in_base_ + in_.size(), 256) + len;
+            const size_t in_total = in_ext ? in_base_ + ext.size() : align_up(in_base_ + run_.size(), 256) + len;
             const bool out_ext = out_open_ && app == out_end_;
             const size_t out_total = out_ext ? out_used_ + cj : align_up(out_used_, 256) + cj;
-            if (c.ncopy > 0 && (in_total > kChunkTarget || out_total > kChunkTarget)) {
+            if (c.ncopy > 0 && (in_total > cap_ || out_total > cap_)) {
                 close_chunk(c, j);  // j opens the next chunk
-                c = ChunkPlan{};
-                c.f0 = j;
-                c.xi0 = p_.in.size();
-                c.xo0 = p_.out.size();
-                open_in(j, o, len);
-                open_out(j, app, cj);
+                pending_ = true;
+                return true;
+            }
+            if (in_ext) {
+                run_ = ext;
+                members_.push_back(j);
             } else {
-                if (in_ext) {
-                    in_ = ext;
-                    members_.push_back(j);
-                } else {
-                    close_in();
-                    open_in(j, o, len);
-                }
-                if (out_ext) {
-                    p_.dout[j] = out_cur_ + (size_t)(app - out_start_);
-                    out_end_ = app + cj;
-                    out_used_ += cj;
-                } else {
-                    close_out();
-                    open_out(j, app, cj);
-                }
+                close_in();
+                open_in(j, o, len);
+            }
+            if (out_ext) {
+                dout_[j] = out_cur_ + (size_t)(app - out_start_);
+                out_end_ = app + cj;
+                out_used_ += cj;
+            } else {
+                close_out();
+                open_out(j, app, cj);
             }
             c.payload += len;
             ++c.ncopy;
         }
         close_chunk(c, n_);
+        done_ = true;
+        return true;
     }
 
   private:
     void open_in(size_t j, size_t o, size_t len) {
         in_base_ = align_up(in_base_, 256);
-        in_ = InRun::single(o, len);
+        run_ = InRun::single(o, len);
         members_.assign(1, j);
     }
     // the open input run becomes a transfer; its members get their chunk offsets
     void close_in() {
-        if (in_.kind == InRun::kNone) return;
+        if (run_.kind == InRun::kNone) return;
         InXfer x{};
         x.doff = in_base_;
-        x.hoff = in_.lo;
-        if (in_.kind == InRun::kPitch) {
-            x.width = in_.width;
-            x.rows = in_.rows;
-            x.hpitch = in_.pitch;
-            x.dpitch = align_up(in_.width, 16);
-            for (size_t r = 0; r < members_.size(); ++r) p_.din[members_[r]] = x.doff + r * x.dpitch;
+        x.hoff = run_.lo;
+        if (run_.kind == InRun::kPitch) {
+            x.width = run_.width;
+            x.rows = run_.rows;
+            x.hpitch = run_.pitch;
+            x.dpitch = align_up(run_.width, 16);
+            for (size_t r = 0; r < members_.size(); ++r) din_[members_[r]] = x.doff + r * x.dpitch;
         } else {
-            x.width = in_.end - in_.lo;
+            x.width = run_.end - run_.lo;
             x.rows = 1;
             x.hpitch = x.dpitch = x.width;
-            for (size_t m : members_) p_.din[m] = x.doff + (f_[m].frag_off - in_.lo);
+            for (size_t m : members_) din_[m] = x.doff + (f_[m].frag_off - run_.lo);
         }
-        p_.in.push_back(x);
-        in_base_ += in_.size();
-        in_ = InRun{};
+        in_->push_back(x);
+        in_base_ += run_.size();
+        run_ = InRun{};
         members_.clear();
     }
     void open_out(size_t j, uint8_t *app, uint32_t cj) {
@@ -243,11 +266,11 @@ class Planner {
         out_start_ = app;
         out_end_ = app + cj;
         out_open_ = true;
-        p_.dout[j] = out_cur_;
+        dout_[j] = out_cur_;
     }
     void close_out() {
         if (!out_open_) return;
-        p_.out.push_back(OutXfer{out_start_, out_cur_, (size_t)(out_end_ - out_start_)});
+        out_->push_back(OutXfer{out_start_, out_cur_, (size_t)(out_end_ - out_start_)});
         out_open_ = false;
     }
     void close_chunk(ChunkPlan &c, size_t f1) {
@@ -256,21 +279,20 @@ class Planner {
         c.f1 = f1;
         c.in_used = in_base_;
         c.out_used = out_used_;
-        c.xi1 = p_.in.size();
-        c.xo1 = p_.out.size();
-        c.mask_word0 = p_.mask_words;
-        p_.mask_words += (c.f1 - c.f0 + 31) / 32;
-        p_.in_need = std::max(p_.in_need, c.in_used);
-        p_.out_need = std::max(p_.out_need, c.out_used);
-        p_.chunks.push_back(c);
         in_base_ = 0;
         out_used_ = 0;
+        first_ = f1;
     }
 
     const lampi_host_recv_frag *f_;
     size_t n_, ring_;
-    RecvPlan &p_;
-    InRun in_;
+    size_t *din_, *dout_;
+    size_t cap_ = kChunkTarget, in_need_ = 0, out_need_ = 0;
+    size_t j_ = 0, first_ = 0;
+    bool pending_ = false, done_ = false;
+    std::vector<InXfer> *in_ = nullptr;
+    std::vector<OutXfer> *out_ = nullptr;
+    InRun run_;
     std::vector<size_t> members_;
     size_t in_base_ = 0;  // input chunk bytes used before the open run
     size_t out_used_ = 0, out_cur_ = 0;
@@ -288,59 +310,65 @@ uint32_t chunk_rows_hint(const ChunkPlan &c) {
     return rows >= 2 ? (uint32_t)std::min<uint64_t>(rows, 0xFFF) : 1u;
 }
 
+// Per-thread planning scratch, kept between calls (no allocation per call once grown).
+struct RecvScratch {
+    std::vector<size_t> din, dout;
+    std::vector<InXfer> in;
+    std::vector<OutXfer> out;
+};
+thread_local RecvScratch t_recv;
+
 hipError_t host_recv(const uint8_t *h_ring, size_t ring_bytes, const lampi_host_recv_frag *f, size_t n,
                      int64_t *h_copied, uint32_t *h_csum, uint32_t *h_mask, uint32_t *h_nbad, int mode,
                      uint32_t hint_override) {
-    RecvPlan plan;
-    Planner(f, n, ring_bytes, plan).run();
+    RecvScratch &rs = t_recv;
+    if (rs.din.size() < n) {
+        rs.din.resize(n);
+        rs.dout.resize(n);
+    }
+    Planner pl(f, n, ring_bytes, rs.din.data(), rs.dout.data());
     PipeState *pp = nullptr;
     TRY(pipe_ctx(&pp));
     PipeState &p = *pp;
     const uint32_t *img = nullptr;
     TRY(device_tables(p.dev, &img));
-    TRY(ensure_chunks(p, std::max<size_t>(plan.in_need, 256)));
-    TRY(ensure_out_chunks(p, std::max<size_t>(plan.out_need, 256)));
+    TRY(ensure_chunks(p, std::max<size_t>(pl.in_need(), 256)));
+    TRY(ensure_out_chunks(p, std::max<size_t>(pl.out_need(), 256)));
 
-    // the call's descriptors and results, in one device block and its pinned image:
-    // [descs | expected] go up in one H2D, [copied | csum | mask | nbad] come back in one D2H
-    const size_t nch = plan.chunks.size();
-    const size_t o_exp = align_up(n * sizeof(lampi_recv_desc), 256);
-    const size_t o_copied = align_up(o_exp + n * sizeof(uint32_t), 256);
+    // the call's descriptors (each chunk's go up with it; the expected checksum rides in the
+    // descriptor's reserved word, where the kernel reads it with a 32-byte stride) and results (one D2H
+    // at the end); the kernel's own mask and count land in a scratch the host never reads: the verdict
+    // is copied[i] == -1
+    const size_t o_copied = align_up(n * sizeof(lampi_recv_desc), 256);
     const size_t o_csum = align_up(o_copied + n * sizeof(int64_t), 256);
-    const size_t o_mask = align_up(o_csum + n * sizeof(uint32_t), 256);
-    const size_t o_nbad = align_up(o_mask + plan.mask_words * sizeof(uint32_t), 256);
-    const size_t total = o_nbad + nch * sizeof(uint32_t);
+    const size_t o_scratch = align_up(o_csum + n * sizeof(uint32_t), 256);
+    const size_t total = o_scratch + ((n + 31) / 32 + 2) * sizeof(uint32_t);
     TRY(ensure_meta(p, total));
     lampi_recv_desc *hd = (lampi_recv_desc *)p.hmeta;
-    uint32_t *he = (uint32_t *)(p.hmeta + o_exp);
-    for (size_t c = 0; c < nch; ++c) {
-        const ChunkPlan &k = plan.chunks[c];
-        const int b = (int)(c % kBufs);
-        const uint64_t in = (uint64_t)(uintptr_t)(p.dchunk + (size_t)b * p.chunk_bytes);
-        const uint64_t out = (uint64_t)(uintptr_t)(p.dout + (size_t)b * p.out_bytes);
-        for (size_t j = k.f0; j < k.f1; ++j) {
-            const bool moves = to_copy(f[j]) != 0;  // others read and write nothing: any valid address
-            hd[j] = lampi_recv_desc{moves ? in + plan.din[j] : in, moves ? out + plan.dout[j] : out, f[j].app_len,
-                                    f[j].length, 0u};
-            he[j] = f[j].expected;
-        }
-    }
     uint8_t *dm = p.dmeta;
+    uint32_t *dmask = (uint32_t *)(dm + o_scratch), *dnbad = dmask + (n + 31) / 32 + 1;
 
     PipeDrain drain(p);  // any early return below leaves nothing in flight
-    TRY(hipMemcpyAsync(dm, p.hmeta, o_copied, hipMemcpyHostToDevice, p.s_in));
-    for (size_t c = 0; c < nch; ++c) {
-        const ChunkPlan &k = plan.chunks[c];
+    ChunkPlan k;
+    for (size_t c = 0; pl.next(k, rs.in, rs.out); ++c) {
         const int b = (int)(c % kBufs);
         uint8_t *din = p.dchunk + (size_t)b * p.chunk_bytes;
         uint8_t *dout = p.dout + (size_t)b * p.out_bytes;
+        for (size_t j = k.f0; j < k.f1; ++j) {
+            const bool moves = to_copy(f[j]) != 0;  // others read and write nothing: any valid address
+            hd[j] = lampi_recv_desc{(uint64_t)(uintptr_t)(moves ? din + rs.din[j] : din),
+                                    (uint64_t)(uintptr_t)(moves ? dout + rs.dout[j] : dout), f[j].app_len,
+                                    f[j].length, f[j].expected};
+        }
         // chunk b's buffers are free once chunk c - kBufs was copied to the app and sent back
         if (c >= (size_t)kBufs) {
             TRY(hipStreamWaitEvent(p.s_in, p.k_done[b], 0));
             TRY(hipStreamWaitEvent(p.s_in, p.out_done[b], 0));
         }
-        for (size_t x = k.xi0; x < k.xi1; ++x) {
-            const InXfer &t = plan.in[x];
+        if (k.f1 > k.f0)
+            TRY(hipMemcpyAsync(dm + k.f0 * sizeof(lampi_recv_desc), hd + k.f0, (k.f1 - k.f0) * sizeof(lampi_recv_desc),
+                               hipMemcpyHostToDevice, p.s_in));
+        for (const InXfer &t : rs.in) {
             if (t.rows == 1)
                 TRY(hipMemcpyAsync(din + t.doff, h_ring + t.hoff, t.width, hipMemcpyHostToDevice, p.s_in));
             else
@@ -350,35 +378,30 @@ hipError_t host_recv(const uint8_t *h_ring, size_t ring_bytes, const lampi_host_
         TRY(hipEventRecord(p.in_done[b], p.s_in));
         TRY(hipStreamWaitEvent(p.s_k, p.in_done[b], 0));
         const uint32_t hint = hint_override ? hint_override : chunk_rows_hint(k);
-        TRY(launch_copy_to_app((const lampi_recv_desc *)dm + k.f0, k.f1 - k.f0, dm + o_exp + k.f0 * sizeof(uint32_t),
-                               sizeof(uint32_t), (int64_t *)(dm + o_copied) + k.f0, (uint32_t *)(dm + o_csum) + k.f0,
-                               (uint32_t *)(dm + o_mask) + k.mask_word0, (uint32_t *)(dm + o_nbad) + c, mode, img, p.s_k,
-                               hint));
+        const lampi_recv_desc *dd = (const lampi_recv_desc *)dm + k.f0;
+        TRY(launch_copy_to_app(dd, k.f1 - k.f0, (const uint8_t *)dd + offsetof(lampi_recv_desc, reserved),
+                               sizeof(lampi_recv_desc), (int64_t *)(dm + o_copied) + k.f0,
+                               (uint32_t *)(dm + o_csum) + k.f0, dmask, dnbad, mode, img, p.s_k, hint));
         TRY(hipEventRecord(p.k_done[b], p.s_k));
         TRY(hipStreamWaitEvent(p.s_out, p.k_done[b], 0));
-        for (size_t x = k.xo0; x < k.xo1; ++x) {
-            const OutXfer &t = plan.out[x];
-            TRY(hipMemcpyAsync(t.h, dout + t.doff, t.bytes, hipMemcpyDeviceToHost, p.s_out));
-        }
+        for (const OutXfer &t : rs.out) TRY(hipMemcpyAsync(t.h, dout + t.doff, t.bytes, hipMemcpyDeviceToHost, p.s_out));
         TRY(hipEventRecord(p.out_done[b], p.s_out));
     }
-    TRY(hipMemcpyAsync(p.hmeta + o_copied, dm + o_copied, total - o_copied, hipMemcpyDeviceToHost, p.s_k));
+    TRY(hipMemcpyAsync(p.hmeta + o_copied, dm + o_copied, o_scratch - o_copied, hipMemcpyDeviceToHost, p.s_k));
     TRY(hipStreamSynchronize(p.s_k));
     TRY(hipStreamSynchronize(p.s_out));
     drain.armed = false;
 
-    std::memcpy(h_copied, p.hmeta + o_copied, n * sizeof(int64_t));
+    const int64_t *hc = (const int64_t *)(p.hmeta + o_copied);
+    std::memcpy(h_copied, hc, n * sizeof(int64_t));
     std::memcpy(h_csum, p.hmeta + o_csum, n * sizeof(uint32_t));
     std::memset(h_mask, 0, (n + 31) / 32 * sizeof(uint32_t));
-    const uint32_t *hm = (const uint32_t *)(p.hmeta + o_mask), *hn = (const uint32_t *)(p.hmeta + o_nbad);
     uint32_t nbad = 0;
-    for (size_t c = 0; c < nch; ++c) {  // chunk masks start at bit 0 of their own words
-        const ChunkPlan &k = plan.chunks[c];
-        nbad += hn[c];
-        if (hn[c] == 0) continue;
-        for (size_t i = 0; i < k.f1 - k.f0; ++i)
-            if ((hm[k.mask_word0 + i / 32] >> (i % 32)) & 1u) h_mask[(k.f0 + i) / 32] |= 1u << ((k.f0 + i) % 32);
-    }
+    for (size_t i = 0; i < n; ++i)
+        if (hc[i] < 0) {
+            h_mask[i / 32] |= 1u << (i % 32);
+            ++nbad;
+        }
     *h_nbad = nbad;
     return hipSuccess;
 }

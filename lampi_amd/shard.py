@@ -53,7 +53,8 @@ def allreduce_digest(local: tuple[int, int], group=None) -> tuple[int, int]:
     import torch
     import torch.distributed as dist
 
-    dev = "cpu" if dist.get_backend(group) == "gloo" else "cuda"
+    # RCCL: a tensor on this rank's own device (bench.py set it with torch.cuda.set_device)
+    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
     mine = torch.tensor([local[0], local[1]], dtype=torch.int64, device=dev)
     parts = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
     dist.all_gather(parts, mine, group=group)

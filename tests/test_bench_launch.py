@@ -33,7 +33,7 @@ def _json_line(stdout):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("gpus", [1, 2, 4])
+@pytest.mark.parametrize("gpus", [1, 2, 4, 8])
 @pytest.mark.parametrize("mode", ["crc", "sum"])
 def test_dry_run_launches_n_ranks(gpus, mode, oracle):
     r = _run(["--gpus", str(gpus), "--dry-run", "--steps", "3", "--warmup", "1", "--mode", mode])
@@ -52,6 +52,27 @@ def test_dry_run_launches_n_ranks(gpus, mode, oracle):
     assert (int(d["parity"]["xor"], 16), int(d["parity"]["wsum"], 16)) == want
     assert d["parity"]["ok"] is True and d["parity"]["all_ranks_ok"] is True
     assert d["aggregate"]["roofline_frac"] > 0
+
+
+@pytest.mark.parametrize("mode", ["crc", "sum"])
+def test_config_d_eight_rank_dry_run(mode):
+    """Config D's own N = 8 plan (32M x 16 KiB, 4M fragments = 64 GiB per rank) through the launch, shard
+    plan, row gather and digest combine of an 8-GPU run: each rank contributes its committed shard digest,
+    the combined digest must be the whole batch's (CRC: BASELINE.md's F2A5DDAD / 3383EB2F) and every rank's
+    CRC XOR BASELINE.md's per-GPU value."""
+    r = _run(["--config", "D", "--gpus", "8", "--dry-run", "--steps", "2", "--warmup", "1", "--mode", mode],
+             timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 8 and d["dry_run"] is True
+    assert [e["rank"] for e in d["per_gpu"]] == list(range(8))
+    assert all(e["bytes"] == 64 << 30 for e in d["per_gpu"])
+    assert d["config"]["fragments_per_gpu"] == 4194304 and d["config"]["frag_bytes"] == 16384
+    assert "mod 8" in d["config"]["sharding"]
+    assert d["parity"]["ok"] is True and d["parity"]["all_ranks_ok"] is True
+    if mode == "crc":
+        assert (d["parity"]["xor"], d["parity"]["wsum"]) == ("f2a5ddad", "3383eb2f")
+        assert "per-GPU shard XOR" in d["parity"]["check"]
 
 
 def test_world_size_must_match_gpus():
