@@ -210,6 +210,33 @@ int lampi_host_header_compare_batch(const void *h_ring, size_t ring_bytes, const
                                     uint32_t crclen, uint32_t csum_offset, uint32_t *h_mask, uint32_t *h_nbad,
                                     int mode);
 
+/* One typemap piece in host memory (32 bytes): offset 0 src, 8 dst, 16 copylen, 20 csumlen, 24 partial,
+ * 28 reserved. */
+typedef struct lampi_host_piece {
+    const void *src;    /* host address of the piece's bytes */
+    void       *dst;    /* host address its first copylen bytes go to (NULL: checksum only) */
+    uint32_t    copylen;
+    uint32_t    csumlen;  /* the checksum covers max(copylen, csumlen) bytes of src */
+    uint32_t    partial;  /* CRC mode, a fragment's first piece: its starting register */
+    uint32_t    reserved; /* 0 */
+} lampi_host_piece;
+
+/* lampi_chain_csum_batch over pieces in host memory: fragment f is the concatenation of the checksummed
+ * ranges of h_pieces[h_first[f]] .. h_pieces[h_first[f+1] - 1] (h_first: nfrags + 1 nondecreasing entries,
+ * h_first[nfrags] <= npieces), each piece also copied to its dst; h_out[f] = what the reference's
+ * piece-by-piece calls return (CRC: the register threaded through the pieces from the first piece's
+ * partial, 0xFFFFFFFF for a fragment without pieces; SUM: the total of the increments with the
+ * partial-word state threaded from a fresh state).  The send side's gather into the NIC payload
+ * (src/path/gm/sendFrag.cc:157-217: bcopy_uicrc(..., csum) / csum += bcopy_uicsum(...) per typemap
+ * piece; ib/sendFrag.cc:140-203) and the receive side's scatter into the application buffer
+ * (non_contiguous_copy, src/path/common/BaseDesc.cc:72-163), a whole batch per call.  The DMA engines read
+ * exactly the pieces' bytes and write exactly their copies: touching pieces move in one copy, equal pieces
+ * at a constant stride (a strided vector) in one 2D copy.  Sources and destinations must not overlap.
+ * Fragments up to 1 GiB.  Synchronous; 0 or a hipError_t (invalid arguments: hipErrorInvalidValue,
+ * nothing written). */
+int lampi_host_chain_csum_batch(const lampi_host_piece *h_pieces, size_t npieces, const uint32_t *h_first,
+                                size_t nfrags, uint32_t *h_out, int mode);
+
 /* Page-lock [h_ptr, h_ptr+len) for direct DMA by the host paths (hipHostRegister) and undo it:
  * the analogue of registering NIC buffers with the network (GM gm_register_memory).  Return 0
  * or a hipError_t. */

@@ -65,6 +65,16 @@ class HostRecvFrag(ctypes.Structure):
 
 assert ctypes.sizeof(HostRecvFrag) == 32
 
+
+class HostPiece(ctypes.Structure):
+    """struct lampi_host_piece (32 bytes): src ptr, dst ptr, copylen, csumlen, partial, reserved u32."""
+
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("copylen", ctypes.c_uint32),
+                ("csumlen", ctypes.c_uint32), ("partial", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(HostPiece) == 32
+
 _lock = threading.Lock()
 _lib = None
 
@@ -120,6 +130,7 @@ PROTOTYPES = {
                                                      ctypes.c_int]),
     "lampi_host_header_compare_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.c_uint32,
                                                        ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_int]),
+    "lampi_host_chain_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, ctypes.c_int]),
     "lampi_device_scratch_bytes": (ctypes.c_int64, []),
     "lampi_host_register": (ctypes.c_int, [c_void_p, c_size_t]),
     "lampi_host_unregister": (ctypes.c_int, [c_void_p]),

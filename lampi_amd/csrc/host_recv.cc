@@ -40,272 +40,37 @@
 #include "frag_csum_kernels.h"
 #include "host_internal.h"
 #include "host_pipe.h"
+#include "host_plan.h"
 
 namespace lampi {
 namespace {
 
 #define TRY LAMPI_TRY
 
-// A DMA transfer host -> chunk (rows == 1: 1D of width bytes) or chunk -> application buffer.
-struct InXfer {
-    size_t hoff;    // ring offset of the first byte
-    size_t width;   // bytes per row
-    size_t rows;
-    size_t hpitch;  // ring bytes between rows (2D)
-    size_t doff;    // offset in the input chunk
-    size_t dpitch;
-};
-struct OutXfer {
-    uint8_t *h;
-    size_t doff;  // offset in the output chunk
-    size_t bytes;
-};
-struct ChunkPlan {
-    size_t f0 = 0, f1 = 0;  // fragments [f0, f1)
-    size_t in_used = 0, out_used = 0;
-    uint64_t payload = 0;   // bytes checksummed
-    size_t ncopy = 0;       // fragments with bytes to deliver
-};
-
 uint32_t to_copy(const lampi_host_recv_frag &x) {
     return x.app_len <= 0 ? 0u : (x.app_len < (int64_t)x.length ? (uint32_t)x.app_len : x.length);
 }
 
-// Dense 1D runs may carry gaps of at most this many bytes each and 1/16 of their payload in all.
-constexpr size_t kDenseGap = 4096;
-
-// The open run of ring bytes being coalesced into one H2D transfer.
-struct InRun {
-    enum Kind { kNone, kOne, kDense, kPitch } kind = kNone;
-    size_t lo = 0, end = 0;        // ring range [lo, end) (1D kinds)
-    size_t last = 0, pitch = 0;    // the last member's offset, the slot pitch (kPitch)
-    size_t width = 0;              // the widest member (kPitch rows)
-    size_t gaps = 0, payload = 0;  // gap and payload bytes (kDense)
-    size_t rows = 0;               // members
-    size_t size() const {          // device bytes it needs
-        if (kind == kNone) return 0;
-        if (kind == kPitch) return rows * align_up(width, 16);
-        return end - lo;
+// The batch as the planner sees it: fragment j reads its `length` ring bytes (all checksummed) and
+// writes lengthToCopy of them to its application address -- or nothing at all when lengthToCopy is 0.
+struct RecvItems {
+    const lampi_host_recv_frag *f;
+    size_t n;
+    size_t size() const { return n; }
+    PlanItem get(size_t j) const {
+        const uint32_t c = to_copy(f[j]);
+        if (!c) return PlanItem{0, 0, nullptr, 0};
+        return PlanItem{f[j].frag_off, f[j].length, (uint8_t *)f[j].app, c};
     }
-    // The run with fragment [o, o + len) appended, or kind kNone if it cannot take it.
-    InRun extended(size_t o, size_t len, size_t ring_bytes) const {
-        InRun r = *this;
-        switch (kind) {
-            case kNone:
-                break;
-            case kOne:
-                if (o >= end && o - end <= kDenseGap && (o - end) * 16 <= payload + len) {
-                    r.kind = kDense;
-                    r.gaps = o - end;
-                    r.payload += len;
-                    r.end = o + len;
-                    r.last = o;
-                    r.rows = 2;
-                    return r;
-                }
-                if (o > last && o - last >= std::max(width, len) && o + std::max(width, len) <= ring_bytes) {
-                    r.kind = kPitch;
-                    r.pitch = o - last;
-                    r.width = std::max(width, len);
-                    r.last = o;
-                    r.rows = 2;
-                    return r;
-                }
-                break;
-            case kDense:
-                if (o >= end && o - end <= kDenseGap && (gaps + o - end) * 16 <= payload + len) {
-                    r.gaps += o - end;
-                    r.payload += len;
-                    r.end = o + len;
-                    r.last = o;
-                    ++r.rows;
-                    return r;
-                }
-                break;
-            case kPitch:
-                if (o > last && o - last == pitch && len <= pitch && o + std::max(width, len) <= ring_bytes) {
-                    r.width = std::max(width, len);
-                    r.last = o;
-                    ++r.rows;
-                    return r;
-                }
-                break;
-        }
-        r.kind = kNone;
-        return r;
-    }
-    static InRun single(size_t o, size_t len) {
-        InRun r;
-        r.kind = kOne;
-        r.lo = r.last = o;
-        r.end = o + len;
-        r.width = r.payload = len;
-        r.rows = 1;
-        return r;
-    }
-};
-
-// Plans the call one chunk at a time (next()), so the first chunk's DMA starts while the later ones
-// are still being planned: the fragments' ring bytes coalesced into transfers, their delivered bytes
-// into runs contiguous in the application buffers, and each fragment's offsets in its input / output
-// chunk (din / dout).
-class Planner {
-  public:
-    Planner(const lampi_host_recv_frag *f, size_t n, size_t ring_bytes, size_t *din, size_t *dout)
-        : f_(f), n_(n), ring_(ring_bytes), din_(din), dout_(dout) {
-        uint64_t total = 0, ncopy = 0, maxlen = 0, maxc = 0, sumc = 0;
-        for (size_t j = 0; j < n; ++j) {
-            const uint32_t c = to_copy(f[j]);
-            if (!c) continue;
-            total += f[j].length;
-            sumc += c;
-            ++ncopy;
-            maxlen = std::max<uint64_t>(maxlen, f[j].length);
-            maxc = std::max<uint64_t>(maxc, c);
-        }
-        cap_ = chunk_target(true);
-        (void)total;
-        // a chunk of several fragments stays within cap_ (each fragment brings at most its length, 4 KiB
-        // of dense-run gap, a 2D row's padding and 256 bytes of alignment); a chunk of one holds just it
-        in_need_ = std::max<uint64_t>(maxlen, std::min<uint64_t>(cap_, ncopy * (maxlen + 4096 + 272)));
-        out_need_ = std::max<uint64_t>(maxc, std::min<uint64_t>(cap_, sumc + ncopy * 256));
-    }
-    size_t in_need() const { return in_need_; }
-    size_t out_need() const { return out_need_; }
-
-    // The next chunk (fragments [c.f0, c.f1), its transfers), or false after the last one.
-    bool next(ChunkPlan &c, std::vector<InXfer> &in, std::vector<OutXfer> &out) {
-        if (done_) return false;  // (a batch with nothing to move still gets one chunk, empty of transfers)
-        in.clear();
-        out.clear();
-        in_ = &in;
-        out_ = &out;
-        c = ChunkPlan{};
-        c.f0 = first_;
-        if (pending_) {  // the fragment that closed the last chunk opens this one
-            pending_ = false;
-            const size_t j = j_++;
-            const lampi_host_recv_frag &x = f_[j];
-            open_in(j, x.frag_off, x.length);
-            open_out(j, (uint8_t *)x.app, to_copy(x));
-            c.payload += x.length;
-            ++c.ncopy;
-        }
-        for (; j_ < n_; ++j_) {
-            const size_t j = j_;
-            const uint32_t cj = to_copy(f_[j]);
-            if (cj == 0) continue;  // nothing to move: its result is decided without its bytes
-            const size_t o = f_[j].frag_off, len = f_[j].length;
-            uint8_t *app = (uint8_t *)f_[j].app;
-            // where j would go: extending the open runs, or opening new ones
-            const InRun ext = run_.extended(o, len, ring_);
-            const bool in_ext = ext.kind != InRun::kNone;
-            const size_t in_total = in_ext ? in_base_ + ext.size() : align_up(in_base_ + run_.size(), 256) + len;
-            const bool out_ext = out_open_ && app == out_end_;
-            const size_t out_total = out_ext ? out_used_ + cj : align_up(out_used_, 256) + cj;
-            if (c.ncopy > 0 && (in_total > cap_ || out_total > cap_)) {
-                close_chunk(c, j);  // j opens the next chunk
-                pending_ = true;
-                return true;
-            }
-            if (in_ext) {
-                run_ = ext;
-                members_.push_back(j);
-            } else {
-                close_in();
-                open_in(j, o, len);
-            }
-            if (out_ext) {
-                dout_[j] = out_cur_ + (size_t)(app - out_start_);
-                out_end_ = app + cj;
-                out_used_ += cj;
-            } else {
-                close_out();
-                open_out(j, app, cj);
-            }
-            c.payload += len;
-            ++c.ncopy;
-        }
-        close_chunk(c, n_);
-        done_ = true;
-        return true;
-    }
-
-  private:
-    void open_in(size_t j, size_t o, size_t len) {
-        in_base_ = align_up(in_base_, 256);
-        run_ = InRun::single(o, len);
-        members_.assign(1, j);
-    }
-    // the open input run becomes a transfer; its members get their chunk offsets
-    void close_in() {
-        if (run_.kind == InRun::kNone) return;
-        InXfer x{};
-        x.doff = in_base_;
-        x.hoff = run_.lo;
-        if (run_.kind == InRun::kPitch) {
-            x.width = run_.width;
-            x.rows = run_.rows;
-            x.hpitch = run_.pitch;
-            x.dpitch = align_up(run_.width, 16);
-            for (size_t r = 0; r < members_.size(); ++r) din_[members_[r]] = x.doff + r * x.dpitch;
-        } else {
-            x.width = run_.end - run_.lo;
-            x.rows = 1;
-            x.hpitch = x.dpitch = x.width;
-            for (size_t m : members_) din_[m] = x.doff + (f_[m].frag_off - run_.lo);
-        }
-        in_->push_back(x);
-        in_base_ += run_.size();
-        run_ = InRun{};
-        members_.clear();
-    }
-    void open_out(size_t j, uint8_t *app, uint32_t cj) {
-        out_cur_ = align_up(out_used_, 256);
-        out_used_ = out_cur_ + cj;
-        out_start_ = app;
-        out_end_ = app + cj;
-        out_open_ = true;
-        dout_[j] = out_cur_;
-    }
-    void close_out() {
-        if (!out_open_) return;
-        out_->push_back(OutXfer{out_start_, out_cur_, (size_t)(out_end_ - out_start_)});
-        out_open_ = false;
-    }
-    void close_chunk(ChunkPlan &c, size_t f1) {
-        close_in();
-        close_out();
-        c.f1 = f1;
-        c.in_used = in_base_;
-        c.out_used = out_used_;
-        in_base_ = 0;
-        out_used_ = 0;
-        first_ = f1;
-    }
-
-    const lampi_host_recv_frag *f_;
-    size_t n_, ring_;
-    size_t *din_, *dout_;
-    size_t cap_ = kChunkTarget, in_need_ = 0, out_need_ = 0;
-    size_t j_ = 0, first_ = 0;
-    bool pending_ = false, done_ = false;
-    std::vector<InXfer> *in_ = nullptr;
-    std::vector<OutXfer> *out_ = nullptr;
-    InRun run_;
-    std::vector<size_t> members_;
-    size_t in_base_ = 0;  // input chunk bytes used before the open run
-    size_t out_used_ = 0, out_cur_ = 0;
-    uint8_t *out_start_ = nullptr, *out_end_ = nullptr;
-    bool out_open_ = false;
+    bool boundary(size_t) const { return true; }
 };
 
 // Rows per fragment for the row-group schedule of the chunk's copy kernel: the fragments' mean
 // length in 4 KiB rows (GM's 65,456-byte payloads: 16 -> 69-70% of read + write against 59%
 // walking the rows in one wave); 1 for fragments of about a row or less.
 uint32_t chunk_rows_hint(const ChunkPlan &c) {
-    if (c.ncopy == 0) return 1;
-    const uint64_t mean = c.payload / c.ncopy;
+    if (c.nread == 0) return 1;
+    const uint64_t mean = c.payload / c.nread;
     const uint64_t rows = (mean + kRowBytes - 1) / kRowBytes;
     return rows >= 2 ? (uint32_t)std::min<uint64_t>(rows, 0xFFF) : 1u;
 }
@@ -326,7 +91,11 @@ hipError_t host_recv(const uint8_t *h_ring, size_t ring_bytes, const lampi_host_
         rs.din.resize(n);
         rs.dout.resize(n);
     }
-    Planner pl(f, n, ring_bytes, rs.din.data(), rs.dout.data());
+    const RecvItems items{f, n};
+    PlanRules rules;
+    rules.ring = true;
+    rules.ring_bytes = ring_bytes;
+    StreamPlanner<RecvItems> pl(items, rules, chunk_target(true), rs.din.data(), rs.dout.data());
     PipeState *pp = nullptr;
     TRY(pipe_ctx(&pp));
     PipeState &p = *pp;
@@ -354,7 +123,8 @@ hipError_t host_recv(const uint8_t *h_ring, size_t ring_bytes, const lampi_host_
         const int b = (int)(c % kBufs);
         uint8_t *din = p.dchunk + (size_t)b * p.chunk_bytes;
         uint8_t *dout = p.dout + (size_t)b * p.out_bytes;
-        for (size_t j = k.f0; j < k.f1; ++j) {
+        const size_t f0 = k.j0, f1 = k.j1;
+        for (size_t j = f0; j < f1; ++j) {
             const bool moves = to_copy(f[j]) != 0;  // others read and write nothing: any valid address
             hd[j] = lampi_recv_desc{(uint64_t)(uintptr_t)(moves ? din + rs.din[j] : din),
                                     (uint64_t)(uintptr_t)(moves ? dout + rs.dout[j] : dout), f[j].app_len,
@@ -365,26 +135,20 @@ hipError_t host_recv(const uint8_t *h_ring, size_t ring_bytes, const lampi_host_
             TRY(hipStreamWaitEvent(p.s_in, p.k_done[b], 0));
             TRY(hipStreamWaitEvent(p.s_in, p.out_done[b], 0));
         }
-        if (k.f1 > k.f0)
-            TRY(hipMemcpyAsync(dm + k.f0 * sizeof(lampi_recv_desc), hd + k.f0, (k.f1 - k.f0) * sizeof(lampi_recv_desc),
+        if (f1 > f0)
+            TRY(hipMemcpyAsync(dm + f0 * sizeof(lampi_recv_desc), hd + f0, (f1 - f0) * sizeof(lampi_recv_desc),
                                hipMemcpyHostToDevice, p.s_in));
-        for (const InXfer &t : rs.in) {
-            if (t.rows == 1)
-                TRY(hipMemcpyAsync(din + t.doff, h_ring + t.hoff, t.width, hipMemcpyHostToDevice, p.s_in));
-            else
-                TRY(hipMemcpy2DAsync(din + t.doff, t.dpitch, h_ring + t.hoff, t.hpitch, t.width, t.rows,
-                                     hipMemcpyHostToDevice, p.s_in));
-        }
+        TRY(issue_in(rs.in, h_ring, din, p.s_in));
         TRY(hipEventRecord(p.in_done[b], p.s_in));
         TRY(hipStreamWaitEvent(p.s_k, p.in_done[b], 0));
         const uint32_t hint = hint_override ? hint_override : chunk_rows_hint(k);
-        const lampi_recv_desc *dd = (const lampi_recv_desc *)dm + k.f0;
-        TRY(launch_copy_to_app(dd, k.f1 - k.f0, (const uint8_t *)dd + offsetof(lampi_recv_desc, reserved),
-                               sizeof(lampi_recv_desc), (int64_t *)(dm + o_copied) + k.f0,
-                               (uint32_t *)(dm + o_csum) + k.f0, dmask, dnbad, mode, img, p.s_k, hint));
+        const lampi_recv_desc *dd = (const lampi_recv_desc *)dm + f0;
+        TRY(launch_copy_to_app(dd, f1 - f0, (const uint8_t *)dd + offsetof(lampi_recv_desc, reserved),
+                               sizeof(lampi_recv_desc), (int64_t *)(dm + o_copied) + f0,
+                               (uint32_t *)(dm + o_csum) + f0, dmask, dnbad, mode, img, p.s_k, hint));
         TRY(hipEventRecord(p.k_done[b], p.s_k));
         TRY(hipStreamWaitEvent(p.s_out, p.k_done[b], 0));
-        for (const OutXfer &t : rs.out) TRY(hipMemcpyAsync(t.h, dout + t.doff, t.bytes, hipMemcpyDeviceToHost, p.s_out));
+        TRY(issue_out(rs.out, dout, p.s_out));
         TRY(hipEventRecord(p.out_done[b], p.s_out));
     }
     TRY(hipMemcpyAsync(p.hmeta + o_copied, dm + o_copied, o_scratch - o_copied, hipMemcpyDeviceToHost, p.s_k));

@@ -130,3 +130,30 @@ def test_native_host_receive_path_matches_oracle(cuda):
     assert any(" nbad 0 " not in ln and ln.startswith("headers ") for ln in lines)
     assert any(ln.startswith("copy_to_app ") and " nbad 0 " not in ln for ln in lines)
     assert "pinned_after_release 0 scratch_after_release 0" in out
+
+
+def test_native_host_typemap_chains_match_reference(cuda, tmp_path):
+    """lampi_host_chain_csum_batch from a native C++ caller (tests/native/host_chain_caller.cc): the
+    reference's 150 chain fixtures (values computed by the compiled MemFunctions.cc, passed to the program
+    as text), strided-vector typemaps gathered and scattered (8 B .. 4 KiB elements), random typemaps with
+    checksum-only and csumlen > copylen pieces and CRC starting registers; both modes, pinned and pageable
+    buffers, two threads at once, then the main thread.  Every checksum and destination byte is checked."""
+    import json
+
+    with open(os.path.join(HERE, "golden", "fixtures.json")) as f:
+        cases = json.load(f)["chain"]
+    path = tmp_path / "chain_cases.txt"
+    with open(path, "w") as f:
+        for c in cases:
+            f.write(" ".join(str(v) for v in [c["seed"], c["off"], c["len"], c["crc"], c["sum"], len(c["cuts"])]
+                             + list(c["cuts"])) + "\n")
+    r = subprocess.run([_bin("host_chain_caller"), str(path), "2"], capture_output=True, text=True, timeout=600)
+    out = r.stdout
+    assert r.returncode == 0, out[-4000:] + r.stderr[-2000:]
+    assert out.strip().endswith("bad 0 done"), out[-2000:]
+    assert f"fixture_cases {len(cases)}" in out and len(cases) == 150
+    lines = [ln for ln in out.splitlines() if ln.startswith(("fixtures ", "vector_", "random ", "invalid", "fragments"))]
+    assert lines and all(ln.endswith(" ok") for ln in lines)
+    # per thread: 2 x 2 fixture batches, 6 shapes x 2 buffers x 2 modes x (gather + scatter), 6 x 2 random
+    assert len(lines) == 3 * (4 + 6 * 2 * 2 * 2 + 6 * 2) + 2
+    assert "pinned_after_release 0 scratch_after_release 0" in out
