@@ -306,32 +306,27 @@ struct RecvSource {
     }
 };
 
-// Descriptor batches without a row-count hint hand their large fragments to the table-light kernel
-// (launch_crc_desc): the piece-stream workgroups whose bytes lie almost all in fragments of >= 8 rows
-// append those fragments to a device list (one entry per group of up to kListRows rows) and skip them;
-// crc_light_list_kernel then runs the list.  hdr: [0] entries appended, [1] entries claimed, [2]
-// workgroups finished (zero between calls: the list kernel's last workgroup resets them).
-struct ListCtl {
-    uint32_t *hdr;
-    uint2 *ent;     // (fragment, its first entry)
-    uint32_t *gv;   // per entry: the group's value (normal domain), for fragments of several groups
-    uint32_t *cd;   // per fragment: groups still to finish
-    uint32_t cap;   // entries at most
-};
-struct ListDescSource {
+// Read-only CRC descriptor batches of moderate size without a row-count hint run in two launches by
+// size class (launch_crc_desc): fragments of 8-16 rows (GM's 65,456-byte payloads) on the table-light
+// kernel, one wave each -- its best shape, 80% with the hint -- (SplitDescSource<true>), the rest on the
+// piece streams (SplitDescSource<false>).  Each source reads a fragment of the other class as not its own
+// (aux = 1): the light kernel's wave exits, the piece streams skip it and leave its out[] word alone.
+__device__ __forceinline__ bool split_large(uint32_t len) { return len > 7u * kRowBytes && len <= 16u * kRowBytes; }
+template <bool kLarge>
+struct SplitDescSource {
     static constexpr bool kCopy = false;
     static constexpr bool kPhase = false;
     const lampi_frag_desc *d;
-    ListCtl L;
     __device__ FragInfo get(size_t f) const {
         const lampi_frag_desc x = d[f];
+        if (split_large(x.length) != kLarge) return {(gbyte *)(uintptr_t)x.addr, 0u, 0u, nullptr, 0u, 1u};
         return {(gbyte *)(uintptr_t)x.addr, x.length, x.partial, nullptr, 0u};
     }
 };
 template <class S>
-struct IsList : std::false_type {};
-template <>
-struct IsList<ListDescSource> : std::true_type {};
+struct IsSplit : std::false_type {};
+template <bool B>
+struct IsSplit<SplitDescSource<B>> : std::true_type {};
 
 template <class S>
 struct IsRecv : std::false_type {};
@@ -430,8 +425,8 @@ __device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v, 
         if (v != 0) atomicAdd(out + f / src.rpf, v);
         return;
     }
-    if constexpr (IsList<Src>::value)
-        if (fi.aux) return;  // handed over to crc_light_list_kernel, which stores it
+    if constexpr (IsSplit<Src>::value)
+        if (fi.aux) return;  // the other launch's fragment
     out[f] = v;
     if constexpr (IsRecv<Src>::value) src.verdict(f, v, fi);
 }
@@ -1813,63 +1808,6 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
     }
 }
 
-constexpr uint32_t kListMinRows = 8;  // a fragment of at least this many 4 KiB rows is "large"
-constexpr uint32_t kListRows = 16;    // rows per list entry (the light kernel's group of a fragment)
-
-// The piece-stream workgroup's share of a list batch: when at least 7/8 of its bytes lie in large
-// fragments, every large fragment of it gets ceil(R / kListRows) consecutive list entries (appended
-// with one atomic per wave), its group countdown, and is skipped here (len 0, aux 1: emit leaves its
-// out[] word to the list kernel).  A fragment whose entries would pass the list's capacity stays.
-// Called by every thread of the workgroup.
-template <int kWv>
-__device__ __forceinline__ void list_handover(const ListCtl &L, size_t base, uint32_t t, uint32_t nwg, FragInfo &mine) {
-    __shared__ uint64_t red[2 * kWv];
-    const uint32_t lane = t & 63u, wave = t >> 6;
-    const uint64_t len = t < nwg ? mine.len : 0u;
-    const uint32_t R = (uint32_t)((len + kRowBytes - 1) / kRowBytes);
-    const bool big = R >= kListMinRows;
-    uint64_t a = len, b = big ? len : 0u;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        a += __shfl_xor(a, o, 64);
-        b += __shfl_xor(b, o, 64);
-    }
-    if (lane == 0) {
-        red[2 * wave] = a;
-        red[2 * wave + 1] = b;
-    }
-    __syncthreads();
-    uint64_t total = 0, large = 0;
-#pragma unroll
-    for (int w = 0; w < kWv; ++w) {
-        total += red[2 * w];
-        large += red[2 * w + 1];
-    }
-    if (large == 0 || large * 8 < total * 7) return;  // (uniform over the workgroup)
-    const uint32_t ng = big ? (R + kListRows - 1) / kListRows : 0u;
-    uint32_t pre = ng;  // inclusive scan of the wave's entry counts
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
-        if (lane >= (uint32_t)o) pre += y;
-    }
-    const uint32_t wtot = (uint32_t)__shfl((int)pre, 63, 64);
-    uint32_t wbase = 0;
-    if (lane == 0 && wtot) wbase = atomicAdd(L.hdr, wtot);
-    wbase = (uint32_t)__shfl((int)wbase, 0, 64);
-    if (!big) return;
-    const uint64_t e0 = (uint64_t)wbase + pre - ng;
-    const size_t f = base + t;
-    if (e0 + ng > L.cap) {  // no room: the fragment stays here; its entries (inside the cap) are voided
-        for (uint64_t e = e0; e < L.cap && e < e0 + ng; ++e) L.ent[e] = make_uint2(~0u, 0u);
-        return;
-    }
-    if (ng > 1) L.cd[f] = ng;
-    for (uint32_t g = 0; g < ng; ++g) L.ent[e0 + g] = make_uint2((uint32_t)f, (uint32_t)e0);
-    mine.len = 0u;
-    mine.aux = 1u;
-}
-
 // kK: chains per wave, kWv: waves per workgroup (kWv * kK chains); kWaveCap > 0 asks the
 // compiler for that many waves per SIMD.  (Round 1's ablated variants -- loads and task walk
 // only, no piece lookups -- ran as a template switch here until commit d95cfff:
@@ -1906,7 +1844,6 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
 
     FragInfo mine{nullptr, 0u, 0u, nullptr, 0u};
     if (t < nwg) mine = src.get(base + t);
-    if constexpr (IsList<Src>::value) list_handover<kWv>(src.L, base, t, nwg, mine);
     if (t < kChains) {
         chead[t] = 0u;
         sjoin[t] = 0u;  // read after the rows
@@ -2597,84 +2534,6 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
     }
 }
 
-// Two fragments of at most 2 KiB on one wave, one per half-wave (IB's 1,976-byte payloads): lane m of
-// half h holds the 16-byte chunks at 16m + 512q (q = 0..3) of fragment h's 2 KiB half frame (the
-// fragment right-aligned, padding zeros), loaded per lane (each half has its own fragment, so no wave-wide
-// buffer descriptor); the chunk cut by the fragment's start is rebuilt from its first 16 bytes.  Horner
-// over the 512-byte chunk step, the lane tree's first three levels as for a row, then each eight-lane
-// group g of a half shifts by 128 * (3 - g) and two DPP steps XOR a half's four groups into its last lane
-// (31 / 63).  Per fragment: the lookups of a half frame, half the waves, and the workgroup's table
-// staging shared by eight fragments instead of four.  Both fragments must hold 16..2048 bytes.
-template <class Src>
-__device__ __forceinline__ void light_pair_issue(const FragInfo &fi, uint32_t lane, u32x4 (&d)[4], u32x4 &head) {
-    const uint32_t m = lane & 31u, P = 2048u - fi.len;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int32_t x = (int32_t)(16u * m + 512u * q) - (int32_t)P;
-        d[q] = x >= 0 ? ld16u((gu32x4_a1 *)(fi.addr + x)) : u32x4{0u, 0u, 0u, 0u};
-    }
-    head = ld16u((gu32x4_a1 *)fi.addr);
-}
-
-template <class Src>
-__device__ __forceinline__ void light_pair_run(const Src &src, size_t fh, const FragInfo &fi, bool live_h,
-                                               const uint32_t *lds, uint32_t lane, uint32_t *out, u32x4 (&d)[4],
-                                               const u32x4 &head) {
-    const uint32_t m = lane & 31u, P = 2048u - fi.len, kP = P >> 4, sP = P & 15u;
-    const uint32_t cend = fi.copylen + P;
-    {  // the chunk cut by the fragment's start: [zeros | first 16 - sP bytes] (component selects: a
-       // per-lane chunk index would make the compiler index d[] in scratch)
-        const u32x4 v = shl_bytes16(head, sP);
-        const bool mine = sP != 0 && (kP & 31u) == m;
-        const uint32_t qs = kP >> 5;
-        auto put = [&](u32x4 &x, bool c) {
-            x.x = c ? v.x : x.x;
-            x.y = c ? v.y : x.y;
-            x.z = c ? v.z : x.z;
-            x.w = c ? v.w : x.w;
-        };
-        put(d[0], mine && qs == 0u);
-        put(d[1], mine && qs == 1u);
-        put(d[2], mine && qs == 2u);
-        put(d[3], mine && qs == 3u);
-    }
-    if constexpr (Src::kCopy) {
-        if (live_h) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t x = 16u * m + 512u * q;  // frame offset; fragment byte x - P
-                if (x >= P && x + 16u <= cend) {
-                    st16u((gwu32x4_a1 *)(fi.dst + (x - P)), d[q]);
-                } else if (x < cend && x + 16u > P) {  // cut by the copy's start or end: byte stores
-                    for (uint32_t j = 0; j < 16; ++j)
-                        if (x + j >= P && x + j < cend)
-                            ((gbyte_w *)fi.dst)[x + j - P] =
-                                (uint8_t)(pick4(d[q].x, d[q].y, d[q].z, d[q].w, (int)(j >> 2)) >> (8u * (j & 3u)));
-                }
-            }
-        }
-    }
-    inject_register(d, P, fi.partial, [&](int q) { return m + 32u * q; });
-    uint32_t lanec2, sel[4];
-    light_lane_consts(lane, lanec2, sel);
-    const uint32_t c0 = light_chunk(lds, lanec2, sel, d[0]);
-    const uint32_t c1 = light_chunk(lds, lanec2, sel, d[1]);
-    const uint32_t c2 = light_chunk(lds, lanec2, sel, d[2]);
-    const uint32_t c3 = light_chunk(lds, lanec2, sel, d[3]);
-    constexpr uint32_t k512 = kLtNib + kLtTab * 7u;  // the 128 * (7 - g) table of g = 3: 512 bytes
-    uint32_t v = light_shift_at(lds, k512, light_shift_at(lds, k512, light_shift_at(lds, k512, c0) ^ c1) ^ c2) ^ c3;
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<1>(lds, v), 0x111, 0xF, 0xF, false);  // row_shr:1
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<2>(lds, v), 0x112, 0xF, 0xF, false);  // row_shr:2
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<3>(lds, v), 0x114, 0xF, 0xF, false);  // row_shr:4
-    // group g of the half (its last lane 8g + 7) shifts by 128 * (3 - g): table 4 + (7 - (3 - g)) = 8 + g
-    const uint32_t gh = (lane >> 3) & 3u;
-    const uint32_t wv = light_shift_at(lds, kLtNib + kLtTab * (8u + min(gh, 2u)), v);
-    v = gh < 3u ? wv : v;
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 (rows 1, 3)
-    if (m == 31u && live_h) emit(src, out, fh, __builtin_bswap32(v), fi);
-}
-
 // One fragment (or row group) per wave: item = 4 * blockIdx.x + wave, four waves per workgroup.
 template <class Src>
 __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src, size_t n,
@@ -2696,135 +2555,19 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     FragInfo fi{nullptr, 0u, 0u, nullptr, 0u};
     if (f < n) fi = src.get(f);
     LightFrag F;
-    F.init(fi, f < n, W, g);
+    F.init(fi, f < n && !(IsSplit<Src>::value && fi.aux), W, g);
     u32x4 d[4];
     uint32_t o[4];
     F.load_row(lane, F.r0, F.live, d, o, F.half);  // (an empty or dead wave's descriptor reads nothing but zeros)
     const u32x4 head = F.load_head();
+    if constexpr (IsSplit<Src>::value)  // the size split's light launch: most workgroups hold no fragment of its
+        if (!__syncthreads_or(F.live)) return;  // class and leave before staging the tables
     build_slices_light(reinterpret_cast<char *>(lds), bs);
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
     __syncthreads();
     if (!F.live) return;
     light_frag_run(src, f, F, lds, lane, out, [&](uint32_t v) { groups[f * W + g] = v; }, d, o, head);
-}
-
-// Eight waves, eight fragments per workgroup (fragment 8 * blockIdx.x + wave): the workgroup's table staging
-// shared by twice the fragments.  When all eight hold 16..2048 bytes (IB's 1,976-byte payloads) waves 0..3
-// take them in pairs, one per half-wave (light_pair_run), and waves 4..7 only help stage; otherwise every
-// wave runs its own fragment as above.  (The threads of waves 4..7 stage nothing: the builders are
-// written for 256 threads.)
-template <class Src>
-__global__ void __launch_bounds__(512) crc_light_frag8_kernel(const Src src, size_t n, const uint32_t *__restrict__ img,
-                                                             uint32_t *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
-    const uint32_t t = threadIdx.x, lane = t & 63u, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const size_t f = (size_t)blockIdx.x * 8 + wave;
-    constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
-    const uint32_t ts = t & 255u;
-    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[ts];
-    const uint32_t t2 = min(256u + ts, kNibPieces - 1);
-    const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
-    u32x4 bs[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((ts & 7u) >> 1) * 4 + i];
-    FragInfo fi{nullptr, 0u, 0u, nullptr, 0u};
-    if (f < n) fi = src.get(f);
-    const bool small = f >= n || (fi.len >= 16u && fi.len <= 2048u);
-    LightFrag F;
-    F.init(fi, f < n, 1u, 0u);
-    u32x4 d[4];
-    uint32_t o[4];
-    F.load_row(lane, 0u, F.live, d, o, F.half);
-    const u32x4 head = F.load_head();
-    if (t < 256u) {
-        build_slices_light(reinterpret_cast<char *>(lds), bs);
-        reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
-        reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
-    }
-    const bool pairs = __syncthreads_and(small) != 0;
-    if (!pairs) {
-        if (!F.live) return;
-        light_frag_run(src, f, F, lds, lane, out, [](uint32_t) {}, d, o, head);  // (W == 1: whole)
-        return;
-    }
-    if (wave >= 4u) return;
-    const size_t fa = (size_t)blockIdx.x * 8 + 2 * wave, fb = fa + 1;
-    if (fa >= n) return;
-    const bool hb = lane >= 32u, live_h = !hb || fb < n;
-    FragInfo fh = src.get(hb && fb < n ? fb : fa);  // (a dead second half reads fragment a again)
-    u32x4 pd[4], ph;
-    light_pair_issue<Src>(fh, lane, pd, ph);
-    light_pair_run(src, hb ? fb : fa, fh, live_h, lds, lane, out, pd, ph);
-}
-
-// The list of large fragments a batch's piece-stream workgroups handed over (list_handover): a grid of
-// about three workgroups per CU stages the tables once each, and its waves claim list entries one at a
-// time -- entry e = group e - e0 of fragment f, rows [g k, (g + 1) k) of its frame, k = ceil(R / ng) --
-// and run them as crc_light_frag_copy_kernel runs a row group (read-only).  A fragment of one group
-// emits its checksum; the groups of a longer one leave their values in gv and count down cd[f], and the
-// group that finishes last joins them (shifted past the rows after each, XORed) and emits.  The last
-// workgroup to finish resets the list's counters for the next call on the stream.
-__global__ void __launch_bounds__(256) crc_light_list_kernel(const lampi_frag_desc *__restrict__ d, ListCtl L,
-                                                             const uint32_t *__restrict__ img,
-                                                             uint32_t *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
-    __shared__ uint32_t s_count;
-    const uint32_t t = threadIdx.x, lane = t & 63u;
-    constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
-    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
-    const uint32_t t2 = min(256u + t, kNibPieces - 1);
-    const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
-    u32x4 bs[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
-    if (t == 0) s_count = min(__hip_atomic_load(L.hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), L.cap);
-    build_slices_light(reinterpret_cast<char *>(lds), bs);
-    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
-    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
-    __syncthreads();
-    const uint32_t count = s_count;
-    const DescSource src{d};
-    while (count) {
-        uint32_t e = 0;
-        if (lane == 0) e = atomicAdd(L.hdr + 1, 1u);
-        e = __builtin_amdgcn_readfirstlane(e);
-        if (e >= count) break;
-        const uint2 en = L.ent[e];
-        if (en.x == ~0u) continue;  // voided (the list overflowed there)
-        const size_t f = en.x;
-        const FragInfo fi = src.get(f);
-        const uint32_t R = (uint32_t)(((uint64_t)fi.len + kRowBytes - 1) / kRowBytes);
-        const uint32_t ng = (R + kListRows - 1) / kListRows, g = e - en.y;
-        LightFrag F;
-        F.init(fi, true, ng, g);
-        u32x4 dd[4];
-        uint32_t oo[4];
-        F.load_row(lane, F.r0, true, dd, oo, F.half);
-        const u32x4 head = F.load_head();
-        auto sink = [&](uint32_t v) {  // (lane 63 only)
-            L.gv[e] = v;
-            __threadfence();
-            if (atomicSub(L.cd + f, 1u) != 1u) return;
-            __threadfence();  // the last group of the fragment: join every group's value
-            const uint32_t k = (R + ng - 1) / ng;
-            uint32_t acc = 0;
-            for (uint32_t j = 0; j < ng; ++j)
-                acc ^= shift_rows(__hip_atomic_load(L.gv + en.y + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                  R - min((j + 1u) * k, R));
-            out[f] = acc;
-        };
-        light_frag_run(src, f, F, lds, lane, out, sink, dd, oo, head);
-    }
-    __syncthreads();
-    if (t == 0) {
-        __threadfence();
-        if (atomicAdd(L.hdr + 2, 1u) == gridDim.x - 1u) {  // every claim is over: reset for the next call
-            L.hdr[0] = 0u;
-            L.hdr[1] = 0u;
-            L.hdr[2] = 0u;
-        }
-    }
 }
 
 // The fragments of more than one row group: value = XOR over the groups of group g shifted past the rows
@@ -2851,15 +2594,6 @@ __global__ void __launch_bounds__(256) crc_light_group_join_kernel(const Src src
     if (j == 0) emit(src, out, f, acc, fi);
 }
 
-// (A/B knob, LAMPI_LIGHT_PAIRS=1: eight-wave workgroups, IB-sized fragments in pairs)
-static bool light_pairs() {
-    static const bool on = [] {
-        const char *e = std::getenv("LAMPI_LIGHT_PAIRS");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
 // W: row groups per fragment (1: one wave walks all the fragment's rows)
 template <class Src>
 static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
@@ -2867,12 +2601,8 @@ static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uin
     W = min(W, 4096u);  // (the join: at most 64 groups per lane)
     while (W > 1 && (size_t)n * W > ((size_t)1 << 26)) W >>= 1;  // (grid: items * 64 threads < 2^32)
     if (W <= 1) {
-        if (light_pairs())
-            hipLaunchKernelGGL(crc_light_frag8_kernel<Src>, dim3((unsigned)((n + 7) / 8)), dim3(512), 0, s, src, n, img,
-                               out);
-        else
-            hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
-                               img, out, 1u, (uint32_t *)nullptr);
+        hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
+                           img, out, 1u, (uint32_t *)nullptr);
         return hipGetLastError();
     }
     uint32_t *groups = nullptr;
@@ -4270,44 +4000,15 @@ static hipError_t launch_row_segments(const lampi_frag_desc *d, size_t n, uint32
     return hipGetLastError();
 }
 
-// Read-only CRC descriptor batches of at least kListMinBatch fragments and no hint: the piece streams
-// hand their large fragments to crc_light_list_kernel (list_handover), which runs them after them on the
-// same stream.  Scratch: the list header (zeroed here), up to n + 2^20 entries, their values, a countdown
-// per fragment.
-constexpr size_t kListMinBatch = 256;
-static bool light_list() {  // (A/B knob: LAMPI_LIGHT_LIST=0 keeps every fragment on the piece streams)
-    static const bool on = [] {
-        const char *e = std::getenv("LAMPI_LIGHT_LIST");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-static hipError_t launch_listed(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
-                                hipStream_t s) {
-    const size_t cap = n + ((size_t)1 << 20);
-    const size_t o_ent = 256, o_gv = o_ent + cap * sizeof(uint2), o_cd = o_gv + cap * sizeof(uint32_t);
-    uint8_t *scr = nullptr;
-    bool pooled = false;
-    hipError_t e = stream_scratch(s, o_cd + n * sizeof(uint32_t), (void **)&scr, &pooled);
-    if (e != hipSuccess) return e;
-    const ListCtl L{(uint32_t *)scr, (uint2 *)(scr + o_ent), (uint32_t *)(scr + o_gv), (uint32_t *)(scr + o_cd),
-                    (uint32_t)std::min<size_t>(cap, 0xFFFFFFFFull)};
-    e = hipMemsetAsync(L.hdr, 0, 4 * sizeof(uint32_t), s);
-    if (e == hipSuccess) {
-        const uint32_t fpg = frags_per_wg(n);
-        hipLaunchKernelGGL((crc_stream_kernel<ListDescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
-                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, ListDescSource{d, L}, n, fpg, img, out,
-                           nullptr);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) {
-        const unsigned g = (unsigned)std::min<size_t>((size_t)3 * (size_t)std::max(grid, 1), (n + 3) / 4);
-        hipLaunchKernelGGL(crc_light_list_kernel, dim3(g), dim3(256), 0, s, d, L, img, out);
-        e = hipGetLastError();
-    }
-    return scratch_done(s, scr, pooled, e);
-}
+// The two-launch size split for read-only CRC descriptor batches without a hint (SplitDescSource), for
+// batches of kSplitMin..kSplitMax fragments.  Same box (profiles/r04/split_ab.txt): 16,404 x 65,456 B
+// 55.6 -> 75.7-76.5%, 16,404 x 40,000 B 54 -> 72-75%, config C and 1 MiB fragments unchanged (outside /
+// not of the light class).  The light launch costs a dead workgroup per four fragments of the other class
+// (a vote before the table staging): 4,096 x 4 KiB 10.2 -> 12.8 us per call, 65,536 x 4 KiB 52.6 -> 71 us;
+// so smaller batches (latency) and larger ones (config C's 659,114 fragments: 74.6 -> 40.9%, its 8-16-row
+// fragments run on the light kernel only after the piece streams) keep one launch.  Running the two
+// launches concurrently on a forked stream measured worse (GM 67-68%).
+constexpr size_t kSplitMin = 1024, kSplitMax = 65536;
 
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
                            hipStream_t s, bool plan, uint32_t rows_hint) {  // (defaults: frag_csum_kernels.h)
@@ -4319,7 +4020,15 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
                                           rows_hint <= kSegRows ? 1u : (rows_hint + kLightRoRows - 1) / kLightRoRows);
     if (rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<false, kStreamWv, kStreamCap>(d, n, out, img, s, rows_hint);
-    if (n >= kListMinBatch && n <= 0xFFFFFFFFull && light_list()) return launch_listed(d, n, out, img, grid, s);
+    if (n >= kSplitMin && n <= kSplitMax) {  // both size classes, one launch each (SplitDescSource)
+        const uint32_t fpg = frags_per_wg(n);
+        hipLaunchKernelGGL((crc_stream_kernel<SplitDescSource<false>, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
+                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, SplitDescSource<false>{d}, n, fpg, img, out,
+                           nullptr);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        return launch_crc_light_frag_copy(SplitDescSource<true>{d}, n, img, out, s, 1u);
+    }
     const uint32_t fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
                        frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);

@@ -201,6 +201,30 @@ def test_descriptor_batch_random(cuda, oracle):
             assert np.array_equal(got, want), by_bytes
 
 
+@pytest.mark.parametrize("n", [1023, 1024, 5000, 65536, 65537])
+def test_descriptor_batch_size_split(cuda, oracle, n):
+    """Read-only CRC batches of 1,024..65,536 descriptors run in two launches by size class (DESIGN.md 4.2:
+    8-16-row fragments on the table-light kernel, the rest on the piece streams, each skipping the other's):
+    the class boundaries 28,672 / 28,673 and 65,536 / 65,537 bytes, empty and tiny fragments, any alignment,
+    random registers -- and the batch sizes on either side of the split's range -- against the oracle."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(n)
+    base = torch.empty(96 << 20, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=34)
+    host = base.cpu().numpy()
+    edge = np.array([0, 1, 15, 16, 4095, 28671, 28672, 28673, 40000, 65455, 65456, 65535, 65536, 65537, 70000],
+                    np.uint64)
+    lens = np.where(rng.random(n) < 0.5, rng.choice(edge, size=n), rng.integers(0, 70000, size=n)).astype(np.uint64)
+    offs = rng.integers(0, (96 << 20) - 70001, size=n).astype(np.uint64)
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    descs = dv.make_descs(base, offs, lens, parts)
+    want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32), 0)
+    got = dv.as_u32(dv.frag_csum_batch(descs, mode=0))
+    assert np.array_equal(got, want)
+
+
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 @pytest.mark.parametrize("case", ["three", "aligned40", "mixed600", "huge_first"])
 def test_descriptor_batch_fragments_across_chains(cuda, oracle, case, mode):
