@@ -37,6 +37,10 @@ CASES = [
     (2, 16404, 65456, 1, (1,)),
     (2, 1024, 1048576, 0, (1,)),           # --desc --rows-hint 256 / 1024: 1 MiB and 4 MiB fragments
     (2, 256, 4194304, 0, (1,)),
+    (2, 16384, 65456, 0, (1,)),            # --recv --frags 16384 --frag-bytes 65456: the GM receive lines
+    (2, 16384, 65456, 1, (1,)),
+    (2, 1024, 1048576, 1, (1,)),           # --desc --mode sum, 1 MiB / 4 MiB
+    (2, 256, 4194304, 1, (1,)),
 ]
 # config D per-GPU shards: (seed, n_total, L, mode, nshard)
 SHARD_CASES = [(3, 33554432, 16384, 0, 8), (3, 33554432, 16384, 1, 8)]
