@@ -441,7 +441,7 @@ def test_descriptor_batch_row_segments_large(cuda, oracle):
 def test_descriptor_batch_two_buffers(cuda, oracle):
     """Fragments from two buffers more than 2 GiB apart, interleaved in runs so workgroups hold both,
     with lengths at the 64-byte-piece edges that round 3's packed-row experiment (crc_list_kernel,
-    profiles/r03/list_kernel_ab.txt) keyed on (64, 1024, 1088, 2048, 2112 bytes), odd lengths beside them,
+    DESIGN.md §11) keyed on (64, 1024, 1088, 2048, 2112 bytes), odd lengths beside them,
     empty fragments and random registers.  Every fragment against the oracle."""
     import torch
 

@@ -2,7 +2,7 @@
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
 #   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchCsum | benchD | bcopy |
-#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | e2e | recv | gm | bigdesc | microbench
+#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | pmcdesc | e2e | recv | gm | bigdesc
 # Any failure (a test failure, fault, abort, segfault, timeout or kill) ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -57,6 +57,12 @@ for step in "$@"; do
                  SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv \
                  -d gpurun_out/pmc_sq$cfg -o run -- python3 bench.py --steps 3 --warmup 1 $extra
            done ;;
+    pmcdesc) for spec in crc:1024:1048576:256 crc:256:4194304:1024 sum:4194304:4096:0 sum:16404:65456:0; do  # FETCH_SIZE per line
+               IFS=: read -r m nf fb h <<< "$spec"
+               run pmcdesc_${m}_${fb}_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+                 -d gpurun_out/pmcdesc_${m}_${fb}_fetch -o run -- python3 bench.py --desc --mode $m --frags $nf \
+                 --frag-bytes $fb --rows-hint $h --steps 5 --warmup 1 --no-cpu-baseline || exit 1
+             done ;;
     e2e) run e2e 600 python bench.py --e2e ;;
     recv) run recv 600 python bench.py --recv --steps 10 &&
           run recvsum 600 python bench.py --recv --mode sum --steps 10 ;;
@@ -82,7 +88,6 @@ for step in "$@"; do
     tests_verify) run pytest_verify 600 python -m pytest tests/test_gpu_verify.py -m gpu -x -q ;;
     tests_native) run pytest_native 600 python -u -m pytest tests/test_gpu_native.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     sweep) run sweep 500 tools/microbench/frags_sweep ;;
-    microbench) run microbench 300 tools/microbench/readbw ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
