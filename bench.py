@@ -561,6 +561,7 @@ def run_device(args):
                 "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2], max(kern_ms))],
                 "algorithmic_bytes_per_launch": n * L,
                 "traffic_source": None if traffic is None else traffic.get("source"),
+                "sq_per_4KiB_row": None if traffic is None else traffic.get("sq_per_4KiB_row"),
                 "note": "rank 0's kernel; every rank's in per_gpu",
             },
             "per_gpu": per_gpu,
@@ -659,6 +660,7 @@ def run_mixed(args):
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None if traffic is None else traffic["hbm_bytes_per_launch"],
                      "traffic_source": None if traffic is None else traffic.get("source"),
+                     "sq_per_4KiB_row": None if traffic is None else traffic.get("sq_per_4KiB_row"),
                      "kernel": "crc_stream_kernel" if mode == dv.CRC32 else "crc_stream_kernel<kSum>",
                      "incl_metadata": {"bytes": meta, "achieved": round(meta / kern_avg_s / 1e9, 1),
                                        "frac": round(meta / kern_avg_s / 1e9 / HBM_PEAK_GBS, 4)},
