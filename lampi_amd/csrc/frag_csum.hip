@@ -2166,11 +2166,19 @@ __device__ __forceinline__ void build_slices_light(char *b, const u32x4 bs[4]) {
 }
 
 // register after the shift of nibble table `base` (a byte address in LDS; swapped domain)
+// (the byte offsets of all eight lookups from two masks: a holds 4 * nibbles 0, 2, 4, 6 in its bytes, b
+// 4 * nibbles 1, 3, 5, 7 -- one bit-field extract per lookup instead of a shift and a mask -- and the
+// eight entries XORed as a three-input tree)
 __device__ __forceinline__ uint32_t light_shift_at(const uint32_t *lds, uint32_t base, uint32_t C) {
-    uint32_t r = lds_u32(lds, base + ((C << 2) & 0x3Cu));
+    uint32_t a = (C << 2) & 0x3C3C3C3Cu, b = (C >> 2) & 0x3C3C3C3Cu;
+    asm("" : "+v"(a), "+v"(b));  // (opaque: otherwise folded back into a shift and a mask per lookup)
+    uint32_t e[8];
 #pragma unroll
-    for (int p = 1; p < 8; ++p) r ^= lds_u32(lds, base + 64u * p + ((C >> (4 * p - 2)) & 0x3Cu));
-    return r;
+    for (int k = 0; k < 4; ++k) {
+        e[2 * k] = lds_u32(lds, base + 128u * k + ((a >> (8 * k)) & 0xFFu));
+        e[2 * k + 1] = lds_u32(lds, base + 128u * k + 64u + ((b >> (8 * k)) & 0xFFu));
+    }
+    return xor3(xor3(e[0], e[1], e[2]), xor3(e[3], e[4], e[5]), e[6]) ^ e[7];
 }
 template <int kTab>
 __device__ __forceinline__ uint32_t light_shift(const uint32_t *lds, uint32_t C) {
@@ -2458,7 +2466,7 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
     // (hf: BoolC<true> for a half frame -- its own copy of the body, kept out of the row loop)
     auto step = [&](auto hf, uint32_t r, u32x4 (&dc)[4], const uint32_t (&oc)[4], u32x4 (&dn)[4],
                     uint32_t (&on)[4]) {
-        F.load_row(lane, r + 1, r + 1 < r1, dn, on);
+        if constexpr (!decltype(hf)::value) F.load_row(lane, r + 1, r + 1 < r1, dn, on);  // (a half frame: one row)
         if (r == 0 && sP != 0) {  // the chunk cut by the fragment's start: [zeros | first 16 - sP bytes]
             const u32x4 v = shl_bytes16(head, sP);
             const bool mine = lane == (kP & 63u);
@@ -2475,20 +2483,27 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
             if constexpr (Src::kCopy)
                 __builtin_amdgcn_raw_buffer_store_b128(dc[q], F.drs, full ? oc[q] : 0xFFFFFFF0u, 0, kBufNt);
         }
-        // chunks cut by the copy's start or end (at most two per fragment): byte stores
-        const uint64_t row0 = (uint64_t)r * kRowBytes;
-        if (Src::kCopy &&
-            ((r == 0 && sP != 0) || (cend > row0 && cend < row0 + kRowBytes && (cend & 15u) != 0))) {
+        // chunks cut by the copy's start or end (at most two per fragment, wave-uniform frame chunks kP and
+        // kE): sixteen byte stores from the one lane holding each, through the destination's buffer
+        // descriptor -- its range check drops the bytes outside [0, copylen) (those before the fragment
+        // have wrapped offsets), so no byte needs a test of its own
+        if constexpr (Src::kCopy) {
+            auto store_cut = [&](uint32_t k) {  // k: the cut chunk's index in the frame, in row r
+                if (lane == (k & 63u)) {
+                    const uint32_t qk = (k >> 6) & 3u;
+                    const u32x4 v = qk == 0 ? dc[0] : qk == 1 ? dc[1] : qk == 2 ? dc[2] : dc[3];
+                    const uint32_t ob = 16u * k - P;
+                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint64_t x = rbase + 1024u * q;
-                if (!(x >= P && x + 16u <= cend) && x < cend && x + 16u > P) {
-                    for (uint32_t j = 0; j < 16; ++j)
-                        if (x + j >= P && x + j < cend)
-                            ((gbyte_w *)fi.dst)[x + j - P] =
-                                (uint8_t)(pick4(dc[q].x, dc[q].y, dc[q].z, dc[q].w, (int)(j >> 2)) >> (8u * (j & 3u)));
+                    for (int j = 0; j < 16; ++j)
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j >> 2] >> (8 * (j & 3))), F.drs, ob + j, 0,
+                                                             kBufNt);
                 }
-            }
+            };
+            const bool any = fi.copylen != 0;
+            if (any && sP != 0 && (kP >> 8) == r) store_cut(kP);
+            const uint64_t kE = (cend - 1) >> 4;  // the chunk holding the copy's last byte
+            if (any && (cend & 15u) != 0 && (kE >> 8) == r && !(sP != 0 && kE == kP)) store_cut((uint32_t)kE);
         }
         // the register: in row 0, or row 1 when kP is row 0's last chunk
         if (r == 0 || (r == 1 && kP == 255u))
