@@ -45,6 +45,7 @@
 #include <utility>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 
 #include "crc_const.h"
 #include "crc_tables.h"
@@ -2550,7 +2551,7 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
 }
 
 // One fragment (or row group) per wave: item = 4 * blockIdx.x + wave, four waves per workgroup.
-template <class Src>
+template <class Src, bool kLate = false>
 __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src, size_t n,
                                                                   const uint32_t *__restrict__ img,
                                                                   uint32_t *__restrict__ out, uint32_t W,
@@ -2573,8 +2574,11 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     F.init(fi, f < n && !(IsSplit<Src>::value && fi.aux), W, g);
     u32x4 d[4];
     uint32_t o[4];
-    F.load_row(lane, F.r0, F.live, d, o, F.half);  // (an empty or dead wave's descriptor reads nothing but zeros)
-    const u32x4 head = F.load_head();
+    u32x4 head;
+    if constexpr (!kLate) {
+        F.load_row(lane, F.r0, F.live, d, o, F.half);  // (an empty or dead wave's descriptor reads nothing but zeros)
+        head = F.load_head();
+    }
     if constexpr (IsSplit<Src>::value)  // the size split's light launch: most workgroups hold no fragment of its
         if (!__syncthreads_or(F.live)) return;  // class and leave before staging the tables
     build_slices_light(reinterpret_cast<char *>(lds), bs);
@@ -2582,7 +2586,140 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
     __syncthreads();
     if (!F.live) return;
+    if constexpr (kLate) {
+        F.load_row(lane, F.r0, F.live, d, o, F.half);
+        head = F.load_head();
+    }
     light_frag_run(src, f, F, lds, lane, out, [&](uint32_t v) { groups[f * W + g] = v; }, d, o, head);
+}
+
+// IB-sized fragments two to a wave (crc_light_pair_copy_kernel; the launcher picks it when the stream's
+// learned batch shape says every sampled fragment was at most 2 KiB): a 4-wave workgroup takes eight
+// fragments, wave w fragments 2w and 2w + 1, half-wave h (lanes 32h .. 32h + 31) one of them in a 2 KiB
+// half frame (front padding P = 2048 - L).  Lane l' = l & 31 holds the frame's chunks k = 32q + l' (frame
+// bytes 512q + 16l', q = 0..3): four chunks, as a lane of a 4 KiB row has, so a wave does one row's
+// lookups for two fragments and the workgroup's table staging serves eight (one wave per 1,976-byte IB
+// payload spent a whole wave's prologue and tree on 4 KB of traffic).  Loads and stores are global with
+// per-lane addresses (two fragments per wave: no single buffer descriptor): chunks wholly in the padding
+// read the table image's zero chunk and store nothing, the chunk cut by the fragment's start is rebuilt
+// from its first 16 bytes, the chunks cut by the copy's ends go out byte by byte.  Horner over the 512-byte
+// step (group table 3 of the light set), a lane tree of three levels within 16-lane rows, the 8-lane
+// groups shifted by 128 (3 - g') through the light group tables, and row_shr:8 + row_bcast:15 leave the
+// fragments' values in lanes 31 and 63.  A workgroup holding a pair that is not two fragments of 16..2048
+// bytes (or a lone last fragment that is not) runs its fragments one after the other through
+// light_frag_run, each on a whole wave.
+// A pair crc_light_pair_copy_kernel cannot take in half frames: fragments f0 and f0 + 1 (if < n), each
+// on the whole wave through light_frag_run.
+template <class Src>
+__device__ __forceinline__ void light_pair_fallback(const Src src, size_t f0, size_t n, const uint32_t *lds,
+                                                             uint32_t lane, uint32_t *out) {
+#pragma nounroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        const size_t f = f0 + k;
+        if (f >= n) break;
+        LightFrag F;
+        F.init(src.get(f), true, 1u, 0u);
+        u32x4 dd[4];
+        uint32_t oo[4];
+        F.load_row(lane, F.r0, F.live, dd, oo, F.half);
+        const u32x4 hh = F.load_head();
+        light_frag_run(src, f, F, lds, lane, out, [](uint32_t) {}, dd, oo, hh);
+    }
+}
+
+template <class Src>
+__global__ void __launch_bounds__(256) crc_light_pair_copy_kernel(const Src src, size_t n,
+                                                                  const uint32_t *__restrict__ img,
+                                                                  uint32_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const size_t f0 = ((size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6)) * 2;
+    constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
+    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+    const uint32_t t2 = min(256u + t, kNibPieces - 1);
+    const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
+    u32x4 bs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
+    FragInfo fa{nullptr, 0u, 0u, nullptr, 0u}, fb{nullptr, 0u, 0u, nullptr, 0u};
+    const bool la = f0 < n, lb = f0 + 1 < n;
+    if (la) fa = src.get(f0);
+    if (lb) fb = src.get(f0 + 1);
+    auto pairable = [](const FragInfo &x) { return x.len >= 16u && x.len <= (uint32_t)kRowBytes / 2u; };
+    const bool pair = la && pairable(fa) && (!lb || pairable(fb));
+    // this lane's fragment (half-wave h) and its chunk loads, issued before the table staging
+    const uint32_t h = lane >> 5, lp = lane & 31u;
+    const bool live = h ? lb : la;
+    const FragInfo fi = h ? fb : fa;
+    const uint32_t L = fi.len, P = (uint32_t)kRowBytes / 2u - L;  // (pair only: 16 <= L <= 2048)
+    u32x4 d[4];
+    u32x4 head = u32x4{0u, 0u, 0u, 0u};
+    if (pair) {
+        gbyte *zero = (gbyte *)(img + kImgZero);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t x = 512u * q + 16u * lp;  // frame offset of the chunk
+            const bool in = live && x >= P;          // wholly inside the fragment (the frame ends with it)
+            d[q] = ld16c((gu32x4_a1 *)(in ? fi.addr + (x - P) : zero));
+        }
+        head = ld16c((gu32x4_a1 *)(live ? fi.addr : zero));
+    }
+    // a workgroup with a pair it cannot take runs all its fragments one after the other, each on a whole
+    // wave (rare; a per-workgroup choice keeps the two paths' registers apart)
+    const bool wg_pair = __syncthreads_and(pair || !la) != 0;
+    build_slices_light(reinterpret_cast<char *>(lds), bs);
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
+    __syncthreads();
+    if (!la) return;
+    if (!wg_pair) {
+        light_pair_fallback(src, f0, n, lds, lane, out);
+        return;
+    }
+    const uint32_t kP = P >> 4, sP = P & 15u;
+    if (live && sP != 0 && (kP & 31u) == lp) {  // the chunk cut by the fragment's start
+        const u32x4 v = shl_bytes16(head, sP);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if ((uint32_t)q == (kP >> 5)) d[q] = v;
+    }
+    if constexpr (Src::kCopy) {
+        const uint32_t cend = P + fi.copylen;  // the copy's end in the frame (<= 2048)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t x = 512u * q + 16u * lp;
+            if (live && x >= P && x + 16u <= cend) st16u((gwu32x4_a1 *)(fi.dst + (x - P)), d[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // chunks cut by the copy's start or end: byte by byte
+            const uint32_t x = 512u * q + 16u * lp;
+            if (live && !(x >= P && x + 16u <= cend) && x < cend && x + 16u > P) {
+                for (uint32_t j = 0; j < 16; ++j)
+                    if (x + j >= P && x + j < cend)
+                        ((gbyte_w *)fi.dst)[x + j - P] =
+                            (uint8_t)(pick4(d[q].x, d[q].y, d[q].z, d[q].w, (int)(j >> 2)) >> (8u * (j & 3u)));
+            }
+        }
+    }
+    if (live) inject_register(d, P, fi.partial, [&](int q) { return 32u * q + lp; });
+    uint32_t lanec2, sel[4];
+    light_lane_consts(lane, lanec2, sel);
+    constexpr uint32_t kShift512 = kLtNib + kLtTab * (4u + 3u);  // group table 3: 128 * (7 - 3) bytes
+    const uint32_t c0 = light_chunk(lds, lanec2, sel, d[0]);
+    const uint32_t c1 = light_chunk(lds, lanec2, sel, d[1]);
+    const uint32_t c2 = light_chunk(lds, lanec2, sel, d[2]);
+    const uint32_t c3 = light_chunk(lds, lanec2, sel, d[3]);
+    uint32_t v = light_shift_at(lds, kShift512, light_shift_at(lds, kShift512, light_shift_at(lds, kShift512, c0) ^ c1) ^ c2) ^ c3;
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<1>(lds, v), 0x111, 0xF, 0xF, false);  // row_shr:1
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<2>(lds, v), 0x112, 0xF, 0xF, false);  // row_shr:2
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<3>(lds, v), 0x114, 0xF, 0xF, false);  // row_shr:4
+    // group g' = (lane >> 3) & 3 of the half: shift by 128 (3 - g') through light group table 4 + (g' + 4)
+    const uint32_t gq = (lane >> 3) & 3u;
+    const uint32_t wv = light_shift_at(lds, kLtNib + kLtTab * (8u + min(gq, 2u)), v);
+    v = gq < 3u ? wv : v;
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 (rows 1, 3)
+    if (live && lp == 31u) emit(src, out, f0 + h, __builtin_bswap32(v), fi);
 }
 
 // The fragments of more than one row group: value = XOR over the groups of group g shifted past the rows
@@ -2609,23 +2746,43 @@ __global__ void __launch_bounds__(256) crc_light_group_join_kernel(const Src src
     if (j == 0) emit(src, out, f, acc, fi);
 }
 
+template <class Src>
+static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
+                                             hipStream_t s) {
+    hipLaunchKernelGGL(crc_light_pair_copy_kernel<Src>, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, src, n, img,
+                       out);
+    return hipGetLastError();
+}
+
 // W: row groups per fragment (1: one wave walks all the fragment's rows)
 template <class Src>
 static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
                                              hipStream_t s, uint32_t W = 1) {
     W = min(W, 4096u);  // (the join: at most 64 groups per lane)
     while (W > 1 && (size_t)n * W > ((size_t)1 << 26)) W >>= 1;  // (grid: items * 64 threads < 2^32)
+    static const bool late = [] {
+        const char *e = std::getenv("LAMPI_LIGHT_LATE");
+        return e && e[0] == '1';
+    }();
     if (W <= 1) {
-        hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
-                           img, out, 1u, (uint32_t *)nullptr);
+        if (late)
+            hipLaunchKernelGGL((crc_light_frag_copy_kernel<Src, true>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s,
+                               src, n, img, out, 1u, (uint32_t *)nullptr);
+        else
+            hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
+                               img, out, 1u, (uint32_t *)nullptr);
         return hipGetLastError();
     }
     uint32_t *groups = nullptr;
     bool pooled = false;
     hipError_t e = stream_scratch(s, n * W * sizeof(uint32_t), (void **)&groups, &pooled);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n * W + 3) / 4)), dim3(256), 0, s, src, n, img,
-                       out, W, groups);
+    if (late)
+        hipLaunchKernelGGL((crc_light_frag_copy_kernel<Src, true>), dim3((unsigned)((n * W + 3) / 4)), dim3(256), 0, s,
+                           src, n, img, out, W, groups);
+    else
+        hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n * W + 3) / 4)), dim3(256), 0, s, src, n,
+                           img, out, W, groups);
     e = hipGetLastError();
     if (e == hipSuccess) {
         uint32_t G = 1;
@@ -3873,10 +4030,22 @@ static dim3 grid_for(size_t n, uint32_t fpw) { return dim3((unsigned)((n + (size
 namespace {
 std::atomic<int64_t> g_scratch_bytes{0};
 
+// What the census kernel records about a batch (BatchShape, below): host-mapped, one per entry-point kind.
+struct BatchShape {
+    uint32_t seq;      // written last; 0: nothing recorded yet
+    uint32_t sampled;  // descriptors sampled (up to 64, spread over the batch)
+    uint32_t rmin, rmax;  // fewest / most rows (4 KiB) among them
+    uint32_t nhalf;    // how many were at most 2 KiB
+    uint32_t pad[3];
+};
+constexpr int kShapeKinds = 3;  // read-only descriptors, copy descriptors, receive descriptors
+
 struct ScratchTable {
     struct Slot {
         void *p = nullptr;
         size_t cap = 0;
+        BatchShape *shape[kShapeKinds] = {};  // host-mapped (coherent), lazily allocated
+        uint32_t calls[kShapeKinds] = {};
     };
     std::map<std::pair<int, hipStream_t>, Slot> slots;
     ScratchTable() = default;
@@ -3900,6 +4069,12 @@ struct ScratchTable {
             (void)hipStreamSynchronize(it->first.second);
             (void)hipFree(it->second.p);
             g_scratch_bytes.fetch_sub((int64_t)it->second.cap, std::memory_order_relaxed);
+            for (BatchShape *&b : it->second.shape)
+                if (b) {
+                    (void)hipHostFree(b);
+                    g_scratch_bytes.fetch_sub((int64_t)sizeof(BatchShape), std::memory_order_relaxed);
+                    b = nullptr;
+                }
             it = slots.erase(it);
         }
         if (have_cur && set != cur) (void)hipSetDevice(cur);
@@ -3952,6 +4127,106 @@ int64_t device_scratch_bytes() { return g_scratch_bytes.load(std::memory_order_r
 static hipError_t scratch_done(hipStream_t s, void *p, bool pooled, hipError_t e) {
     const hipError_t f = pooled ? hipFreeAsync(p, s) : hipSuccess;
     return e != hipSuccess ? e : f;
+}
+
+// ---- Batch shapes learned on the device ----------------------------------------------------------
+// A descriptor batch's lengths live on the device, so the host cannot size a one-row-per-wave grid for
+// it (LAMPI_CSUM_ROWS_HINT is the caller's way to say it).  Without a hint the library learns the shape
+// from the stream's earlier batches: every kShapeEvery-th call of an entry point on a stream (and its
+// first) launches census_kernel ahead of the batch's kernels -- one wave reading up to 64 descriptors
+// spread over the batch, recording the fewest / most rows among them into a host-mapped BatchShape --
+// and a later call on that stream reads the record (no synchronization: whatever has landed) and, when
+// the sampled fragments were all of 8 or more rows within a factor of two of each other, runs as if
+// the caller had passed LAMPI_CSUM_ROWS_HINT(most rows); CRC copies and receives whose sampled
+// fragments were all at most 2 KiB (IB's payloads) run two fragments to a wave
+// (crc_light_pair_copy_kernel).  The results never depend on it (every
+// schedule is exact for any lengths); the first batches of a stream, mixed batches (config C), batches
+// under kShapeMin fragments and graph captures keep the given schedule.  LAMPI_CSUM_NO_SHAPES=1
+// turns it off.
+constexpr size_t kShapeMin = 256;
+constexpr uint32_t kShapeEvery = 16;
+constexpr uint32_t kShapeRows = 8;  // fewest rows of a learned hint (16 KiB copies: hint 4 no better, receive worse)
+
+template <class Src>
+__global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, BatchShape *rec, uint32_t seq) {
+    const uint32_t l = threadIdx.x;
+    const uint32_t m = (uint32_t)min<size_t>(n, 64);
+    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u;
+    if (l < m) {
+        const FragInfo fi = src.get((size_t)l * n / m);
+        const uint32_t R = (uint32_t)(((uint64_t)fi.len + kRowBytes - 1) / kRowBytes);
+        rmin = R;
+        rmax = R;
+        half = fi.len <= (uint32_t)kRowBytes / 2u ? 1u : 0u;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        rmin = min(rmin, (uint32_t)__shfl_xor((int)rmin, o));
+        rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o));
+        half += (uint32_t)__shfl_xor((int)half, o);
+    }
+    if (l == 0) {
+        volatile BatchShape *r = rec;
+        r->sampled = m;
+        r->rmin = rmin;
+        r->rmax = rmax;
+        r->nhalf = half;
+        __threadfence_system();
+        r->seq = seq;
+    }
+}
+
+static bool shapes_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("LAMPI_CSUM_NO_SHAPES");
+        return !(e && e[0] == '1');
+    }();
+    return on;
+}
+
+// The rows hint to run this batch with: the caller's, or the one learned from the stream's earlier
+// batches of this kind (launching the census for later ones when due).
+template <class Src>
+static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int kind, uint32_t rows_hint,
+                                  bool *pairs = nullptr) {
+    if (pairs) *pairs = false;
+    if (rows_hint > 1 || n < kShapeMin || !shapes_enabled()) return rows_hint;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return rows_hint;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return rows_hint;
+    ScratchTable::Slot &slot = t_scratch.slots[{dev, s}];
+    BatchShape *&rec = slot.shape[kind];
+    if (!rec) {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, sizeof(BatchShape), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            return rows_hint;
+        }
+        std::memset(p, 0, sizeof(BatchShape));
+        rec = (BatchShape *)p;
+        g_scratch_bytes.fetch_add((int64_t)sizeof(BatchShape), std::memory_order_relaxed);
+    }
+    // the last record that landed (seq read before and after the fields: a record being written is skipped)
+    const volatile BatchShape *v = rec;
+    uint32_t W = rows_hint;
+    const uint32_t q0 = v->seq;
+    const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (q0 != 0 && v->seq == q0 && sampled > 0) {
+        if (rmin >= kShapeRows && rmax <= 2 * rmin) W = rmax;
+        if (pairs && nhalf == sampled) *pairs = true;  // every sampled fragment at most 2 KiB: two per wave
+    }
+    const uint32_t c = slot.calls[kind]++;
+    if (c % kShapeEvery == 0) {
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, rec, 0) == hipSuccess) {
+            hipLaunchKernelGGL(census_kernel<Src>, dim3(1), dim3(64), 0, s, src, n, (BatchShape *)dp, c + 1);
+            (void)hipGetLastError();
+        } else {
+            (void)hipGetLastError();
+        }
+    }
+    return W;
 }
 
 template <bool kSum, int kWv, int kCap>
@@ -4030,6 +4305,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
+    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint);
     if (rows_hint >= kLightDescRows)  // one wave per kSegRows rows of a fragment, read-only
         return launch_crc_light_frag_copy(DescSource{d}, n, img, out, s,
                                           rows_hint <= kSegRows ? 1u : (rows_hint + kLightRoRows - 1) / kLightRoRows);
@@ -4203,6 +4479,9 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
                              hipStream_t s, uint32_t rows_hint) {
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC)
+    bool pairs = false;
+    rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, mode == LAMPI_CSUM_CRC32 ? &pairs : nullptr);
+    if (pairs) return launch_crc_light_pair_copy(CopySource{d}, n, img, out, s);
     if (mode == LAMPI_CSUM_CRC32)
         return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
     return launch_sum_copy_groups(CopySource{d}, n, out, s, rows_hint);
@@ -4217,6 +4496,9 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
     if (!img) return hipErrorInvalidValue;
     const bool crc = mode == LAMPI_CSUM_CRC32;
     const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
+    bool pairs = false;
+    rows_hint = learned_rows_hint(src, n, s, 2, rows_hint, crc ? &pairs : nullptr);
+    if (pairs) return launch_crc_light_pair_copy(src, n, img, csum, s);
     if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s, rows_hint);
     return launch_sum_copy_groups(src, n, csum, s, rows_hint);
 }
@@ -4244,6 +4526,7 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
+    if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint);
     if (img && rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<true, kSumWv, kSumCap>(d, n, out, img, s, rows_hint);
     if (img) {  // piece streams (img: the zero chunk)

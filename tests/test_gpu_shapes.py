@@ -1,0 +1,236 @@
+"""Batch shapes learned on the device ("Batch shapes learned on the device").
+
+Without LAMPI_CSUM_ROWS_HINT the library samples a stream's descriptor batches on the device
+(census_kernel, every 16th call) and runs later batches of 8-16-row fragments with the row-group
+schedule the hint would select.  The schedule may change between two calls with the same inputs, so
+every call is checked: read-only CRC and SUM batches, fused copies (checksums and every destination
+byte) and the receive step, over GM-shaped batches, a mixed batch in between (the shape changes under
+the learned hint) and GM-shaped batches again -- all against the oracle on a stream of their own.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = 300  # >= the census's 256-descriptor minimum
+
+
+def _dv():
+    from lampi_amd import device as dv
+
+    return dv
+
+
+def _batches(rng, size):
+    """Two shapes over one source buffer: GM-like (28,673..65,536 bytes: 8-16 rows, mostly 65,456) and
+    mixed (0..70,000 bytes)."""
+    gm = np.where(rng.random(N) < 0.7, 65456, rng.integers(28673, 65537, size=N)).astype(np.uint64)
+    mixed = rng.integers(0, 70001, size=N).astype(np.uint64)
+    offs = rng.integers(0, size - 70001, size=N).astype(np.uint64)
+    parts = rng.integers(0, 2**32, size=N, dtype=np.uint64)
+    return {"gm": gm, "mixed": mixed}, offs, parts
+
+
+SEQUENCE = ["gm"] * 20 + ["mixed"] * 3 + ["gm"] * 18
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_learned_shape_read_only(cuda, oracle, mode):
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(71 + mode)
+    size = 48 << 20
+    base = torch.empty(size, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=72)
+    host = base.cpu().numpy()
+    lens, offs, parts = _batches(rng, size)
+    prepared = {}
+    for k, ln in lens.items():
+        descs = dv.make_descs(base, offs, ln, parts if mode == 0 else None)
+        want = oracle.desc_batch(host, offs, ln, parts.astype(np.uint32) if mode == 0 else None, mode)
+        prepared[k] = (descs, want)
+    stream = torch.cuda.Stream(device=cuda)
+    with torch.cuda.stream(stream):
+        for i, k in enumerate(SEQUENCE):
+            descs, want = prepared[k]
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, stream=stream))
+            assert np.array_equal(got, want), (i, k, int(np.count_nonzero(got != want)))
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_learned_shape_copies(cuda, oracle, mode):
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(81 + mode)
+    size = 48 << 20
+    src = torch.empty(size, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(src, seed=82)
+    host = src.cpu().numpy()
+    lens, offs, parts = _batches(rng, size)
+    dst = torch.empty(N * 70016, dtype=torch.uint8, device=cuda)
+    doffs = (np.arange(N, dtype=np.uint64) * 70016 + rng.integers(0, 16, size=N).astype(np.uint64))
+    prepared = {}
+    for k, ln in lens.items():
+        # copy all but a ragged tail of some fragments (the residue is checksummed, not copied)
+        cl = np.where(rng.random(N) < 0.2, ln - np.minimum(ln, rng.integers(0, 40, size=N).astype(np.uint64)), ln)
+        descs = dv.make_copy_descs(src, offs, dst, doffs, cl, ln, parts if mode == 0 else None)
+        want = oracle.desc_batch(host, offs, ln.astype(np.uint32), parts.astype(np.uint32) if mode == 0 else None,
+                                 mode)
+        want_dst = np.zeros(dst.numel(), np.uint8)
+        for i in range(N):
+            a, b, c = int(offs[i]), int(doffs[i]), int(cl[i])
+            want_dst[b:b + c] = host[a:a + c]
+        prepared[k] = (descs, want, torch.from_numpy(want_dst).to(cuda))
+    stream = torch.cuda.Stream(device=cuda)
+    with torch.cuda.stream(stream):
+        for i, k in enumerate(SEQUENCE):
+            descs, want, want_dst = prepared[k]
+            dst.zero_()
+            got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=mode, stream=stream))
+            assert np.array_equal(got, want), (i, k, int(np.count_nonzero(got != want)))
+            assert torch.equal(dst, want_dst), (i, k)
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_learned_shape_receive(cuda, oracle, mode):
+    """CopyToApp over GM-shaped slots: every verdict, checksum and app byte, with a few fragments whose
+    expected checksum is wrong (mask bits exact) and app buffers shorter than some fragments."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(91 + mode)
+    size = 48 << 20
+    frag = torch.empty(size, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(frag, seed=92)
+    host = frag.cpu().numpy()
+    lens, offs, _ = _batches(rng, size)
+    app = torch.empty(N * 70016, dtype=torch.uint8, device=cuda)
+    aoffs = np.arange(N, dtype=np.uint64) * 70016
+    prepared = {}
+    for k, ln in lens.items():
+        app_len = np.where(rng.random(N) < 0.1, ln.astype(np.int64) - 100, ln.astype(np.int64) + 5)
+        csum = oracle.desc_batch(host, offs, ln.astype(np.uint32), None if mode == 1 else
+                                 np.full(N, 0xFFFFFFFF, np.uint32), mode)
+        # AppBufferLen <= 0: DataOK, nothing copied, the checksum of nothing (oracle.copy_to_app)
+        none = app_len <= 0
+        csum = np.where(none, np.uint32(0xFFFFFFFF if mode == 0 else 0), csum).astype(np.uint32)
+        bad = (rng.random(N) < 0.05) & ~none
+        expected = np.where(bad, csum ^ 0x00A4A400, csum).astype(np.uint32)
+        descs = dv.make_recv_descs(frag, offs, app, aoffs, ln, app_len)
+        copy = np.minimum(ln.astype(np.int64), np.maximum(app_len, 0))
+        want_app = np.zeros(app.numel(), np.uint8)
+        for i in range(N):
+            if not bad[i]:
+                a, b, c = int(offs[i]), int(aoffs[i]), int(copy[i])
+                want_app[b:b + c] = host[a:a + c]
+        want_copied = np.where(bad, -1, copy)
+        prepared[k] = (descs, torch.from_numpy(expected.view(np.int32)).to(cuda), csum, bad, want_copied,
+                       torch.from_numpy(want_app).to(cuda))
+    stream = torch.cuda.Stream(device=cuda)
+    with torch.cuda.stream(stream):
+        for i, k in enumerate(SEQUENCE):
+            descs, expected, csum, bad, want_copied, want_app = prepared[k]
+            app.zero_()
+            copied, got, mask, nbad = dv.copy_to_app_batch(descs, expected, mode=mode, stream=stream)
+            assert np.array_equal(dv.as_u32(got), csum), (i, k)
+            assert np.array_equal(dv.mask_bits(mask, N), bad), (i, k)
+            assert int(nbad.item()) == int(bad.sum()), (i, k)
+            assert np.array_equal(copied.cpu().numpy(), want_copied), (i, k)
+            # (a corrupt fragment's bytes may or may not have reached the app buffer: compare the good ones)
+            good = torch.from_numpy(np.repeat(~bad, 70016)).to(cuda)
+            assert torch.equal(app[good], want_app[good]), (i, k)
+
+
+def _ib_lengths(rng, n, odd):
+    """IB-sized fragments (16..2048 bytes, the half-frame edges among them); `odd`: a few fragments the
+    pair kernel cannot take (0, 5, 15, 2049, 4096, 70,000 bytes) at indices the census does not sample,
+    so the learned schedule still picks pairs and their workgroups run the per-fragment fallback."""
+    edge = np.array([16, 17, 31, 32, 33, 1024, 1975, 1976, 2031, 2032, 2047, 2048], np.uint64)
+    ln = np.where(rng.random(n) < 0.6, 1976, np.where(rng.random(n) < 0.5, rng.choice(edge, size=n),
+                                                      rng.integers(16, 2049, size=n))).astype(np.uint64)
+    if odd:
+        sampled = set(int(x) for x in np.arange(64) * n // 64)
+        free = [i for i in range(n) if i not in sampled]
+        pick = rng.choice(free, size=12, replace=False)
+        ln[pick] = rng.choice(np.array([0, 5, 15, 2049, 4096, 70000], np.uint64), size=12)
+    return ln
+
+
+@pytest.mark.parametrize("odd", [False, True], ids=["ib", "ib_odd"])
+def test_learned_pairs_copies(cuda, oracle, odd):
+    """CRC copies of IB-sized fragments: after the census, two fragments to a wave (crc_light_pair_copy_kernel),
+    odd lengths, ragged copies (copylen < csumlen), misaligned sources and destinations, an odd count."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(101 + odd)
+    n = 601
+    ln = _ib_lengths(rng, n, odd)
+    cl = np.where(rng.random(n) < 0.2, ln - np.minimum(ln, rng.integers(0, 24, size=n).astype(np.uint64)), ln)
+    src = torch.empty(n * 70016 + 64, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(src, seed=102)
+    host = src.cpu().numpy()
+    offs = np.arange(n, dtype=np.uint64) * 70016 + rng.integers(0, 16, size=n).astype(np.uint64)
+    dst = torch.empty(n * 70016 + 64, dtype=torch.uint8, device=cuda)
+    doffs = np.arange(n, dtype=np.uint64) * 70016 + rng.integers(0, 16, size=n).astype(np.uint64)
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    descs = dv.make_copy_descs(src, offs, dst, doffs, cl, ln, parts)
+    want = oracle.desc_batch(host, offs, ln.astype(np.uint32), parts.astype(np.uint32), 0)
+    want_dst = np.zeros(dst.numel(), np.uint8)
+    for i in range(n):
+        a, b, c = int(offs[i]), int(doffs[i]), int(cl[i])
+        want_dst[b:b + c] = host[a:a + c]
+    want_dst = torch.from_numpy(want_dst).to(cuda)
+    stream = torch.cuda.Stream(device=cuda)
+    with torch.cuda.stream(stream):
+        for i in range(20):
+            dst.zero_()
+            got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=0, stream=stream))
+            assert np.array_equal(got, want), (i, [(int(j), int(ln[j])) for j in np.nonzero(got != want)[0][:8]])
+            assert torch.equal(dst, want_dst), i
+
+
+@pytest.mark.parametrize("odd", [False, True], ids=["ib", "ib_odd"])
+def test_learned_pairs_receive(cuda, oracle, odd):
+    """CopyToApp of IB-sized fragments after the census picked pairs: checksums, verdicts (a few wrong
+    expected values), AppBufferLen <= 0 / < / >= length, every delivered byte."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(111 + odd)
+    n = 601
+    ln = _ib_lengths(rng, n, odd)
+    frag = torch.empty(n * 70016 + 64, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(frag, seed=112)
+    host = frag.cpu().numpy()
+    offs = np.arange(n, dtype=np.uint64) * 70016 + 8
+    app = torch.empty(n * 70016, dtype=torch.uint8, device=cuda)
+    aoffs = np.arange(n, dtype=np.uint64) * 70016 + rng.integers(0, 8, size=n).astype(np.uint64)
+    app_len = np.where(rng.random(n) < 0.1, ln.astype(np.int64) - 30, ln.astype(np.int64) + 3)
+    csum = oracle.desc_batch(host, offs, ln.astype(np.uint32), np.full(n, 0xFFFFFFFF, np.uint32), 0)
+    none = app_len <= 0
+    csum = np.where(none, np.uint32(0xFFFFFFFF), csum).astype(np.uint32)
+    bad = (rng.random(n) < 0.05) & ~none
+    expected = np.where(bad, csum ^ 0x00A4A400, csum).astype(np.uint32)
+    descs = dv.make_recv_descs(frag, offs, app, aoffs, ln, app_len)
+    copy = np.minimum(ln.astype(np.int64), np.maximum(app_len, 0))
+    want_app = np.zeros(app.numel(), np.uint8)
+    for i in range(n):
+        a, b, c = int(offs[i]), int(aoffs[i]), int(copy[i])
+        want_app[b:b + c] = host[a:a + c]
+    want_app = torch.from_numpy(want_app).to(cuda)
+    exp_t = torch.from_numpy(expected.view(np.int32)).to(cuda)
+    want_copied = np.where(bad, -1, copy)
+    good = torch.from_numpy(np.repeat(~bad, 70016)).to(cuda)
+    stream = torch.cuda.Stream(device=cuda)
+    with torch.cuda.stream(stream):
+        for i in range(20):
+            app.zero_()
+            copied, got, mask, nbad = dv.copy_to_app_batch(descs, exp_t, mode=0, stream=stream)
+            assert np.array_equal(dv.as_u32(got), csum), i
+            assert np.array_equal(dv.mask_bits(mask, n), bad), i
+            assert int(nbad.item()) == int(bad.sum()), i
+            assert np.array_equal(copied.cpu().numpy(), want_copied), i
+            assert torch.equal(app[good], want_app[good]), i
