@@ -2551,7 +2551,7 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
 }
 
 // One fragment (or row group) per wave: item = 4 * blockIdx.x + wave, four waves per workgroup.
-template <class Src, bool kLate = false>
+template <class Src>
 __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src, size_t n,
                                                                   const uint32_t *__restrict__ img,
                                                                   uint32_t *__restrict__ out, uint32_t W,
@@ -2574,11 +2574,9 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     F.init(fi, f < n && !(IsSplit<Src>::value && fi.aux), W, g);
     u32x4 d[4];
     uint32_t o[4];
-    u32x4 head;
-    if constexpr (!kLate) {
-        F.load_row(lane, F.r0, F.live, d, o, F.half);  // (an empty or dead wave's descriptor reads nothing but zeros)
-        head = F.load_head();
-    }
+    // the first row's loads before the table staging (after it: 4 KiB copies 73 -> 66%, profiles/r04/late_loads_ab.txt)
+    F.load_row(lane, F.r0, F.live, d, o, F.half);  // (an empty or dead wave's descriptor reads nothing but zeros)
+    const u32x4 head = F.load_head();
     if constexpr (IsSplit<Src>::value)  // the size split's light launch: most workgroups hold no fragment of its
         if (!__syncthreads_or(F.live)) return;  // class and leave before staging the tables
     build_slices_light(reinterpret_cast<char *>(lds), bs);
@@ -2586,10 +2584,6 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
     __syncthreads();
     if (!F.live) return;
-    if constexpr (kLate) {
-        F.load_row(lane, F.r0, F.live, d, o, F.half);
-        head = F.load_head();
-    }
     light_frag_run(src, f, F, lds, lane, out, [&](uint32_t v) { groups[f * W + g] = v; }, d, o, head);
 }
 
@@ -2760,29 +2754,17 @@ static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uin
                                              hipStream_t s, uint32_t W = 1) {
     W = min(W, 4096u);  // (the join: at most 64 groups per lane)
     while (W > 1 && (size_t)n * W > ((size_t)1 << 26)) W >>= 1;  // (grid: items * 64 threads < 2^32)
-    static const bool late = [] {
-        const char *e = std::getenv("LAMPI_LIGHT_LATE");
-        return e && e[0] == '1';
-    }();
     if (W <= 1) {
-        if (late)
-            hipLaunchKernelGGL((crc_light_frag_copy_kernel<Src, true>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s,
-                               src, n, img, out, 1u, (uint32_t *)nullptr);
-        else
-            hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
-                               img, out, 1u, (uint32_t *)nullptr);
+        hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
+                           img, out, 1u, (uint32_t *)nullptr);
         return hipGetLastError();
     }
     uint32_t *groups = nullptr;
     bool pooled = false;
     hipError_t e = stream_scratch(s, n * W * sizeof(uint32_t), (void **)&groups, &pooled);
     if (e != hipSuccess) return e;
-    if (late)
-        hipLaunchKernelGGL((crc_light_frag_copy_kernel<Src, true>), dim3((unsigned)((n * W + 3) / 4)), dim3(256), 0, s,
-                           src, n, img, out, W, groups);
-    else
-        hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n * W + 3) / 4)), dim3(256), 0, s, src, n,
-                           img, out, W, groups);
+    hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n * W + 3) / 4)), dim3(256), 0, s, src, n, img,
+                       out, W, groups);
     e = hipGetLastError();
     if (e == hipSuccess) {
         uint32_t G = 1;
