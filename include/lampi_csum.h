@@ -64,7 +64,12 @@ enum lampi_csum_mode {
  * r >= 8 walks each fragment's rows in one wave of the table-light kernel (above 16 rows, one wave per
  * 8 rows, joined exactly) -- 1 GiB of GM payloads CRC 56 -> 80%, of 1 MiB / 4 MiB descriptors 57 / 34
  * -> 80%; smaller r and SUM size workgroups by the hinted length and cut fragments of more than 16
- * rows into 16-row segments on the device (out zeroed, parts joined exactly): SUM 61 -> 74%. */
+ * rows into 16-row segments on the device (out zeroed, parts joined exactly): SUM 61 -> 74%.
+ * Without the hint the library learns it: batches of >= 256 descriptors are sampled on the device every
+ * 16th call per stream and entry point, and later batches whose sampled fragments all span 8+ rows
+ * (within a factor of two) run as if the hint had been given; CRC copies / receives of fragments all
+ * <= 2 KiB (IB) run two to a wave.  The hint, when given, wins; LAMPI_CSUM_NO_SHAPES=1 in the environment
+ * turns the learning off.  Results never depend on either. */
 #define LAMPI_CSUM_ROWS_HINT(r) ((int)(((unsigned)(r) & 0xFFFu) << 16))
 #define LAMPI_CSUM_ROWS_HINT_MASK LAMPI_CSUM_ROWS_HINT(0xFFFu)
 #define LAMPI_CSUM_ROWS_HINT_OF(mode) ((((unsigned)(mode)) >> 16) & 0xFFFu)
