@@ -56,6 +56,8 @@ namespace lampi {
 // per-stream device scratch (defined with the launchers)
 static hipError_t stream_scratch(hipStream_t s, size_t bytes, void **out, bool *pooled);
 static hipError_t scratch_done(hipStream_t s, void *p, bool pooled, hipError_t e);
+static hipError_t pair_counters(hipStream_t s, uint32_t **cur, uint32_t **next);
+static hipError_t scratch_done(hipStream_t s, void *p, bool pooled, hipError_t e);
 
 namespace {
 
@@ -2365,6 +2367,29 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
+// Bytes 0..nb-1 of v (nb <= 16, wave-uniform) to offsets ob.. of a buffer descriptor, on the lanes with
+// `on` (the others aimed out of range): whole words as dword stores, then a short and a byte -- byte stores
+// cost (sixteen of them per cut chunk: 445 against 489 us per GiB of IB copies for eight).  Unaligned dword
+// stores are fine; bytes past the descriptor's range (copylen) are dropped, and the caller keeps ob + nb
+// within it unless those bytes are to be dropped.
+__device__ __forceinline__ void store_bytes(const u32x4 &v, __amdgpu_buffer_rsrc_t rs, bool on, uint32_t ob,
+                                            uint32_t nb) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uint32_t o = on ? ob : 0xFFFFFFF0u;  // (o + 15 < 2^32)
+    const uint32_t nw = nb >> 2, rem = nb & 3u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if ((uint32_t)i < nw) __builtin_amdgcn_raw_buffer_store_b32(w[i], rs, o + 4 * i, 0, kBufNt);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if ((uint32_t)i == nw && rem != 0) {
+            if (rem & 2u) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w[i], rs, o + 4 * i, 0, kBufNt);
+            if (rem & 1u)
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[i] >> (8 * (rem & 2u))), rs, o + 4 * i + (rem & 2u), 0,
+                                                     kBufNt);
+        }
+}
+
 // One fragment (or one row group of it) on one wave: geometry, source / destination descriptors and
 // the row loads (ok false: offsets aimed out of range, no memory traffic -- a prefetch past the last
 // row; hf: a half frame's row, chunks q = 0, 1 only).
@@ -2485,26 +2510,33 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
                 __builtin_amdgcn_raw_buffer_store_b128(dc[q], F.drs, full ? oc[q] : 0xFFFFFFF0u, 0, kBufNt);
         }
         // chunks cut by the copy's start or end (at most two per fragment, wave-uniform frame chunks kP and
-        // kE): sixteen byte stores from the one lane holding each, through the destination's buffer
-        // descriptor -- its range check drops the bytes outside [0, copylen) (those before the fragment
-        // have wrapped offsets), so no byte needs a test of its own
+        // kE): sixteen byte stores from one lane each, through the destination's buffer descriptor, whose
+        // range check drops the bytes past copylen -- the start's bytes from the fragment's first 16 (the
+        // head) at offsets 0..15, so no offset is below zero (a wrapped one is not out of range once the
+        // compiler folds the byte index into the instruction offset)
         if constexpr (Src::kCopy) {
-            auto store_cut = [&](uint32_t k) {  // k: the cut chunk's index in the frame, in row r
-                if (lane == (k & 63u)) {
-                    const uint32_t qk = (k >> 6) & 3u;
-                    const u32x4 v = qk == 0 ? dc[0] : qk == 1 ? dc[1] : qk == 2 ? dc[2] : dc[3];
-                    const uint32_t ob = 16u * k - P;
-                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const bool any = fi.copylen != 0;
+            // the start: the fragment's first 16 - sP bytes are the head's first bytes, at offsets 0.. (past
+            // copylen dropped: a word partly past it goes out as bytes)
+            if (any && sP != 0 && (kP >> 8) == r) {
+                const uint32_t nb = 16u - sP;
+                if (fi.copylen >= nb) {
+                    store_bytes(head, F.drs, lane == (kP & 63u), 0u, nb);
+                } else {
+                    const uint32_t w[4] = {head.x, head.y, head.z, head.w};
 #pragma unroll
                     for (int j = 0; j < 16; ++j)
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j >> 2] >> (8 * (j & 3))), F.drs, ob + j, 0,
-                                                             kBufNt);
+                        if ((uint32_t)j < nb && lane == (kP & 63u))
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j >> 2] >> (8 * (j & 3))), F.drs, j, 0,
+                                                                 kBufNt);
                 }
-            };
-            const bool any = fi.copylen != 0;
-            if (any && sP != 0 && (kP >> 8) == r) store_cut(kP);
-            const uint64_t kE = (cend - 1) >> 4;  // the chunk holding the copy's last byte
-            if (any && (cend & 15u) != 0 && (kE >> 8) == r && !(sP != 0 && kE == kP)) store_cut((uint32_t)kE);
+            }
+            const uint64_t kE = (cend - 1) >> 4;  // the chunk holding the copy's last byte (16 kE >= P)
+            if (any && (cend & 15u) != 0 && (kE >> 8) == r && !(sP != 0 && kE == kP)) {
+                const uint32_t qk = (uint32_t)(kE >> 6) & 3u;
+                store_bytes(qk == 0 ? dc[0] : qk == 1 ? dc[1] : qk == 2 ? dc[2] : dc[3], F.drs, lane == (kE & 63u),
+                            (uint32_t)(16u * kE - P), (uint32_t)(cend & 15u));
+            }
         }
         // the register: in row 0, or row 1 when kP is row 0's last chunk
         if (r == 0 || (r == 1 && kP == 255u))
@@ -2593,20 +2625,24 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
 // half frame (front padding P = 2048 - L).  Lane l' = l & 31 holds the frame's chunks k = 32q + l' (frame
 // bytes 512q + 16l', q = 0..3): four chunks, as a lane of a 4 KiB row has, so a wave does one row's
 // lookups for two fragments and the workgroup's table staging serves eight (one wave per 1,976-byte IB
-// payload spent a whole wave's prologue and tree on 4 KB of traffic).  Loads and stores are global with
-// per-lane addresses (two fragments per wave: no single buffer descriptor): chunks wholly in the padding
-// read the table image's zero chunk and store nothing, the chunk cut by the fragment's start is rebuilt
-// from its first 16 bytes, the chunks cut by the copy's ends go out byte by byte.  Horner over the 512-byte
-// step (group table 3 of the light set), a lane tree of three levels within 16-lane rows, the 8-lane
-// groups shifted by 128 (3 - g') through the light group tables, and row_shr:8 + row_bcast:15 leave the
-// fragments' values in lanes 31 and 63.  A workgroup holding a pair that is not two fragments of 16..2048
-// bytes (or a lone last fragment that is not) runs its fragments one after the other through
-// light_frag_run, each on a whole wave.
-// A pair crc_light_pair_copy_kernel cannot take in half frames: fragments f0 and f0 + 1 (if < n), each
-// on the whole wave through light_frag_run.
+// payload spent a whole wave's prologue and tree on 4 KB of traffic).  Each half's geometry is
+// wave-uniform (its descriptor is a scalar load).  Loads are global with per-lane addresses (two
+// fragments: no single buffer descriptor), chunks wholly in the padding reading the table image's zero
+// chunk; the chunk cut by the fragment's start is rebuilt from its first 16 bytes.  Stores go through a
+// buffer descriptor per half, every store instruction issued by every lane with the offsets of lanes
+// that must not store aimed out of range -- whole chunks as 16-byte stores, the chunks cut by the
+// copy's ends as sixteen byte stores -- so no memory operation sits under a branch (the compiler's
+// merged waits after a branch with a store waited for every store to complete: 760 us against 520 per
+// GiB, profiles/r04/pairs_ab.txt).  Horner over the 512-byte step (light group table 3), a three-level
+// lane tree within 16-lane rows, the 8-lane groups shifted by 128 (3 - g') (light group tables 8..10) and
+// row_shr:8 + row_bcast:15 leave the fragments' values in lanes 31 and 63.  A wave holding a fragment
+// under 16 bytes or over 2 KiB stages its part of the tables, leaves its index in a per-stream list and
+// exits; crc_light_pair_leftover_kernel, launched after it, runs those waves' two fragments through
+// light_frag_run (rare; inside this kernel the walk's registers took it from 52 to 137 VGPRs).
+// Fragments f0 and f0 + 1 (if < n) of a leftover pair, each on the whole wave through light_frag_run.
 template <class Src>
 __device__ __forceinline__ void light_pair_fallback(const Src src, size_t f0, size_t n, const uint32_t *lds,
-                                                             uint32_t lane, uint32_t *out) {
+                                                    uint32_t lane, uint32_t *out) {
 #pragma nounroll
     for (uint32_t k = 0; k < 2; ++k) {
         const size_t f = f0 + k;
@@ -2624,10 +2660,11 @@ __device__ __forceinline__ void light_pair_fallback(const Src src, size_t f0, si
 template <class Src>
 __global__ void __launch_bounds__(256) crc_light_pair_copy_kernel(const Src src, size_t n,
                                                                   const uint32_t *__restrict__ img,
-                                                                  uint32_t *__restrict__ out) {
+                                                                  uint32_t *__restrict__ out, uint32_t *left,
+                                                                  uint32_t *__restrict__ list) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    const size_t f0 = ((size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6)) * 2;
+    const size_t wave = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6), f0 = wave * 2;
     constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
     const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
     const uint32_t t2 = min(256u + t, kNibPieces - 1);
@@ -2640,36 +2677,35 @@ __global__ void __launch_bounds__(256) crc_light_pair_copy_kernel(const Src src,
     if (la) fa = src.get(f0);
     if (lb) fb = src.get(f0 + 1);
     auto pairable = [](const FragInfo &x) { return x.len >= 16u && x.len <= (uint32_t)kRowBytes / 2u; };
-    const bool pair = la && pairable(fa) && (!lb || pairable(fb));
-    // this lane's fragment (half-wave h) and its chunk loads, issued before the table staging
+    const bool pair = la && pairable(fa) && (!lb || pairable(fb));  // (wave-uniform)
+    // this lane's half: its fragment's chunks and first 16 bytes, loaded before the table staging
     const uint32_t h = lane >> 5, lp = lane & 31u;
-    const bool live = h ? lb : la;
-    const FragInfo fi = h ? fb : fa;
-    const uint32_t L = fi.len, P = (uint32_t)kRowBytes / 2u - L;  // (pair only: 16 <= L <= 2048)
+    const bool live = pair && (h ? lb : la);
+    gbyte *const addr = h ? fb.addr : fa.addr;
+    const uint32_t L = h ? fb.len : fa.len;
+    const uint32_t P = (uint32_t)kRowBytes / 2u - L;  // (a live half: 16 <= L <= 2048)
+    gbyte *zero = (gbyte *)(img + kImgZero);
     u32x4 d[4];
-    u32x4 head = u32x4{0u, 0u, 0u, 0u};
-    if (pair) {
-        gbyte *zero = (gbyte *)(img + kImgZero);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t x = 512u * q + 16u * lp;  // frame offset of the chunk
-            const bool in = live && x >= P;          // wholly inside the fragment (the frame ends with it)
-            d[q] = ld16c((gu32x4_a1 *)(in ? fi.addr + (x - P) : zero));
-        }
-        head = ld16c((gu32x4_a1 *)(live ? fi.addr : zero));
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = 512u * q + 16u * lp;  // frame offset of the chunk
+        d[q] = ld16c((gu32x4_a1 *)(live && x >= P ? addr + (x - P) : zero));
     }
-    // a workgroup with a pair it cannot take runs all its fragments one after the other, each on a whole
-    // wave (rare; a per-workgroup choice keeps the two paths' registers apart)
-    const bool wg_pair = __syncthreads_and(pair || !la) != 0;
+    u32x4 head = ld16c((gu32x4_a1 *)(live ? addr : zero));
     build_slices_light(reinterpret_cast<char *>(lds), bs);
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
     __syncthreads();
     if (!la) return;
-    if (!wg_pair) {
-        light_pair_fallback(src, f0, n, lds, lane, out);
+    if (!pair) {  // left to crc_light_pair_leftover_kernel
+        if (lane == 0) list[atomicAdd(left, 1u)] = (uint32_t)wave;
         return;
     }
+    // the chunk loads complete, and seen by the compiler as defined here: its waitcnt pass otherwise lost
+    // track of them across the branches below and put a vmcnt(0) -- every store issued so far -- before
+    // each byte store
+    asm volatile("s_waitcnt vmcnt(0) ; lampi-wait %0 %1 %2 %3 %4"
+                 : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(head)::"memory");
     const uint32_t kP = P >> 4, sP = P & 15u;
     if (live && sP != 0 && (kP & 31u) == lp) {  // the chunk cut by the fragment's start
         const u32x4 v = shl_bytes16(head, sP);
@@ -2678,24 +2714,71 @@ __global__ void __launch_bounds__(256) crc_light_pair_copy_kernel(const Src src,
             if ((uint32_t)q == (kP >> 5)) d[q] = v;
     }
     if constexpr (Src::kCopy) {
-        const uint32_t cend = P + fi.copylen;  // the copy's end in the frame (<= 2048)
+        const __amdgpu_buffer_rsrc_t rs0 = light_rsrc(fa.dst, fa.copylen), rs1 = light_rsrc(fb.dst, lb ? fb.copylen : 0u);
+        const uint32_t cend = P + (h ? fb.copylen : fa.copylen);  // the copy's end in the frame (<= 2048)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t x = 512u * q + 16u * lp;
-            if (live && x >= P && x + 16u <= cend) st16u((gwu32x4_a1 *)(fi.dst + (x - P)), d[q]);
+            const bool full = live && x >= P && x + 16u <= cend;
+            __builtin_amdgcn_raw_buffer_store_b128(d[q], rs0, full && h == 0 ? x - P : 0xFFFFFFF0u, 0, kBufNt);
+            __builtin_amdgcn_raw_buffer_store_b128(d[q], rs1, full && h == 1 ? x - P : 0xFFFFFFF0u, 0, kBufNt);
         }
+        // the chunks cut by the copy's start or end (frame chunks kc, wave-uniform per half): sixteen byte
+        // stores, only the lane holding the chunk aimed in range; the descriptor's range check drops the
+        // bytes outside [0, copylen)
+        auto cut = [&](const FragInfo &x, uint32_t hh, const __amdgpu_buffer_rsrc_t &rs) {
+            if (x.copylen == 0) return;
+            const uint32_t Px = (uint32_t)kRowBytes / 2u - x.len, kPx = Px >> 4, sPx = Px & 15u;
+            const uint32_t ce = Px + x.copylen, kE = (ce - 1) >> 4;
+            // the start: the head's first 16 - sP bytes at offsets 0.. (the half's first lane holds the same
+            // head; the rest of the chunk belongs to the next, whole one)
+            if (sPx != 0) {
+                const uint32_t nb = 16u - sPx;
+                if (x.copylen >= nb) {
+                    store_bytes(head, rs, lane == 32u * hh, 0u, nb);
+                } else {
+                    const uint32_t w[4] = {head.x, head.y, head.z, head.w};
+                    const uint32_t o = lane == 32u * hh ? 0u : 0xFFFFFFF0u;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {  // chunks cut by the copy's start or end: byte by byte
-            const uint32_t x = 512u * q + 16u * lp;
-            if (live && !(x >= P && x + 16u <= cend) && x < cend && x + 16u > P) {
-                for (uint32_t j = 0; j < 16; ++j)
-                    if (x + j >= P && x + j < cend)
-                        ((gbyte_w *)fi.dst)[x + j - P] =
-                            (uint8_t)(pick4(d[q].x, d[q].y, d[q].z, d[q].w, (int)(j >> 2)) >> (8u * (j & 3u)));
+                    for (int j = 0; j < 16; ++j)
+                        if ((uint32_t)j < nb)
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j >> 2] >> (8 * (j & 3))), rs, o + j, 0,
+                                                                 kBufNt);
+                }
             }
-        }
+            if ((ce & 15u) != 0 && !(sPx != 0 && kE == kPx)) {
+                const int qk = (int)(kE >> 5);  // (component selects: a select of whole vectors went to scratch)
+                const u32x4 v = {pick4(d[0].x, d[1].x, d[2].x, d[3].x, qk), pick4(d[0].y, d[1].y, d[2].y, d[3].y, qk),
+                                 pick4(d[0].z, d[1].z, d[2].z, d[3].z, qk), pick4(d[0].w, d[1].w, d[2].w, d[3].w, qk)};
+                store_bytes(v, rs, lane == 32u * hh + (kE & 31u), 16u * kE - Px, ce & 15u);
+            }
+        };
+        cut(fa, 0u, rs0);
+        if (lb) cut(fb, 1u, rs1);
     }
-    if (live) inject_register(d, P, fi.partial, [&](int q) { return 32u * q + lp; });
+    // the register enters as data at frame offset P: words w, w + 1 of chunk kP (shifted by sP % 4 bytes),
+    // spilling into chunk kP + 1 for w = 3 -- wave-uniform per half, only the lanes holding those chunks
+    // change
+    auto inject = [&](const FragInfo &x, uint32_t hh) {
+        const uint32_t Px = (uint32_t)kRowBytes / 2u - x.len, kPx = Px >> 4, sPx = Px & 15u;
+        const uint32_t inj = __builtin_bswap32(x.partial), w = sPx >> 2, m = (sPx & 3u) * 8u;
+        const uint32_t lo = inj << m, hi = m ? inj >> (32u - m) : 0u;
+        auto xor_word = [&](uint32_t k, uint32_t c, uint32_t val) {  // (k, c uniform)
+            if (lane != 32u * hh + (k & 31u)) return;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((uint32_t)q == (k >> 5)) {
+                    if (c == 0) d[q].x ^= val;
+                    else if (c == 1) d[q].y ^= val;
+                    else if (c == 2) d[q].z ^= val;
+                    else d[q].w ^= val;
+                }
+        };
+        xor_word(kPx, w, lo);
+        if (hi != 0u) xor_word(w == 3u ? kPx + 1u : kPx, w == 3u ? 0u : w + 1u, hi);
+    };
+    inject(fa, 0u);
+    if (lb) inject(fb, 1u);
     uint32_t lanec2, sel[4];
     light_lane_consts(lane, lanec2, sel);
     constexpr uint32_t kShift512 = kLtNib + kLtTab * (4u + 3u);  // group table 3: 128 * (7 - 3) bytes
@@ -2707,13 +2790,51 @@ __global__ void __launch_bounds__(256) crc_light_pair_copy_kernel(const Src src,
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<1>(lds, v), 0x111, 0xF, 0xF, false);  // row_shr:1
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<2>(lds, v), 0x112, 0xF, 0xF, false);  // row_shr:2
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)light_shift<3>(lds, v), 0x114, 0xF, 0xF, false);  // row_shr:4
-    // group g' = (lane >> 3) & 3 of the half: shift by 128 (3 - g') through light group table 4 + (g' + 4)
+    // group g' = (lane >> 3) & 3 of the half: shift by 128 (3 - g') through light group table 8 + g'
     const uint32_t gq = (lane >> 3) & 3u;
     const uint32_t wv = light_shift_at(lds, kLtNib + kLtTab * (8u + min(gq, 2u)), v);
     v = gq < 3u ? wv : v;
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 (rows 1, 3)
-    if (live && lp == 31u) emit(src, out, f0 + h, __builtin_bswap32(v), fi);
+    if (lp == 31u && (h ? lb : la)) emit(src, out, f0 + h, __builtin_bswap32(v), h ? fb : fa);
+}
+
+// The pair kernel's leftover waves (list[0 .. *left): wave indices, two fragments each) on a fixed grid: a
+// workgroup stages the tables only if one of its waves has an entry.  Calls alternate between two counters:
+// this one zeroes the other, which the stream's next call counts in (no workgroup ever waits for another).
+template <class Src>
+__global__ void __launch_bounds__(256) crc_light_pair_leftover_kernel(const Src src, size_t n,
+                                                                      const uint32_t *__restrict__ img,
+                                                                      uint32_t *__restrict__ out, const uint32_t *left,
+                                                                      uint32_t *next_left,
+                                                                      const uint32_t *__restrict__ list,
+                                                                      uint32_t *shape_nhalf) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const uint32_t c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    // leftovers: the stream's batches are no longer all IB-sized -- tell the host's next call (the learned
+    // shape's count of fragments <= 2 KiB, host-mapped) before the census would
+    if (c != 0 && blockIdx.x == 0 && t == 0 && shape_nhalf) {
+        *(volatile uint32_t *)shape_nhalf = 0u;
+        __threadfence_system();
+    }
+    if (blockIdx.x * 4u < c) {
+        constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
+        const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+        const uint32_t t2 = min(256u + t, kNibPieces - 1);
+        const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
+        u32x4 bs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
+        build_slices_light(reinterpret_cast<char *>(lds), bs);
+        reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
+        reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
+        __syncthreads();
+        for (uint32_t e = blockIdx.x * 4u + w; e < c; e += gridDim.x * 4u)
+            light_pair_fallback(src, (size_t)list[e] * 2, n, lds, lane, out);
+    }
+    if (blockIdx.x == 0 && t == 0) *next_left = 0u;  // the stream's next call counts there
 }
 
 // The fragments of more than one row group: value = XOR over the groups of group g shifted past the rows
@@ -2740,12 +2861,27 @@ __global__ void __launch_bounds__(256) crc_light_group_join_kernel(const Src src
     if (j == 0) emit(src, out, f, acc, fi);
 }
 
+constexpr unsigned kLeftoverWgs = 256;  // (four waves each; the leftover path is rare)
+
 template <class Src>
 static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
-                                             hipStream_t s) {
-    hipLaunchKernelGGL(crc_light_pair_copy_kernel<Src>, dim3((unsigned)((n + 7) / 8)), dim3(256), 0, s, src, n, img,
-                       out);
-    return hipGetLastError();
+                                             hipStream_t s, uint32_t *shape_nhalf) {
+    uint32_t *left = nullptr, *next_left = nullptr, *list = nullptr;
+    hipError_t e = pair_counters(s, &left, &next_left);
+    if (e != hipSuccess) return e;
+    const size_t nwg = (n + 7) / 8;
+    bool pooled = false;
+    e = stream_scratch(s, nwg * sizeof(uint32_t), (void **)&list, &pooled);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(crc_light_pair_copy_kernel<Src>, dim3((unsigned)nwg), dim3(256), 0, s, src, n, img, out, left,
+                       list);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(crc_light_pair_leftover_kernel<Src>, dim3(kLeftoverWgs), dim3(256), 0, s, src, n, img, out,
+                           (const uint32_t *)left, next_left, (const uint32_t *)list, shape_nhalf);
+        e = hipGetLastError();
+    }
+    return scratch_done(s, list, pooled, e);
 }
 
 // W: row groups per fragment (1: one wave walks all the fragment's rows)
@@ -4021,6 +4157,7 @@ struct BatchShape {
     uint32_t pad[3];
 };
 constexpr int kShapeKinds = 3;  // read-only descriptors, copy descriptors, receive descriptors
+constexpr int64_t kLeftBytes = 256;
 
 struct ScratchTable {
     struct Slot {
@@ -4028,6 +4165,8 @@ struct ScratchTable {
         size_t cap = 0;
         BatchShape *shape[kShapeKinds] = {};  // host-mapped (coherent), lazily allocated
         uint32_t calls[kShapeKinds] = {};
+        uint32_t *left = nullptr;  // the pair kernel's two leftover counters (device, zeroed at creation)
+        uint32_t left_calls = 0;
     };
     std::map<std::pair<int, hipStream_t>, Slot> slots;
     ScratchTable() = default;
@@ -4051,6 +4190,10 @@ struct ScratchTable {
             (void)hipStreamSynchronize(it->first.second);
             (void)hipFree(it->second.p);
             g_scratch_bytes.fetch_sub((int64_t)it->second.cap, std::memory_order_relaxed);
+            if (it->second.left) {
+                (void)hipFree(it->second.left);
+                g_scratch_bytes.fetch_sub(kLeftBytes, std::memory_order_relaxed);
+            }
             for (BatchShape *&b : it->second.shape)
                 if (b) {
                     (void)hipHostFree(b);
@@ -4093,6 +4236,31 @@ static hipError_t stream_scratch(hipStream_t s, size_t bytes, void **out, bool *
         g_scratch_bytes.fetch_add((int64_t)want, std::memory_order_relaxed);
     }
     *out = slot.p;
+    return hipSuccess;
+}
+
+// The pair kernel's leftover counters for stream s (this thread's): two, zeroed on the stream when created;
+// calls alternate between them, each call's leftover kernel zeroing the next call's.
+static hipError_t pair_counters(hipStream_t s, uint32_t **cur, uint32_t **next) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    ScratchTable::Slot &slot = t_scratch.slots[{dev, s}];
+    if (!slot.left) {
+        void *p = nullptr;
+        e = hipMalloc(&p, kLeftBytes);
+        if (e != hipSuccess) return e;
+        e = hipMemsetAsync(p, 0, kLeftBytes, s);
+        if (e != hipSuccess) {
+            (void)hipFree(p);
+            return e;
+        }
+        slot.left = (uint32_t *)p;
+        g_scratch_bytes.fetch_add(kLeftBytes, std::memory_order_relaxed);
+    }
+    const uint32_t par = slot.left_calls++ & 1u;
+    *cur = slot.left + par;
+    *next = slot.left + (par ^ 1u);
     return hipSuccess;
 }
 
@@ -4169,7 +4337,7 @@ static bool shapes_enabled() {
 // batches of this kind (launching the census for later ones when due).
 template <class Src>
 static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int kind, uint32_t rows_hint,
-                                  bool *pairs = nullptr) {
+                                  bool *pairs = nullptr, uint32_t **nhalf_dev = nullptr) {
     if (pairs) *pairs = false;
     if (rows_hint > 1 || n < kShapeMin || !shapes_enabled()) return rows_hint;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -4196,7 +4364,15 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     std::atomic_thread_fence(std::memory_order_acquire);
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= kShapeRows && rmax <= 2 * rmin) W = rmax;
-        if (pairs && nhalf == sampled) *pairs = true;  // every sampled fragment at most 2 KiB: two per wave
+        if (pairs && nhalf == sampled) {  // every sampled fragment at most 2 KiB: two per wave
+            void *dp = nullptr;
+            if (nhalf_dev && hipHostGetDevicePointer(&dp, rec, 0) == hipSuccess) {
+                *pairs = true;
+                *nhalf_dev = &((BatchShape *)dp)->nhalf;
+            } else {
+                (void)hipGetLastError();
+            }
+        }
     }
     const uint32_t c = slot.calls[kind]++;
     if (c % kShapeEvery == 0) {
@@ -4462,8 +4638,9 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
     if (n == 0) return hipSuccess;
     if (!img) return hipErrorInvalidValue;  // the tables (CRC)
     bool pairs = false;
-    rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, mode == LAMPI_CSUM_CRC32 ? &pairs : nullptr);
-    if (pairs) return launch_crc_light_pair_copy(CopySource{d}, n, img, out, s);
+    uint32_t *nhalf = nullptr;
+    rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, mode == LAMPI_CSUM_CRC32 ? &pairs : nullptr, &nhalf);
+    if (pairs) return launch_crc_light_pair_copy(CopySource{d}, n, img, out, s, nhalf);
     if (mode == LAMPI_CSUM_CRC32)
         return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
     return launch_sum_copy_groups(CopySource{d}, n, out, s, rows_hint);
@@ -4479,8 +4656,9 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
     const bool crc = mode == LAMPI_CSUM_CRC32;
     const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
     bool pairs = false;
-    rows_hint = learned_rows_hint(src, n, s, 2, rows_hint, crc ? &pairs : nullptr);
-    if (pairs) return launch_crc_light_pair_copy(src, n, img, csum, s);
+    uint32_t *nhalf = nullptr;
+    rows_hint = learned_rows_hint(src, n, s, 2, rows_hint, crc ? &pairs : nullptr, &nhalf);
+    if (pairs) return launch_crc_light_pair_copy(src, n, img, csum, s, nhalf);
     if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s, rows_hint);
     return launch_sum_copy_groups(src, n, csum, s, rows_hint);
 }
