@@ -2489,6 +2489,12 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
     const uint32_t kP = P >> 4, sP = P & 15u;        // the chunk holding the fragment's first byte, and where
     const uint64_t cend = (uint64_t)fi.copylen + P;  // the copy's end in the frame
     uint32_t acc = 0;
+    // the copy of the chunk cut by the fragment's start: the head's first min(16 - sP, copylen) bytes at
+    // offsets 0.. from the lane holding it (the chunk's own offsets start below zero, which is not out of
+    // range once the compiler folds the byte index into the instruction offset; here, outside the row loop,
+    // it costs no registers there)
+    if constexpr (Src::kCopy)
+        if (r0 == 0 && sP != 0) store_bytes(head, F.drs, lane == (kP & 63u), 0u, min(16u - sP, fi.copylen));
     // (hf: BoolC<true> for a half frame -- its own copy of the body, kept out of the row loop)
     auto step = [&](auto hf, uint32_t r, u32x4 (&dc)[4], const uint32_t (&oc)[4], u32x4 (&dn)[4],
                     uint32_t (&on)[4]) {
@@ -2516,26 +2522,17 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
         // compiler folds the byte index into the instruction offset)
         if constexpr (Src::kCopy) {
             const bool any = fi.copylen != 0;
-            // the start: the fragment's first 16 - sP bytes are the head's first bytes, at offsets 0.. (past
-            // copylen dropped: a word partly past it goes out as bytes)
-            if (any && sP != 0 && (kP >> 8) == r) {
-                const uint32_t nb = 16u - sP;
-                if (fi.copylen >= nb) {
-                    store_bytes(head, F.drs, lane == (kP & 63u), 0u, nb);
-                } else {
-                    const uint32_t w[4] = {head.x, head.y, head.z, head.w};
-#pragma unroll
-                    for (int j = 0; j < 16; ++j)
-                        if ((uint32_t)j < nb && lane == (kP & 63u))
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j >> 2] >> (8 * (j & 3))), F.drs, j, 0,
-                                                                 kBufNt);
-                }
-            }
-            const uint64_t kE = (cend - 1) >> 4;  // the chunk holding the copy's last byte (16 kE >= P)
-            if (any && (cend & 15u) != 0 && (kE >> 8) == r && !(sP != 0 && kE == kP)) {
+            // the end (the start went out with the head, above): the chunk holding the copy's last byte
+            // (16 kE >= P: no offset below zero)
+            const uint64_t kE = (cend - 1) >> 4;
+            if (any && (cend & 15u) != 0 && (kE >> 8) == r && !(sP != 0 && kE == kP) && lane == (kE & 63u)) {
                 const uint32_t qk = (uint32_t)(kE >> 6) & 3u;
-                store_bytes(qk == 0 ? dc[0] : qk == 1 ? dc[1] : qk == 2 ? dc[2] : dc[3], F.drs, lane == (kE & 63u),
-                            (uint32_t)(16u * kE - P), (uint32_t)(cend & 15u));
+                const u32x4 v = qk == 0 ? dc[0] : qk == 1 ? dc[1] : qk == 2 ? dc[2] : dc[3];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                const uint32_t ob = (uint32_t)(16u * kE - P);
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j >> 2] >> (8 * (j & 3))), F.drs, ob + j, 0, kBufNt);
             }
         }
         // the register: in row 0, or row 1 when kP is row 0's last chunk
@@ -2732,20 +2729,7 @@ __global__ void __launch_bounds__(256) crc_light_pair_copy_kernel(const Src src,
             const uint32_t ce = Px + x.copylen, kE = (ce - 1) >> 4;
             // the start: the head's first 16 - sP bytes at offsets 0.. (the half's first lane holds the same
             // head; the rest of the chunk belongs to the next, whole one)
-            if (sPx != 0) {
-                const uint32_t nb = 16u - sPx;
-                if (x.copylen >= nb) {
-                    store_bytes(head, rs, lane == 32u * hh, 0u, nb);
-                } else {
-                    const uint32_t w[4] = {head.x, head.y, head.z, head.w};
-                    const uint32_t o = lane == 32u * hh ? 0u : 0xFFFFFFF0u;
-#pragma unroll
-                    for (int j = 0; j < 16; ++j)
-                        if ((uint32_t)j < nb)
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j >> 2] >> (8 * (j & 3))), rs, o + j, 0,
-                                                                 kBufNt);
-                }
-            }
+            if (sPx != 0) store_bytes(head, rs, lane == 32u * hh, 0u, min(16u - sPx, x.copylen));
             if ((ce & 15u) != 0 && !(sPx != 0 && kE == kPx)) {
                 const int qk = (int)(kE >> 5);  // (component selects: a select of whole vectors went to scratch)
                 const u32x4 v = {pick4(d[0].x, d[1].x, d[2].x, d[3].x, qk), pick4(d[0].y, d[1].y, d[2].y, d[3].y, qk),
