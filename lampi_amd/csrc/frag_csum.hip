@@ -284,7 +284,7 @@ struct RecvSource {
     const uint8_t *expected;   // expected checksum of fragment f at expected + f * exp_stride
     size_t exp_stride;
     int64_t *copied;           // CopyToApp's return: lengthToCopy, or -1 when corrupt
-    uint32_t *mask;            // bit f set when corrupt (zeroed by the launcher)
+    uint32_t *mask;            // bit f set when corrupt (zeroed by zero_verdicts_kernel first)
     uint32_t *nbad;
     __device__ static uint32_t to_copy(const lampi_recv_desc &x) {
         return x.app_len <= 0 ? 0u : (x.app_len < (int64_t)x.length ? (uint32_t)x.app_len : x.length);
@@ -2869,11 +2869,17 @@ static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uin
 }
 
 // W: row groups per fragment (1: one wave walks all the fragment's rows)
+// the row groups a light launch runs with for a hint of W
+static uint32_t light_groups(size_t n, uint32_t W) {
+    W = min(W, 4096u);  // (the join: at most 64 groups per lane)
+    while (W > 1 && (size_t)n * W > ((size_t)1 << 26)) W >>= 1;  // (grid: items * 64 threads < 2^32)
+    return W;
+}
+
 template <class Src>
 static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
                                              hipStream_t s, uint32_t W = 1) {
-    W = min(W, 4096u);  // (the join: at most 64 groups per lane)
-    while (W > 1 && (size_t)n * W > ((size_t)1 << 26)) W >>= 1;  // (grid: items * 64 threads < 2^32)
+    W = light_groups(n, W);
     if (W <= 1) {
         hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
                            img, out, 1u, (uint32_t *)nullptr);
@@ -4630,18 +4636,31 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
     return launch_sum_copy_groups(CopySource{d}, n, out, s, rows_hint);
 }
 
+// The receive step's mask words and bad count, zeroed in one launch (two memsets were two ~5 us stream
+// operations per call, 2.5% of a GiB of GM receives)
+__global__ void __launch_bounds__(256) zero_verdicts_kernel(uint32_t *__restrict__ mask, size_t nwords,
+                                                            uint32_t *__restrict__ nbad) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nwords) mask[i] = 0u;
+    if (i == 0) *nbad = 0u;
+}
+
 hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t *expected, size_t exp_stride,
                               int64_t *copied, uint32_t *csum, uint32_t *mask, uint32_t *nbad, int mode,
                               const uint32_t *img, hipStream_t s, uint32_t rows_hint) {
-    hipError_t e = hipMemsetAsync(nbad, 0, sizeof(uint32_t), s);
-    if (e == hipSuccess && n) e = hipMemsetAsync(mask, 0, (n + 31) / 32 * sizeof(uint32_t), s);
-    if (e != hipSuccess || n == 0) return e;
+    if (n == 0) return hipMemsetAsync(nbad, 0, sizeof(uint32_t), s);
     if (!img) return hipErrorInvalidValue;
     const bool crc = mode == LAMPI_CSUM_CRC32;
     const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
     bool pairs = false;
     uint32_t *nhalf = nullptr;
     rows_hint = learned_rows_hint(src, n, s, 2, rows_hint, crc ? &pairs : nullptr, &nhalf);
+    // (not in the row groups' first launch: a fragment of one group gives its verdict there)
+    const size_t nwords = (n + 31) / 32;
+    hipLaunchKernelGGL(zero_verdicts_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, mask, nwords,
+                       nbad);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     if (pairs) return launch_crc_light_pair_copy(src, n, img, csum, s, nhalf);
     if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s, rows_hint);
     return launch_sum_copy_groups(src, n, csum, s, rows_hint);
