@@ -2,7 +2,7 @@
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
 #   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchCsum | benchD | bcopy |
-#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | pmcdesc | e2e | recv | gm | bigdesc
+#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | pmcdesc | e2e | latency | recv | gm | bigdesc
 # Any failure (a test failure, fault, abort, segfault, timeout or kill) ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -64,6 +64,7 @@ for step in "$@"; do
                  --frag-bytes $fb --rows-hint $h --steps 5 --warmup 1 --no-cpu-baseline || exit 1
              done ;;
     e2e) run e2e 600 python bench.py --e2e ;;
+    latency) run latency 300 python bench.py --latency ;;
     recv) run recv 600 python bench.py --recv --steps 10 &&
           run recvsum 600 python bench.py --recv --mode sum --steps 10 ;;
     bcopy) run bcopy 600 python bench.py --bcopy --steps 10 &&
