@@ -2,7 +2,7 @@
 # tools/gpu_session.sh -- run GPU steps on the gpurun box with a time limit each.
 # Usage: tools/gpu_session.sh STEP [STEP ...]   where STEP is one of:
 #   smoke | tests | tests_native | tests_bcopy | bench | bench16k | benchsum | benchC | benchCsum | benchD | bcopy |
-#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | pmcdesc | e2e | latency | recv | gm | bigdesc
+#   prof | profC | pmc | pmcC | pmcCsum | pmcDshard | pmcbcopy | pmcsq | pmcdesc | e2e | latency | copysizes | recv | gm | bigdesc
 # Any failure (a test failure, fault, abort, segfault, timeout or kill) ends the session.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -65,6 +65,8 @@ for step in "$@"; do
              done ;;
     e2e) run e2e 600 python bench.py --e2e ;;
     latency) run latency 300 python bench.py --latency ;;
+    copysizes) run copysizes_crc 400 python tools/microbench/desc_copy_sizes.py crc &&
+               run copysizes_sum 400 python tools/microbench/desc_copy_sizes.py sum ;;
     recv) run recv 600 python bench.py --recv --steps 10 &&
           run recvsum 600 python bench.py --recv --mode sum --steps 10 ;;
     bcopy) run bcopy 600 python bench.py --bcopy --steps 10 &&
