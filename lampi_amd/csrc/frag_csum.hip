@@ -3304,6 +3304,40 @@ __device__ __forceinline__ void store_head16(gwbyte *q, const u32x4 &v, uint32_t
 // 71.5 / 61.4 -> 69.9 / 58.1%; 64 threads: small fragments faster still (64 B 3.4x) but +8 and +1
 // destinations 66%; 192: 75.7%.  The row kernel keeps 256 (128 / 64: GM slots 75 -> 71 / 64%).
 constexpr int kSumWgThreads = 128;
+
+// One fragment's copy and partial sum on kT threads (thread t of them): returns the thread's sum.
+template <int kT, class Src>
+__device__ __forceinline__ uint32_t sum_copy_frag(const FragInfo &fi, uint32_t t) {
+    gbyte *p = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
+    gwbyte *q = (gwbyte *)uniform64((uint64_t)(uintptr_t)fi.dst);
+    const uint32_t len = uniform(fi.len), clen = uniform(fi.copylen);  // clen <= len
+    const uint32_t nfull = len / 16u, cfull = clen / 16u;  // whole 16-byte chunks
+    const uint32_t R = (nfull + kT - 1) / kT;
+    // the loop moves whole chunks only (chunk c = kT r + t); the chunk the copy ends inside is kept (vc) and
+    // the fragment's partial last chunk is read after the loop
+    uint32_t acc = 0;
+    u32x4 v = {0u, 0u, 0u, 0u}, vc = {0u, 0u, 0u, 0u};
+    if (t < nfull) v = ld16u((gu32x4_a1 *)(p + 16u * t));
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t c = kT * r + t;
+        u32x4 nv = {0u, 0u, 0u, 0u};
+        if (c + kT < nfull) nv = ld16u((gu32x4_a1 *)(p + 16u * (c + kT)));
+        if (c < cfull)
+            st16u((gwu32x4_a1 *)(q + 16u * c), v);
+        else if (c == cfull)
+            vc = v;
+        acc += v.x + v.y + v.z + v.w;
+        v = nv;
+    }
+    if ((len & 15u) && t == nfull % kT) {  // the fragment's last 1-15 bytes
+        const u32x4 w = load_tail16(p + 16u * nfull, len & 15u);
+        acc += w.x + w.y + w.z + w.w;
+        if (cfull == nfull) vc = w;
+    }
+    if ((clen & 15u) && t == cfull % kT) store_head16(q + 16u * cfull, vc, clen & 15u);
+    return acc;
+}
+
 template <class Src, int kT = kSumWgThreads>
 __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
     static_assert(Src::kCopy && !Src::kPhase, "word-grid copy sources only");
@@ -3313,35 +3347,8 @@ __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint
     uint32_t it = 0;
     // a grid has at most 2^32 - 1 threads: beyond kMaxWgGrid fragments a workgroup takes several
     for (size_t f = blockIdx.x; f < n; f += gridDim.x, it ^= 1u) {
-        FragInfo fi = src.get(f);
-        gbyte *p = (gbyte *)uniform64((uint64_t)(uintptr_t)fi.addr);
-        gwbyte *q = (gwbyte *)uniform64((uint64_t)(uintptr_t)fi.dst);
-        const uint32_t len = uniform(fi.len), clen = uniform(fi.copylen);  // clen <= len
-        const uint32_t nfull = len / 16u, cfull = clen / 16u;  // whole 16-byte chunks
-        const uint32_t R = (nfull + kT - 1) / kT;
-        // the loop moves whole chunks only (chunk c = kT r + t); the chunk the copy ends inside
-        // is kept (vc) and the fragment's partial last chunk is read after the loop
-        uint32_t acc = 0;
-        u32x4 v = {0u, 0u, 0u, 0u}, vc = {0u, 0u, 0u, 0u};
-        if (t < nfull) v = ld16u((gu32x4_a1 *)(p + 16u * t));
-        for (uint32_t r = 0; r < R; ++r) {
-            const uint32_t c = kT * r + t;
-            u32x4 nv = {0u, 0u, 0u, 0u};
-            if (c + kT < nfull) nv = ld16u((gu32x4_a1 *)(p + 16u * (c + kT)));
-            if (c < cfull)
-                st16u((gwu32x4_a1 *)(q + 16u * c), v);
-            else if (c == cfull)
-                vc = v;
-            acc += v.x + v.y + v.z + v.w;
-            v = nv;
-        }
-        if ((len & 15u) && t == nfull % kT) {  // the fragment's last 1-15 bytes
-            const u32x4 w = load_tail16(p + 16u * nfull, len & 15u);
-            acc += w.x + w.y + w.z + w.w;
-            if (cfull == nfull) vc = w;
-        }
-        if ((clen & 15u) && t == cfull % kT) store_head16(q + 16u * cfull, vc, clen & 15u);
-        acc = wave_add(acc);
+        const FragInfo fi = src.get(f);
+        uint32_t acc = wave_add(sum_copy_frag<kT, Src>(fi, t));
         if constexpr (kW == 1) {
             if (t == 0) emit(src, out, f, acc, fi);
         } else {
@@ -3354,6 +3361,21 @@ __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint
                 emit(src, out, f, sm, fi);
             }
         }
+    }
+}
+
+// Fragments of at most 2 KiB (IB's payloads; the learned batch shape picks it): one fragment per wave, four
+// to a workgroup -- one workgroup per 1,976-byte fragment made the grid's dispatch the bound (522K
+// workgroups per GiB).  Exact for any length.
+template <class Src>
+__global__ void __launch_bounds__(256) sum_copy_waves_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
+    static_assert(Src::kCopy && !Src::kPhase, "word-grid copy sources only");
+    const uint32_t lane = threadIdx.x & 63u;
+    for (size_t f = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); f < n;
+         f += (size_t)gridDim.x * 4) {
+        const FragInfo fi = src.get(f);
+        const uint32_t acc = wave_add(sum_copy_frag<64, Src>(fi, lane));
+        if (lane == 0) emit(src, out, f, acc, fi);
     }
 }
 
@@ -4598,17 +4620,22 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
 // Fused-copy SUM (bcopy_uicsum, LA-MPI's default mode): sum_copy_wg_kernel, one short-lived
 // workgroup per fragment (the textbook copy shape).
 template <class Src>
-static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t s) {
-    hipLaunchKernelGGL(sum_copy_wg_kernel<Src>, dim3((unsigned)std::min<size_t>(n, kMaxWgGrid)), dim3(kSumWgThreads), 0, s, src,
-                       n, out);
+static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t s, bool small = false) {
+    if (small)
+        hipLaunchKernelGGL(sum_copy_waves_kernel<Src>, dim3((unsigned)std::min<size_t>((n + 3) / 4, kMaxWgGrid)),
+                           dim3(256), 0, s, src, n, out);
+    else
+        hipLaunchKernelGGL(sum_copy_wg_kernel<Src>, dim3((unsigned)std::min<size_t>(n, kMaxWgGrid)), dim3(kSumWgThreads),
+                           0, s, src, n, out);
 }
 
 // With LAMPI_CSUM_ROWS_HINT (W > 1): each fragment as W row-group workgroups, their sums joined.
 template <class Src>
-static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out, hipStream_t s, uint32_t W) {
+static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out, hipStream_t s, uint32_t W,
+                                         bool small = false) {
     while (W > 1 && (size_t)n * W > ((size_t)1 << 31)) W >>= 1;
     if (W <= 1) {
-        launch_sum_copy(src, n, out, s);
+        launch_sum_copy(src, n, out, s, small);
         return hipGetLastError();
     }
     uint32_t *groups = nullptr;
@@ -4632,12 +4659,10 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
     bool pairs = false;
     uint32_t *nhalf = nullptr;
     const bool crc = mode == LAMPI_CSUM_CRC32;
-    rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, crc ? &pairs : nullptr, &nhalf,
-                                  crc ? kShapeRows : kShapeRowsSum);
-    if (pairs) return launch_crc_light_pair_copy(CopySource{d}, n, img, out, s, nhalf);
-    if (mode == LAMPI_CSUM_CRC32)
-        return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
-    return launch_sum_copy_groups(CopySource{d}, n, out, s, rows_hint);
+    rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, &pairs, &nhalf, crc ? kShapeRows : kShapeRowsSum);
+    if (crc && pairs) return launch_crc_light_pair_copy(CopySource{d}, n, img, out, s, nhalf);
+    if (crc) return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
+    return launch_sum_copy_groups(CopySource{d}, n, out, s, rows_hint, pairs);  // (pairs: a wave per fragment)
 }
 
 // The receive step's mask words and bad count, zeroed in one launch (two memsets were two ~5 us stream
@@ -4658,17 +4683,16 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
     const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
     bool pairs = false;
     uint32_t *nhalf = nullptr;
-    rows_hint = learned_rows_hint(src, n, s, 2, rows_hint, crc ? &pairs : nullptr, &nhalf,
-                                  crc ? kShapeRows : kShapeRowsSum);
+    rows_hint = learned_rows_hint(src, n, s, 2, rows_hint, &pairs, &nhalf, crc ? kShapeRows : kShapeRowsSum);
     // (not in the row groups' first launch: a fragment of one group gives its verdict there)
     const size_t nwords = (n + 31) / 32;
     hipLaunchKernelGGL(zero_verdicts_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, mask, nwords,
                        nbad);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (pairs) return launch_crc_light_pair_copy(src, n, img, csum, s, nhalf);
+    if (crc && pairs) return launch_crc_light_pair_copy(src, n, img, csum, s, nhalf);
     if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s, rows_hint);
-    return launch_sum_copy_groups(src, n, csum, s, rows_hint);
+    return launch_sum_copy_groups(src, n, csum, s, rows_hint, pairs);  // (pairs: a wave per fragment)
 }
 
 hipError_t launch_sum64_desc(const lampi_frag_desc *d, size_t n, uint64_t *out, bool phased, hipStream_t s) {

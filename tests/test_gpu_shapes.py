@@ -158,10 +158,12 @@ def _ib_lengths(rng, n, odd):
     return ln
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 @pytest.mark.parametrize("odd", [False, True], ids=["ib", "ib_odd"])
-def test_learned_pairs_copies(cuda, oracle, odd):
-    """CRC copies of IB-sized fragments: after the census, two fragments to a wave (crc_light_pair_copy_kernel),
-    odd lengths, ragged copies (copylen < csumlen), misaligned sources and destinations, an odd count."""
+def test_learned_pairs_copies(cuda, oracle, odd, mode):
+    """Copies of IB-sized fragments after the census: CRC two fragments to a wave (crc_light_pair_copy_kernel),
+    SUM one fragment per wave four to a workgroup (sum_copy_waves_kernel); odd lengths, ragged copies
+    (copylen < csumlen), misaligned sources and destinations, an odd count."""
     import torch
 
     dv = _dv()
@@ -176,8 +178,8 @@ def test_learned_pairs_copies(cuda, oracle, odd):
     dst = torch.empty(n * 70016 + 64, dtype=torch.uint8, device=cuda)
     doffs = np.arange(n, dtype=np.uint64) * 70016 + rng.integers(0, 16, size=n).astype(np.uint64)
     parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
-    descs = dv.make_copy_descs(src, offs, dst, doffs, cl, ln, parts)
-    want = oracle.desc_batch(host, offs, ln.astype(np.uint32), parts.astype(np.uint32), 0)
+    descs = dv.make_copy_descs(src, offs, dst, doffs, cl, ln, parts if mode == 0 else None)
+    want = oracle.desc_batch(host, offs, ln.astype(np.uint32), parts.astype(np.uint32) if mode == 0 else None, mode)
     want_dst = np.zeros(dst.numel(), np.uint8)
     for i in range(n):
         a, b, c = int(offs[i]), int(doffs[i]), int(cl[i])
@@ -187,13 +189,14 @@ def test_learned_pairs_copies(cuda, oracle, odd):
     with torch.cuda.stream(stream):
         for i in range(20):
             dst.zero_()
-            got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=0, stream=stream))
+            got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=mode, stream=stream))
             assert np.array_equal(got, want), (i, [(int(j), int(ln[j])) for j in np.nonzero(got != want)[0][:8]])
             assert torch.equal(dst, want_dst), i
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 @pytest.mark.parametrize("odd", [False, True], ids=["ib", "ib_odd"])
-def test_learned_pairs_receive(cuda, oracle, odd):
+def test_learned_pairs_receive(cuda, oracle, odd, mode):
     """CopyToApp of IB-sized fragments after the census picked pairs: checksums, verdicts (a few wrong
     expected values), AppBufferLen <= 0 / < / >= length, every delivered byte."""
     import torch
@@ -209,9 +212,10 @@ def test_learned_pairs_receive(cuda, oracle, odd):
     app = torch.empty(n * 70016, dtype=torch.uint8, device=cuda)
     aoffs = np.arange(n, dtype=np.uint64) * 70016 + rng.integers(0, 8, size=n).astype(np.uint64)
     app_len = np.where(rng.random(n) < 0.1, ln.astype(np.int64) - 30, ln.astype(np.int64) + 3)
-    csum = oracle.desc_batch(host, offs, ln.astype(np.uint32), np.full(n, 0xFFFFFFFF, np.uint32), 0)
+    csum = oracle.desc_batch(host, offs, ln.astype(np.uint32), np.full(n, 0xFFFFFFFF, np.uint32) if mode == 0 else None,
+                             mode)
     none = app_len <= 0
-    csum = np.where(none, np.uint32(0xFFFFFFFF), csum).astype(np.uint32)
+    csum = np.where(none, np.uint32(0xFFFFFFFF if mode == 0 else 0), csum).astype(np.uint32)
     bad = (rng.random(n) < 0.05) & ~none
     expected = np.where(bad, csum ^ 0x00A4A400, csum).astype(np.uint32)
     descs = dv.make_recv_descs(frag, offs, app, aoffs, ln, app_len)
@@ -228,7 +232,7 @@ def test_learned_pairs_receive(cuda, oracle, odd):
     with torch.cuda.stream(stream):
         for i in range(20):
             app.zero_()
-            copied, got, mask, nbad = dv.copy_to_app_batch(descs, exp_t, mode=0, stream=stream)
+            copied, got, mask, nbad = dv.copy_to_app_batch(descs, exp_t, mode=mode, stream=stream)
             assert np.array_equal(dv.as_u32(got), csum), i
             assert np.array_equal(dv.mask_bits(mask, n), bad), i
             assert int(nbad.item()) == int(bad.sum()), i
