@@ -370,6 +370,23 @@ def shard_plan(args, world: int, rank: int):
     return n, L, seed, k0, kstep, n_global
 
 
+def _copy_schedule(crc: bool, src: str, L: int, rows_hint: int) -> str:
+    """The kernels a uniform batch of L-byte descriptor copies / receives runs once the stream's census
+    has landed (frag_csum.hip learned_rows_hint: kShapeRows 8 CRC / kShapeRowsSum 4 SUM, pairs at <= 2 KiB)."""
+    rows = max(1, -(-L // 4096))
+    W = rows_hint if rows_hint > 1 else (rows if rows >= (8 if crc else 4) else 1)
+    if crc:
+        if rows_hint <= 1 and L <= 2048:
+            return f"crc_light_pair_copy_kernel<{src}> (two fragments per wave) + crc_light_pair_leftover_kernel"
+        return (f"crc_light_frag_copy_kernel<{src}>" +
+                (f" ({W}-wave row groups + crc_light_group_join_kernel)" if W > 1 else ""))
+    if W > 1:
+        return f"sum_copy_wg_kernel<GroupSource<{src}>> ({W} row groups) + sum_group_join_kernel"
+    if rows_hint <= 1 and L <= 2048:
+        return f"sum_copy_waves_kernel<{src}> (one fragment per wave, four per workgroup)"
+    return f"sum_copy_wg_kernel<{src}> (one 128-thread workgroup per fragment)"
+
+
 def _traffic(key: str, field: str = "hbm_bytes_per_launch"):
     """A field of a committed PMC traffic entry (profiles/traffic.json), or None."""
     e = read_traffic(key)
@@ -520,9 +537,11 @@ def run_device(args):
                   "crc_stream_kernel<RowSegSource> (descriptors, 16-row segments)"
                   if args.desc and crc and args.rows_hint > 1 else
                   "crc_stream_kernel<RowSegSource, kSum> (descriptors, 16-row segments)"
-                  if args.desc and args.rows_hint > 16 else
-                  "crc_stream_kernel (descriptors)" if args.desc and crc else
-                  "crc_stream_kernel<kSum> (descriptors)" if args.desc else
+                  if args.desc and args.rows_hint > 1 else
+                  "learned schedule (DESIGN.md 4.2 census): crc_stream_kernel (descriptors) until a shape is "
+                  "learned, then the row-group schedule the census picks" if args.desc and crc else
+                  "learned schedule (DESIGN.md 4.2 census): crc_stream_kernel<kSum> (descriptors) until a shape "
+                  "is learned, then the row-segment schedule the census picks" if args.desc else
                   "crc_regular_kernel" if crc else "crc_regular_kernel (kSum: uicsum on the same schedule)")
         workload = (f"config D shard {args.shard} of 8: {n} x {L} B fragments k = {args.shard} (mod 8), seed 3"
                     if args.shard is not None else
@@ -1018,8 +1037,8 @@ def run_recv(args):
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}"),
                      "traffic_source": _traffic(f"{'crc' if mode == dv.CRC32 else 'sum'}_recv_{n}x{L}", "source"),
-                     "kernel": "crc_light_frag_copy_kernel<RecvSource>" if mode == dv.CRC32 else
-                               "sum_copy_wg_kernel<RecvSource> (one 128-thread workgroup per fragment)",
+                     "kernel": "zero_verdicts_kernel + " +
+                               _copy_schedule(mode == dv.CRC32, "RecvSource", L, args.rows_hint),
                      "kernel_avg_ms": round(kern * 1e3, 4), "algorithmic_bytes_per_launch": int(moved),
                      "note": "algorithmic bytes = payload read + payload written; the 4-byte expected value and "
                              "32-byte descriptor per fragment excluded"},
