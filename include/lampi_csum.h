@@ -403,8 +403,10 @@ typedef struct lampi_recv_desc {
  * for every i, whatever its descriptor says) --
  * e.g. dataChecksum (@64) of an array of 72-byte gmHeaderData records (expected_stride 72).
  * d_mask: bit (i % 32) of word i / 32 set iff fragment i is corrupt (zeroed by the call);
- * *d_nbad: number of corrupt fragments.  One wavefront per fragment (CRC) / 16-byte-piece
- * streams (SUM); every payload byte is read from HBM once. */
+ * *d_nbad: number of corrupt fragments.  The schedule follows the batch's shape (the rows hint
+ * above, or the shape the stream's earlier batches showed): one wavefront per fragment, row groups
+ * joined by a second launch, or two IB-sized fragments per wavefront (CRC) / one workgroup or one
+ * wavefront per fragment (SUM); every payload byte is read from HBM once. */
 int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void *d_expected,
                             size_t expected_stride, int64_t *d_copied, uint32_t *d_csum, uint32_t *d_mask,
                             uint32_t *d_nbad, int mode, void *stream);

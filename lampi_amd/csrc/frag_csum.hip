@@ -336,6 +336,18 @@ struct IsRecv : std::false_type {};
 template <>
 struct IsRecv<RecvSource> : std::true_type {};
 
+// The receive step's verdicts zeroed by the launch before the one that gives them (row groups: the first
+// launch, whose waves of group 0 zero the mask word of fragments f = 32i and f = 0 the count), instead of
+// a kernel of its own (zero_verdicts_kernel, ~5 us in the stream).
+__device__ __forceinline__ void zero_verdict_words(const RecvSource &src, size_t f) {
+    if ((f & 31u) == 0) src.mask[f >> 5] = 0u;
+    if (f == 0) *src.nbad = 0u;
+}
+template <class S>
+struct IsGroupRecv : std::false_type {};
+template <>
+struct IsGroupRecv<GroupSource<RecvSource>> : std::true_type {};
+
 // Byte-balanced descriptor batches (launch_crc_desc / launch_sum_desc for n <= kPlanMax): plan_kernel
 // cuts every fragment longer than the plan's window B into segments of at most B bytes and groups the
 // segments into workgroups by bytes, not by count.  A segment is checksummed like a fragment of its
@@ -2156,15 +2168,25 @@ constexpr uint32_t kLtBytes = kLtNib + kLightTables * kLtTab;
 // compile-time constants cost ~150 VALU per wave (gfx9 VALU takes no literal operands: every constant
 // needed a v_mov), about a fifth of the kernel's VALU, which bounds it (SQ counters,
 // profiles/r03/pmc_light_*)
+// (kT = 256 * m: thread t takes rows part * 8 / m .. of thread t % 256's eight, part = t / 256)
+template <int kT = 256>
 __device__ __forceinline__ void build_slices_light(char *b, const u32x4 bs[4]) {
-    const uint32_t t = threadIdx.x, r0 = t >> 3;
+    static_assert(kT == 256 || kT == 512 || kT == 1024, "256, 512 or 1024 threads");
+    constexpr int kRows = 8 * 256 / kT;
+    const uint32_t t = threadIdx.x, r0 = (t >> 3) & 31u, part = t >> 8;  // (part: wave-uniform)
     uint32_t base = 0;
 #pragma unroll
     for (int i = 0; i < 5; ++i) base ^= ((r0 >> i) & 1u) ? bs[i >> 2][i & 3] : 0u;
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-        const uint32_t v = base ^ bs[(5 + kk) >> 2][(5 + kk) & 3];
-        *reinterpret_cast<u32x4 *>(b + (r0 + 32 * kk) * 128 + (t & 7u) * 16) = u32x4{v, v, v, v};
+    for (int kk = 0; kk < kRows; ++kk) {
+        uint32_t v = bs[(5 + kk) >> 2][(5 + kk) & 3];
+#pragma unroll
+        for (int p = 1; p < 256 * 8 / (kRows * 256); ++p) {
+            const int i = 5 + p * kRows + kk;
+            v = part == (uint32_t)p ? bs[i >> 2][i & 3] : v;
+        }
+        v ^= base;
+        *reinterpret_cast<u32x4 *>(b + (r0 + 32 * (kk + kRows * part)) * 128 + (t & 7u) * 16) = u32x4{v, v, v, v};
     }
 }
 
@@ -2211,16 +2233,17 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t light_rsrc(const void *p, uint
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
 }
 
-__global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__restrict__ base, size_t msg_len,
-                                                             uint32_t frag_len, uint32_t R, size_t nitems,
-                                                             uint32_t partial, uint8_t *__restrict__ dst,
-                                                             size_t dst_stride, const uint32_t *__restrict__ img,
-                                                             uint32_t *__restrict__ out) {
+template <int kWv = 4>
+__global__ void __launch_bounds__(64 * kWv) crc_light_copy_kernel(const uint8_t *__restrict__ base, size_t msg_len,
+                                                                  uint32_t frag_len, uint32_t R, size_t nitems,
+                                                                  uint32_t partial, uint8_t *__restrict__ dst,
+                                                                  size_t dst_stride, const uint32_t *__restrict__ img,
+                                                                  uint32_t *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
     const uint32_t t = threadIdx.x, lane = t & 63u;
     // (fragment, row) of this wave, wave-uniform: the fragment's source and slot become buffer
     // descriptors in SGPRs
-    const size_t item = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6);
+    const size_t item = (size_t)blockIdx.x * kWv + __builtin_amdgcn_readfirstlane(t >> 6);
     const bool live = item < nitems;
     const size_t f = live ? item / R : 0;
     const uint32_t r = live ? (uint32_t)(item - f * R) : 0u;
@@ -2233,9 +2256,10 @@ __global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__re
     // piece again -- a load or store under a branch waits for itself before the row loads issue)
     constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
     static_assert(kNibPieces > 256 && kNibPieces <= 512, "two nibble-table pieces per thread at most");
-    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[min(t, kNibPieces - 1)];
     const uint32_t t2 = min(256u + t, kNibPieces - 1);
-    const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
+    u32x4 nib2 = nib;
+    if constexpr (kWv == 4) nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
     u32x4 bs[4];  // the slicing basis of table (t & 7) >> 1
 #pragma unroll
     for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
@@ -2254,9 +2278,10 @@ __global__ void __launch_bounds__(256) crc_light_copy_kernel(const uint8_t *__re
         d[q] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, o[q], 0, kBufNt);
     }
     // tables: slicing from the basis, then the uniform shifts, while the row loads fly
-    build_slices_light(reinterpret_cast<char *>(lds), bs);
-    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
-    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;  // (t >= 140: the last piece again)
+    build_slices_light<64 * kWv>(reinterpret_cast<char *>(lds), bs);
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[min(t, kNibPieces - 1)] = nib;
+    if constexpr (kWv == 4)
+        reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;  // (t >= 140: the last piece again)
     __syncthreads();
     if (!live) return;
     // the copy: every chunk of the fragment, 16-byte stores (dword-aligned slots run at the aligned rate)
@@ -2411,7 +2436,7 @@ struct LightFrag {
         const uint32_t k = W > 1 ? (R + W - 1) / W : R;
         r0 = W > 1 ? min(g * k, R) : 0u;
         r1 = W > 1 ? min(r0 + k, R) : R;
-        whole = r0 == 0u && r1 == R;  // the fragment's only group: emits its checksum
+        whole = W <= 1u;  // one wave per fragment: it emits the checksum (row groups: the join kernel, for all)
         if (W > 1 && g > 0u && r0 >= r1) live = false;
         srs = light_rsrc((const void *)fi.addr, L);
         drs = light_rsrc(fi.dst, fi.copylen);
@@ -2465,7 +2490,8 @@ __device__ __forceinline__ void inject_register(u32x4 (&dc)[4], uint32_t P, uint
 
 // The rest of one fragment (group) on its wave, after the tables are in LDS: its first row (d, o) and
 // head are already loaded.  Short fragments (under 16 bytes) run on lane 0.
-// A group of several (F.whole false) hands its value (normal domain) to sink.
+// In row groups (F.whole false) every group hands its value (normal domain) to sink, the fragment's only
+// group (and a short fragment's) too: the join kernel emits every fragment.
 template <class Src, class Sink>
 __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const LightFrag &F, const uint32_t *lds,
                                                uint32_t lane, uint32_t *out, Sink sink, u32x4 (&d)[4],
@@ -2476,7 +2502,10 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
         if (lane == 0) {
             uint32_t C = __builtin_bswap32(fi.partial);
             for (uint32_t i = 0; i < L; ++i) C = (C >> 8) ^ lds[((C ^ fi.addr[i]) & 255u) * 32u + 24u];
-            emit(src, out, f, __builtin_bswap32(C), fi);
+            if (F.whole)
+                emit(src, out, f, __builtin_bswap32(C), fi);
+            else
+                sink(__builtin_bswap32(C));
         }
         if constexpr (Src::kCopy)
             if (lane < fi.copylen) ((gbyte_w *)fi.dst)[lane] = fi.addr[lane];
@@ -2580,18 +2609,19 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
 }
 
 // One fragment (or row group) per wave: item = 4 * blockIdx.x + wave, four waves per workgroup.
-template <class Src>
-__global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src, size_t n,
-                                                                  const uint32_t *__restrict__ img,
-                                                                  uint32_t *__restrict__ out, uint32_t W,
-                                                                  uint32_t *__restrict__ groups) {
+template <class Src, int kWv = 4>
+__global__ void __launch_bounds__(64 * kWv) crc_light_frag_copy_kernel(const Src src, size_t n,
+                                                                       const uint32_t *__restrict__ img,
+                                                                       uint32_t *__restrict__ out, uint32_t W,
+                                                                       uint32_t *__restrict__ groups) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    const size_t item = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6);
+    const size_t item = (size_t)blockIdx.x * kWv + __builtin_amdgcn_readfirstlane(t >> 6);
     constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
-    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[min(t, kNibPieces - 1)];
     const uint32_t t2 = min(256u + t, kNibPieces - 1);
-    const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
+    u32x4 nib2 = nib;
+    if constexpr (kWv == 4) nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
     u32x4 bs[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
@@ -2601,6 +2631,8 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     if (f < n) fi = src.get(f);
     LightFrag F;
     F.init(fi, f < n && !(IsSplit<Src>::value && fi.aux), W, g);
+    if constexpr (IsRecv<Src>::value)  // row groups: the join kernel gives every verdict, this launch zeroes them
+        if (W > 1u && lane == 0u && f < n && g == 0u) zero_verdict_words(src, f);
     u32x4 d[4];
     uint32_t o[4];
     // the first row's loads before the table staging (after it: 4 KiB copies 73 -> 66%, profiles/r04/late_loads_ab.txt)
@@ -2608,9 +2640,9 @@ __global__ void __launch_bounds__(256) crc_light_frag_copy_kernel(const Src src,
     const u32x4 head = F.load_head();
     if constexpr (IsSplit<Src>::value)  // the size split's light launch: most workgroups hold no fragment of its
         if (!__syncthreads_or(F.live)) return;  // class and leave before staging the tables
-    build_slices_light(reinterpret_cast<char *>(lds), bs);
-    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
-    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
+    build_slices_light<64 * kWv>(reinterpret_cast<char *>(lds), bs);
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[min(t, kNibPieces - 1)] = nib;
+    if constexpr (kWv == 4) reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
     __syncthreads();
     if (!F.live) return;
     light_frag_run(src, f, F, lds, lane, out, [&](uint32_t v) { groups[f * W + g] = v; }, d, o, head);
@@ -2654,18 +2686,19 @@ __device__ __forceinline__ void light_pair_fallback(const Src src, size_t f0, si
     }
 }
 
-template <class Src>
-__global__ void __launch_bounds__(256) crc_light_pair_copy_kernel(const Src src, size_t n,
-                                                                  const uint32_t *__restrict__ img,
-                                                                  uint32_t *__restrict__ out, uint32_t *left,
-                                                                  uint32_t *__restrict__ list) {
+template <class Src, int kWv = 4>
+__global__ void __launch_bounds__(64 * kWv) crc_light_pair_copy_kernel(const Src src, size_t n,
+                                                                       const uint32_t *__restrict__ img,
+                                                                       uint32_t *__restrict__ out, uint32_t *left,
+                                                                       uint32_t *__restrict__ list) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLtBytes / 4];
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    const size_t wave = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(t >> 6), f0 = wave * 2;
+    const size_t wave = (size_t)blockIdx.x * kWv + __builtin_amdgcn_readfirstlane(t >> 6), f0 = wave * 2;
     constexpr uint32_t kNibPieces = kLightTables * kLightTableWords / 4;
-    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t];
+    const u32x4 nib = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[min(t, kNibPieces - 1)];
     const uint32_t t2 = min(256u + t, kNibPieces - 1);
-    const u32x4 nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
+    u32x4 nib2 = nib;
+    if constexpr (kWv == 4) nib2 = reinterpret_cast<const u32x4 *>(img + kImgLightNib)[t2];
     u32x4 bs[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) bs[i] = reinterpret_cast<const u32x4 *>(img + kImgSliceBasis)[((t & 7u) >> 1) * 4 + i];
@@ -2689,9 +2722,10 @@ __global__ void __launch_bounds__(256) crc_light_pair_copy_kernel(const Src src,
         d[q] = ld16c((gu32x4_a1 *)(live && x >= P ? addr + (x - P) : zero));
     }
     u32x4 head = ld16c((gu32x4_a1 *)(live ? addr : zero));
-    build_slices_light(reinterpret_cast<char *>(lds), bs);
-    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t] = nib;
-    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
+    build_slices_light<64 * kWv>(reinterpret_cast<char *>(lds), bs);
+    // (eight waves: one nibble-table piece per thread, the clamped rest storing the last piece again)
+    reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[min(t, kNibPieces - 1)] = nib;
+    if constexpr (kWv == 4) reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
     __syncthreads();
     if (!la) return;
     if (!pair) {  // left to crc_light_pair_leftover_kernel
@@ -2835,10 +2869,12 @@ __global__ void __launch_bounds__(256) crc_light_group_join_kernel(const Src src
     if (f >= n) return;  // (the G lanes of a fragment leave or stay together)
     const FragInfo fi = src.get(f);
     const uint32_t R = (uint32_t)(((uint64_t)fi.len + kRowBytes - 1) / kRowBytes);
-    if (fi.len < 16u || R <= 1u) return;  // (emitted by its only wave)
-    const uint32_t k = (R + W - 1) / W, ng = (R + k - 1) / k;
-    if (ng <= 1u) return;
     const uint32_t *p = groups + f * W;
+    if (fi.len < 16u || R <= 1u) {  // (one group: its value as it is)
+        if (j == 0) emit(src, out, f, p[0], fi);
+        return;
+    }
+    const uint32_t k = (R + W - 1) / W, ng = (R + k - 1) / k;
     uint32_t acc = 0;
     for (uint32_t g = j; g < ng; g += G) acc ^= shift_rows(p[g], R - min((g + 1u) * k, R));
     for (uint32_t o = G >> 1; o >= 1u; o >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, (int)o);
@@ -2853,12 +2889,24 @@ static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uin
     uint32_t *left = nullptr, *next_left = nullptr, *list = nullptr;
     hipError_t e = pair_counters(s, &left, &next_left);
     if (e != hipSuccess) return e;
-    const size_t nwg = (n + 7) / 8;
+    static const int kWv = [] {
+        const char *e = std::getenv("LAMPI_PAIR_WAVES");
+        return e && e[0] == '1' ? 16 : e && e[0] == '4' ? 4 : 8;
+    }();
+    const size_t nwg = (n + 2 * kWv - 1) / (2 * kWv);
     bool pooled = false;
-    e = stream_scratch(s, nwg * sizeof(uint32_t), (void **)&list, &pooled);
+    // (one entry per wave at most: a batch whose shape changed since the census leaves every wave)
+    e = stream_scratch(s, nwg * kWv * sizeof(uint32_t), (void **)&list, &pooled);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(crc_light_pair_copy_kernel<Src>, dim3((unsigned)nwg), dim3(256), 0, s, src, n, img, out, left,
-                       list);
+    if (kWv == 16)
+        hipLaunchKernelGGL((crc_light_pair_copy_kernel<Src, 16>), dim3((unsigned)nwg), dim3(1024), 0, s, src, n, img, out,
+                           left, list);
+    else if (kWv == 8)
+        hipLaunchKernelGGL((crc_light_pair_copy_kernel<Src, 8>), dim3((unsigned)nwg), dim3(512), 0, s, src, n, img, out,
+                           left, list);
+    else
+        hipLaunchKernelGGL((crc_light_pair_copy_kernel<Src, 4>), dim3((unsigned)nwg), dim3(256), 0, s, src, n, img, out,
+                           left, list);
     e = hipGetLastError();
     if (e == hipSuccess) {
         hipLaunchKernelGGL(crc_light_pair_leftover_kernel<Src>, dim3(kLeftoverWgs), dim3(256), 0, s, src, n, img, out,
@@ -2866,6 +2914,18 @@ static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uin
         e = hipGetLastError();
     }
     return scratch_done(s, list, pooled, e);
+}
+
+// waves per workgroup of the table-light copy kernels: four (the copy shape, four 36 KiB workgroups per CU);
+// the receive step eight -- the same LDS, twice the waves per CU (profiles/r04/light_waves_ab.txt: 4 KiB
+// receive 69.2 -> 71.8%, 1 MiB 71 -> 73%; the copies and the read-only walk lost 3-7 points).  A/B knob
+// LAMPI_LIGHT_WAVES = 4, 8, 16 for all of them.
+static int light_waves(bool recv = false) {
+    static const int w = [] {
+        const char *e = std::getenv("LAMPI_LIGHT_WAVES");
+        return e && e[0] == '1' ? 16 : e && e[0] == '8' ? 8 : e && e[0] == '4' ? 4 : 0;
+    }();
+    return w ? w : recv ? 8 : 4;
 }
 
 // W: row groups per fragment (1: one wave walks all the fragment's rows)
@@ -2880,17 +2940,28 @@ template <class Src>
 static hipError_t launch_crc_light_frag_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
                                              hipStream_t s, uint32_t W = 1) {
     W = light_groups(n, W);
+    const int kWv = light_waves(IsRecv<Src>::value);
+    auto launch = [&](size_t items, uint32_t *groups) {
+        if (kWv == 16)
+            hipLaunchKernelGGL((crc_light_frag_copy_kernel<Src, 16>), dim3((unsigned)((items + 15) / 16)), dim3(1024), 0,
+                               s, src, n, img, out, W, groups);
+        else if (kWv == 8)
+            hipLaunchKernelGGL((crc_light_frag_copy_kernel<Src, 8>), dim3((unsigned)((items + 7) / 8)), dim3(512), 0, s,
+                               src, n, img, out, W, groups);
+        else
+            hipLaunchKernelGGL((crc_light_frag_copy_kernel<Src, 4>), dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s,
+                               src, n, img, out, W, groups);
+    };
     if (W <= 1) {
-        hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, src, n,
-                           img, out, 1u, (uint32_t *)nullptr);
+        W = 1;
+        launch(n, nullptr);
         return hipGetLastError();
     }
     uint32_t *groups = nullptr;
     bool pooled = false;
     hipError_t e = stream_scratch(s, n * W * sizeof(uint32_t), (void **)&groups, &pooled);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(crc_light_frag_copy_kernel<Src>, dim3((unsigned)((n * W + 3) / 4)), dim3(256), 0, s, src, n, img,
-                       out, W, groups);
+    launch(n * W, groups);
     e = hipGetLastError();
     if (e == hipSuccess) {
         uint32_t G = 1;
@@ -3347,6 +3418,8 @@ __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint
     uint32_t it = 0;
     // a grid has at most 2^32 - 1 threads: beyond kMaxWgGrid fragments a workgroup takes several
     for (size_t f = blockIdx.x; f < n; f += gridDim.x, it ^= 1u) {
+        if constexpr (IsGroupRecv<Src>::value)  // (row groups of the receive step: the join gives the verdicts)
+            if (t == 0 && f % src.W == 0) zero_verdict_words(src.src, f / src.W);
         const FragInfo fi = src.get(f);
         uint32_t acc = wave_add(sum_copy_frag<kT, Src>(fi, t));
         if constexpr (kW == 1) {
@@ -4630,10 +4703,15 @@ static void launch_sum_copy(const Src &src, size_t n, uint32_t *out, hipStream_t
 }
 
 // With LAMPI_CSUM_ROWS_HINT (W > 1): each fragment as W row-group workgroups, their sums joined.
+static uint32_t sum_groups(size_t n, uint32_t W) {
+    while (W > 1 && (size_t)n * W > ((size_t)1 << 31)) W >>= 1;
+    return W;
+}
+
 template <class Src>
 static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out, hipStream_t s, uint32_t W,
                                          bool small = false) {
-    while (W > 1 && (size_t)n * W > ((size_t)1 << 31)) W >>= 1;
+    W = sum_groups(n, W);
     if (W <= 1) {
         launch_sum_copy(src, n, out, s, small);
         return hipGetLastError();
@@ -4684,12 +4762,16 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
     bool pairs = false;
     uint32_t *nhalf = nullptr;
     rows_hint = learned_rows_hint(src, n, s, 2, rows_hint, &pairs, &nhalf, crc ? kShapeRows : kShapeRowsSum);
-    // (not in the row groups' first launch: a fragment of one group gives its verdict there)
-    const size_t nwords = (n + 31) / 32;
-    hipLaunchKernelGGL(zero_verdicts_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, mask, nwords,
-                       nbad);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    // row groups: the first launch zeroes the verdicts (zero_verdict_words), the join gives them; otherwise
+    // the fragments' own waves give them, after this
+    const bool groups = crc ? !pairs && light_groups(n, rows_hint) > 1 : sum_groups(n, rows_hint) > 1;
+    if (!groups) {
+        const size_t nwords = (n + 31) / 32;
+        hipLaunchKernelGGL(zero_verdicts_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, mask, nwords,
+                           nbad);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     if (crc && pairs) return launch_crc_light_pair_copy(src, n, img, csum, s, nhalf);
     if (crc) return launch_crc_light_frag_copy(src, n, img, csum, s, rows_hint);
     return launch_sum_copy_groups(src, n, csum, s, rows_hint, pairs);  // (pairs: a wave per fragment)
@@ -4768,18 +4850,27 @@ static hipError_t launch_crc_light_copy(const uint8_t *base, size_t msg_len, siz
                                         hipStream_t s) {
     const uint32_t R = (uint32_t)((frag_len + kRowBytes - 1) / kRowBytes);
     const size_t items = n * R;
-    const dim3 grid((unsigned)((items + 3) / 4));
+    const int kWv = light_waves();
+    auto launch = [&](uint32_t *o) {
+        if (kWv == 16)
+            hipLaunchKernelGGL(crc_light_copy_kernel<16>, dim3((unsigned)((items + 15) / 16)), dim3(1024), 0, s, base,
+                               msg_len, (uint32_t)frag_len, R, items, partial, dst, dst_stride, img, o);
+        else if (kWv == 8)
+            hipLaunchKernelGGL(crc_light_copy_kernel<8>, dim3((unsigned)((items + 7) / 8)), dim3(512), 0, s, base,
+                               msg_len, (uint32_t)frag_len, R, items, partial, dst, dst_stride, img, o);
+        else
+            hipLaunchKernelGGL(crc_light_copy_kernel<4>, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, base,
+                               msg_len, (uint32_t)frag_len, R, items, partial, dst, dst_stride, img, o);
+    };
     if (R == 1) {
-        hipLaunchKernelGGL(crc_light_copy_kernel, grid, dim3(256), 0, s, base, msg_len, (uint32_t)frag_len, R, items,
-                           partial, dst, dst_stride, img, out);
+        launch(out);
         return hipGetLastError();
     }
     uint32_t *rows = nullptr;
     bool pooled = false;
     hipError_t e = stream_scratch(s, items * sizeof(uint32_t), (void **)&rows, &pooled);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(crc_light_copy_kernel, grid, dim3(256), 0, s, base, msg_len, (uint32_t)frag_len, R, items,
-                       partial, dst, dst_stride, img, rows);
+    launch(rows);
     e = hipGetLastError();
     if (e == hipSuccess) {
         const size_t per_wg = R <= kJoinThreadRows ? 256 : 4;  // fragments per workgroup

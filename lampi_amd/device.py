@@ -330,7 +330,10 @@ def copy_to_app_batch(descs: torch.Tensor, expected: torch.Tensor, expected_stri
     _records(expected.view(torch.uint8)[expected_offset:] if count else expected, count, expected_stride, "expected")
     copied = torch.empty(max(count, 1), dtype=torch.int64, device=descs.device)
     csum = torch.empty(max(count, 1), dtype=torch.int32, device=descs.device)
-    mask, nbad = _mask_out(count, descs.device)
+    # (the call zeroes the mask words and the count itself: no fill kernels here, except for an empty batch)
+    mask, nbad = (_mask_out(count, descs.device) if count == 0 else
+                  (torch.empty((count + 31) // 32, dtype=torch.int32, device=descs.device),
+                   torch.empty(1, dtype=torch.int32, device=descs.device)))
     check(lib().lampi_copy_to_app_batch(descs.data_ptr(), count, expected.data_ptr() + expected_offset, expected_stride,
                                         copied.data_ptr(), csum.data_ptr(), mask.data_ptr(), nbad.data_ptr(),
                                         mode | rows_hint_bits(rows_hint), _stream_handle(stream)),

@@ -238,3 +238,42 @@ def test_learned_pairs_receive(cuda, oracle, odd, mode):
             assert int(nbad.item()) == int(bad.sum()), i
             assert np.array_equal(copied.cpu().numpy(), want_copied), i
             assert torch.equal(app[good], want_app[good]), i
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_learned_pairs_shape_change(cuda, oracle, mode):
+    """IB-sized copies until the census picks pairs, then batches of larger fragments on the same stream
+    (the first of them still runs the pair schedule: every CRC wave leaves its fragments to the leftover
+    kernel -- the list holds one entry per wave), then IB again."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(121 + mode)
+    n = 601
+    shapes = {"ib": _ib_lengths(rng, n, False),
+              "big": rng.integers(2049, 70001, size=n).astype(np.uint64)}
+    src = torch.empty(n * 70016 + 64, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(src, seed=122)
+    host = src.cpu().numpy()
+    offs = np.arange(n, dtype=np.uint64) * 70016 + rng.integers(0, 16, size=n).astype(np.uint64)
+    dst = torch.empty(n * 70016 + 64, dtype=torch.uint8, device=cuda)
+    doffs = np.arange(n, dtype=np.uint64) * 70016 + rng.integers(0, 16, size=n).astype(np.uint64)
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    prepared = {}
+    for k, ln in shapes.items():
+        descs = dv.make_copy_descs(src, offs, dst, doffs, ln, ln, parts if mode == 0 else None)
+        want = oracle.desc_batch(host, offs, ln.astype(np.uint32), parts.astype(np.uint32) if mode == 0 else None,
+                                 mode)
+        want_dst = np.zeros(dst.numel(), np.uint8)
+        for i in range(n):
+            a, b, c = int(offs[i]), int(doffs[i]), int(ln[i])
+            want_dst[b:b + c] = host[a:a + c]
+        prepared[k] = (descs, want, torch.from_numpy(want_dst).to(cuda))
+    stream = torch.cuda.Stream(device=cuda)
+    with torch.cuda.stream(stream):
+        for i, k in enumerate(["ib"] * 20 + ["big"] * 4 + ["ib"] * 4):
+            descs, want, want_dst = prepared[k]
+            dst.zero_()
+            got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=mode, stream=stream))
+            assert np.array_equal(got, want), (i, k, int(np.count_nonzero(got != want)))
+            assert torch.equal(dst, want_dst), (i, k)

@@ -2,7 +2,7 @@
 fragments of L bytes, aligned or into destinations 8 bytes past a 16-byte boundary, and the receive
 step (lampi_copy_to_app_batch) from GM-style slots.  Prints the fraction of 8 TB/s (read + write)
 after a warm-up past the clocks' transient; checksums are compared with lampi_msg_csum.
-python tools/microbench/desc_copy_sizes.py [crc|sum]  (LAMPI_CSUM_LIB picks the library)"""
+python tools/microbench/desc_copy_sizes.py [crc|sum] [L,L,...]  (LAMPI_CSUM_LIB picks the library)"""
 import os
 import sys
 
@@ -31,7 +31,8 @@ MODE = dv.SUM32 if len(sys.argv) > 1 and sys.argv[1] == "sum" else dv.CRC32
 src = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
 dv.fill_stream(src, seed=31)
 dst = torch.zeros((1 << 30) + (1 << 24), dtype=torch.uint8, device="cuda")
-for L in (1976, 4096, 16384, 65456, 1 << 20):
+SIZES = tuple(int(x) for x in sys.argv[2].split(",")) if len(sys.argv) > 2 else (1976, 4096, 16384, 65456, 1 << 20)
+for L in SIZES:
     n = (1 << 30) // (L + 80)
     offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
     want = dv.msg_csum(src[:n * L], L, mode=MODE)
