@@ -51,6 +51,13 @@ for step in "$@"; do
             -o run -- python3 bench.py --bcopy --steps 5 --warmup 3 &&
          run pmcbcopy_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcbcopy_write \
             -o run -- python3 bench.py --bcopy --steps 5 --warmup 3 ;;
+    pmclds) for cfg in B C R; do  # LDS array cycles and bank conflicts, stall split (R: GM receive, learned row groups)
+             args="--no-cpu-baseline"; [ $cfg = C ] && args="--config C"
+             [ $cfg = R ] && args="--recv --frags 16384 --frag-bytes 65456 --warmup 40"
+             run pmc_lds$cfg 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_ANY \
+                 SQ_WAIT_INST_ANY SQ_WAVE_CYCLES --output-format csv \
+                 -d gpurun_out/pmc_lds$cfg -o run -- python3 bench.py --steps 3 $args
+           done ;;
     pmcsq) for cfg in B C D; do
              extra="--no-cpu-baseline"; [ $cfg = C ] && extra="--config C"; [ $cfg = D ] && extra="--desc --no-cpu-baseline"
              run pmc_sq$cfg 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU \
