@@ -389,12 +389,9 @@ def _copy_schedule(crc: bool, src: str, L: int, rows_hint: int) -> str:
 
 def _recv_schedule(crc: bool, L: int, rows_hint: int) -> str:
     """The receive step's kernels: row groups zero the verdicts in their first launch, the other schedules
-    after zero_verdicts_kernel (frag_csum.hip launch_copy_to_app); the CRC light kernels in 8-wave workgroups."""
+    after zero_verdicts_kernel (frag_csum.hip launch_copy_to_app)."""
     k = _copy_schedule(crc, "RecvSource", L, rows_hint)
-    grouped = "row groups" in k
-    if crc and "frag_copy" in k:
-        k += ", 8-wave workgroups"
-    return k if grouped else "zero_verdicts_kernel + " + k
+    return k if "row groups" in k else "zero_verdicts_kernel + " + k
 
 
 def _traffic(key: str, field: str = "hbm_bytes_per_launch"):

@@ -2391,6 +2391,11 @@ template <bool B>
 struct BoolC {
     static constexpr bool value = B;
 };
+enum { kStepWalk, kStepHalf, kStepLast };
+template <int M>
+struct StepC {
+    static constexpr int value = M;
+};
 
 // Bytes 0..nb-1 of v (nb <= 16, wave-uniform) to offsets ob.. of a buffer descriptor, on the lanes with
 // `on` (the others aimed out of range): whole words as dword stores, then a short and a byte -- byte stores
@@ -2525,9 +2530,11 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
     if constexpr (Src::kCopy)
         if (r0 == 0 && sP != 0) store_bytes(head, F.drs, lane == (kP & 63u), 0u, min(16u - sP, fi.copylen));
     // (hf: BoolC<true> for a half frame -- its own copy of the body, kept out of the row loop)
-    auto step = [&](auto hf, uint32_t r, u32x4 (&dc)[4], const uint32_t (&oc)[4], u32x4 (&dn)[4],
+    // (mode: kStepWalk a row with the next row's loads in flight, kStepHalf a half frame, kStepLast a group's only
+    // row -- no prefetch: its four loads aimed out of range still took address-pipeline slots)
+    auto step = [&](auto mode, uint32_t r, u32x4 (&dc)[4], const uint32_t (&oc)[4], u32x4 (&dn)[4],
                     uint32_t (&on)[4]) {
-        if constexpr (!decltype(hf)::value) F.load_row(lane, r + 1, r + 1 < r1, dn, on);  // (a half frame: one row)
+        if constexpr (decltype(mode)::value == kStepWalk) F.load_row(lane, r + 1, r + 1 < r1, dn, on);
         if (r == 0 && sP != 0) {  // the chunk cut by the fragment's start: [zeros | first 16 - sP bytes]
             const u32x4 v = shl_bytes16(head, sP);
             const bool mine = lane == (kP & 63u);
@@ -2569,7 +2576,7 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
             inject_register(dc, P, fi.partial, [&](int q) { return 256u * r + lane + 64u * q; });
         const uint32_t c0 = light_chunk(lds, lanec2, sel, dc[0]);
         const uint32_t c1 = light_chunk(lds, lanec2, sel, dc[1]);
-        if constexpr (decltype(hf)::value) {  // (one row: r == r0 == 0; chunks 2, 3 lie past the frame)
+        if constexpr (decltype(mode)::value == kStepHalf) {  // (one row: r == r0 == 0; chunks 2, 3 lie past the frame)
             acc = light_shift<0>(lds, c0) ^ c1;
         } else {
             const uint32_t c2 = light_chunk(lds, lanec2, sel, dc[2]);
@@ -2598,13 +2605,17 @@ __device__ __forceinline__ void light_frag_run(const Src &src, size_t f, const L
     u32x4 d2[4];
     uint32_t o2[4];
     if (F.half) {
-        step(BoolC<true>{}, 0u, d, o, d2, o2);
+        step(StepC<kStepHalf>{}, 0u, d, o, d2, o2);
+        return;
+    }
+    if (r1 - r0 == 1u) {  // a 4 KiB fragment, or a row group of one row (GM's row groups)
+        step(StepC<kStepLast>{}, r0, d, o, d2, o2);
         return;
     }
     for (uint32_t r = r0; r < r1; r += 2) {
-        step(BoolC<false>{}, r, d, o, d2, o2);
+        step(StepC<kStepWalk>{}, r, d, o, d2, o2);
         if (r + 1 >= r1) break;
-        step(BoolC<false>{}, r + 1, d2, o2, d, o);
+        step(StepC<kStepWalk>{}, r + 1, d2, o2, d, o);
     }
 }
 
@@ -2916,16 +2927,18 @@ static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uin
     return scratch_done(s, list, pooled, e);
 }
 
-// waves per workgroup of the table-light copy kernels: four (the copy shape, four 36 KiB workgroups per CU);
-// the receive step eight -- the same LDS, twice the waves per CU (profiles/r04/light_waves_ab.txt: 4 KiB
-// receive 69.2 -> 71.8%, 1 MiB 71 -> 73%; the copies and the read-only walk lost 3-7 points).  A/B knob
-// LAMPI_LIGHT_WAVES = 4, 8, 16 for all of them.
+// waves per workgroup of the table-light copy kernels: four (the copy shape, four 36 KiB workgroups per CU).
+// Eight (the same LDS, twice the waves per CU) lost 3-7 points on the copies and the read-only walk and was
+// box-dependent on the receive step (profiles/r04/light_waves_ab.txt, recv_waves_ab.txt); with the
+// single-row step (95 VGPRs) it lost there too: GM receive 72.2 against 69.0% (profiles/r04/last_row_ab.txt).
+// A/B knob LAMPI_LIGHT_WAVES = 4, 8, 16.
 static int light_waves(bool recv = false) {
+    (void)recv;
     static const int w = [] {
         const char *e = std::getenv("LAMPI_LIGHT_WAVES");
-        return e && e[0] == '1' ? 16 : e && e[0] == '8' ? 8 : e && e[0] == '4' ? 4 : 0;
+        return e && e[0] == '1' ? 16 : e && e[0] == '8' ? 8 : 4;
     }();
-    return w ? w : recv ? 8 : 4;
+    return w;
 }
 
 // W: row groups per fragment (1: one wave walks all the fragment's rows)
