@@ -394,6 +394,23 @@ def _recv_schedule(crc: bool, L: int, rows_hint: int) -> str:
     return k if "row groups" in k else "zero_verdicts_kernel + " + k
 
 
+def _warm(fn, warmup: int, min_s: float = 0.5):
+    """W untimed calls, then more until min_s has passed (as the config B / C warm-ups: the clocks of a fresh
+    process ramp, and a copy shape dips for ~20 dispatches before it settles); returns the
+    last call's result."""
+    import torch
+
+    t = time.perf_counter()
+    res, i = None, 0
+    while i < warmup or time.perf_counter() - t < min_s:
+        res = fn()
+        i += 1
+        if i % 50 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    return res
+
+
 def _traffic(key: str, field: str = "hbm_bytes_per_launch"):
     """A field of a committed PMC traffic entry (profiles/traffic.json), or None."""
     e = read_traffic(key)
@@ -869,9 +886,7 @@ def run_bcopy(args):
     stream = torch.cuda.current_stream()
 
     def timed(fn):
-        for _ in range(args.warmup):
-            fn()
-        torch.cuda.synchronize()
+        _warm(fn, args.warmup)
         # (events at the ends of the K back-to-back calls: an event between two calls is a stream packet of
         # its own, ~6 us, which no application sends)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -1008,9 +1023,7 @@ def run_recv(args):
                                np.full(n, L), np.full(n, 1 << 40, dtype=np.int64))
     run = lambda: dv.copy_to_app_batch(descs, nic, expected_stride=stride, expected_offset=64, n=n, mode=mode,  # noqa
                                        rows_hint=args.rows_hint)
-    for _ in range(args.warmup):
-        res = run()
-    torch.cuda.synchronize()
+    res = _warm(run, args.warmup)
     stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
