@@ -3406,10 +3406,12 @@ __device__ __forceinline__ uint32_t sum_copy_frag(const FragInfo &fi, uint32_t t
         const uint32_t c = kT * r + t;
         u32x4 nv = {0u, 0u, 0u, 0u};
         if (c + kT < nfull) nv = ld16u((gu32x4_a1 *)(p + 16u * (c + kT)));
-        if (c < cfull)
-            st16u((gwu32x4_a1 *)(q + 16u * c), v);
-        else if (c == cfull)
-            vc = v;
+        if constexpr (Src::kCopy) {
+            if (c < cfull)
+                st16u((gwu32x4_a1 *)(q + 16u * c), v);
+            else if (c == cfull)
+                vc = v;
+        }
         acc += v.x + v.y + v.z + v.w;
         v = nv;
     }
@@ -3418,13 +3420,14 @@ __device__ __forceinline__ uint32_t sum_copy_frag(const FragInfo &fi, uint32_t t
         acc += w.x + w.y + w.z + w.w;
         if (cfull == nfull) vc = w;
     }
-    if ((clen & 15u) && t == cfull % kT) store_head16(q + 16u * cfull, vc, clen & 15u);
+    if constexpr (Src::kCopy)
+        if ((clen & 15u) && t == cfull % kT) store_head16(q + 16u * cfull, vc, clen & 15u);
     return acc;
 }
 
 template <class Src, int kT = kSumWgThreads>
 __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
-    static_assert(Src::kCopy && !Src::kPhase, "word-grid copy sources only");
+    static_assert(!Src::kPhase, "word-grid sources only (read-only ones: row groups of read-only SUM batches)");
     constexpr uint32_t kW = kT / 64;
     __shared__ uint32_t part[2][kW];  // by iteration parity: one barrier per fragment
     const uint32_t t = threadIdx.x;
@@ -3455,7 +3458,7 @@ __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint
 // workgroups per GiB).  Exact for any length.
 template <class Src>
 __global__ void __launch_bounds__(256) sum_copy_waves_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
-    static_assert(Src::kCopy && !Src::kPhase, "word-grid copy sources only");
+    static_assert(!Src::kPhase, "word-grid sources only");
     const uint32_t lane = threadIdx.x & 63u;
     for (size_t f = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); f < n;
          f += (size_t)gridDim.x * 4) {
@@ -4814,6 +4817,15 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     if (n == 0) return hipSuccess;
     if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
     if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint);
+    static const bool ro_groups = [] {  // (A/B knob)
+        const char *e = std::getenv("LAMPI_SUM_RO_GROUPS");
+        return !(e && e[0] == '0');
+    }();
+    // row groups of up to 8 rows: one short-lived workgroup per group (profiles/r04/sum_ro_groups_ab.txt: 16 KiB
+    // with hint 4 73.7 -> 75.6%, 32 KiB learned 73.3 -> 76.1%; GM's 16 groups lost, 74 -> 71.6%, and keep the
+    // row segments, as longer fragments do)
+    if (img && ro_groups && rows_hint <= 8 && sum_groups(n, rows_hint) > 1)
+        return launch_sum_copy_groups(DescSource{d}, n, out, s, rows_hint);
     if (img && rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<true, kSumWv, kSumCap>(d, n, out, img, s, rows_hint);
     if (img) {  // piece streams (img: the zero chunk)
