@@ -4821,11 +4821,17 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         const char *e = std::getenv("LAMPI_SUM_RO_GROUPS");
         return !(e && e[0] == '0');
     }();
-    // row groups of up to 8 rows: one short-lived workgroup per group (profiles/r04/sum_ro_groups_ab.txt: 16 KiB
-    // with hint 4 73.7 -> 75.6%, 32 KiB learned 73.3 -> 76.1%; GM's 16 groups lost, 74 -> 71.6%, and keep the
-    // row segments, as longer fragments do)
-    if (img && ro_groups && rows_hint <= 8 && sum_groups(n, rows_hint) > 1)
-        return launch_sum_copy_groups(DescSource{d}, n, out, s, rows_hint);
+    // row groups on short-lived workgroups, at most eight per fragment (profiles/r04/sum_ro_groups_ab.txt: 16 KiB
+    // with hint 4 73.7 -> 75.6%, 32 KiB learned 73.3 -> 76.1%; sum_group_cap_ab.txt: GM's 65,456-byte fragments
+    // as eight groups of two rows 74 -> 86.4%, as sixteen of one 71.6%, four of four 84.2%; 1 MiB as eight of
+    // 32 rows 69.6 -> 73%, sum_ro_groups2.txt); fragments over 256 rows keep the row segments (A/B knob
+    // LAMPI_SUM_RO_MAXROWS)
+    static const uint32_t ro_max = [] {
+        const char *e = std::getenv("LAMPI_SUM_RO_MAXROWS");
+        return e ? (uint32_t)std::atoi(e) : 256u;
+    }();
+    if (img && ro_groups && rows_hint > 1 && rows_hint <= ro_max && sum_groups(n, min(rows_hint, 8u)) > 1)
+        return launch_sum_copy_groups(DescSource{d}, n, out, s, min(rows_hint, 8u));
     if (img && rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<true, kSumWv, kSumCap>(d, n, out, img, s, rows_hint);
     if (img) {  // piece streams (img: the zero chunk)
