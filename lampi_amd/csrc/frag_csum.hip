@@ -4440,8 +4440,9 @@ static bool shapes_enabled() {
 template <class Src>
 static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int kind, uint32_t rows_hint,
                                   bool *pairs = nullptr, uint32_t **nhalf_dev = nullptr,
-                                  uint32_t min_rows = kShapeRows) {
+                                  uint32_t min_rows = kShapeRows, bool *one_row = nullptr) {
     if (pairs) *pairs = false;
+    if (one_row) *one_row = false;
     if (rows_hint > 1 || n < kShapeMin || !shapes_enabled()) return rows_hint;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return rows_hint;
@@ -4467,6 +4468,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     std::atomic_thread_fence(std::memory_order_acquire);
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= min_rows && rmax <= 2 * rmin) W = rmax;
+        if (one_row && rmin == 1u && rmax == 1u) *one_row = true;  // every sampled fragment one row (17 B-4 KiB)
         if (pairs && nhalf == sampled) {  // every sampled fragment at most 2 KiB: two per wave
             void *dp = nullptr;
             if (nhalf_dev && hipHostGetDevicePointer(&dp, rec, 0) == hipSuccess) {
@@ -4816,7 +4818,8 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
-    if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint);
+    bool one_row = false;
+    if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, kShapeRows, &one_row);
     static const bool ro_groups = [] {  // (A/B knob)
         const char *e = std::getenv("LAMPI_SUM_RO_GROUPS");
         return !(e && e[0] == '0');
@@ -4834,6 +4837,20 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         return launch_sum_copy_groups(DescSource{d}, n, out, s, min(rows_hint, 8u));
     if (img && rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<true, kSumWv, kSumCap>(d, n, out, img, s, rows_hint);
+    // batches of one-row fragments (the census: every sampled fragment 1-4096 bytes) on short-lived 128-thread
+    // workgroups of two fragments each (profiles/r04/sum_ro_wg_ab.txt: 4 KiB descriptors 79.6 -> 86.3%; one per
+    // workgroup 83.2%, four 82.7%; config C's mixed sizes lost 0.5 on it and keep the piece streams).  A/B knob
+    // LAMPI_SUM_RO_WG = fragments per workgroup (0: off).
+    static const uint32_t ro_wg = [] {
+        const char *e = std::getenv("LAMPI_SUM_RO_WG");
+        return e ? (uint32_t)std::atoi(e) : 2u;
+    }();
+    if (img && ro_wg && one_row && rows_hint <= 1) {
+        hipLaunchKernelGGL(sum_copy_wg_kernel<DescSource>,
+                           dim3((unsigned)std::min<size_t>((n + ro_wg - 1) / ro_wg, kMaxWgGrid)), dim3(kSumWgThreads), 0,
+                           s, DescSource{d}, n, out);
+        return hipGetLastError();
+    }
     if (img) {  // piece streams (img: the zero chunk)
         const uint32_t fpg = sum_frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, true, kSumWv, kSumCap>),
