@@ -165,8 +165,11 @@ def test_restatement_vs_reference_fuzz(oracle, reference):
 def test_cpu_baseline_speed_matches_reference(oracle, reference):
     """The restatement is the same byte-serial algorithm: per-core speed within +-20%."""
     buf = oracle.stream(1, 0, 16 << 20)
-    tp = min(oracle.time_crc_fn(oracle.uicrc_addr(), buf, 16384, 1024, 1)[0] for _ in range(3))
-    tr = min(oracle.time_crc_fn(reference.uicrc_addr(), buf, 16384, 1024, 1)[0] for _ in range(3))
+    # (interleaved, best of seven each: a loaded machine -- pytest -n -- slows both alike)
+    tp, tr = float("inf"), float("inf")
+    for _ in range(7):
+        tp = min(tp, oracle.time_crc_fn(oracle.uicrc_addr(), buf, 16384, 1024, 1)[0])
+        tr = min(tr, oracle.time_crc_fn(reference.uicrc_addr(), buf, 16384, 1024, 1)[0])
     assert 0.8 < tp / tr < 1.25, (tp, tr)
 
 
