@@ -57,6 +57,7 @@ namespace lampi {
 static hipError_t stream_scratch(hipStream_t s, size_t bytes, void **out, bool *pooled);
 static hipError_t scratch_done(hipStream_t s, void *p, bool pooled, hipError_t e);
 static hipError_t pair_counters(hipStream_t s, uint32_t **cur, uint32_t **next);
+static void reset_pair_counters(hipStream_t s);
 static hipError_t scratch_done(hipStream_t s, void *p, bool pooled, hipError_t e);
 
 namespace {
@@ -1468,7 +1469,19 @@ struct RowsN4 {
 // kK chains per wave (1: 512-thread workgroups, 2: 256-thread); kChains = 8 either way.
 // (Round 1 also ran the SUM fused copy on 16-byte-piece streams here; round 2 moved it to
 // sum_rows_kernel, which measured faster on every layout: launch_sum_copy.)
-template <bool kMis, int kD, int kK, bool kSum>
+// Timeline diagnostic (tools/microbench/stream_timeline.py, profiles/r05/configC_ab.txt; never a product
+// path): per workgroup, 16 words of s_memrealtime stamps -- [0] entry, [7] descriptors and tables in, [8] prefix
+// scan done, [1] chains set up, [9] first rows arrived, [2] first row checksummed, [3] rows done, [4] exit --
+// and [5] HW_ID, [6] XCC_ID.
+__device__ uint64_t *g_stream_diag = nullptr;
+#define LAMPI_DIAG_STAMP(K)                                                                            \
+    do {                                                                                               \
+        if constexpr (kDiag) {                                                                         \
+            if (threadIdx.x == 0) g_stream_diag[(size_t)blockIdx.x * 16 + (K)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                              \
+    } while (0)
+
+template <bool kMis, int kD, int kK, bool kSum, bool kDiag = false>
 __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDesc *sdesc, const uint64_t *sstart,
                                             const uint16_t *sj, uint32_t *marks, const StreamChain *sch,
                                             uint32_t *sopen, uint32_t *shead, gbyte *zero, uint32_t *sres,
@@ -1795,8 +1808,10 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 #define LAMPI_STREAM_STEP(S)                                                                  \
     if constexpr ((S) < kD) {                                                                 \
         wait_slot(ring[S], std::integral_constant<int, (S)>{});                               \
+        if (step == 0u) LAMPI_DIAG_STAMP(9);                                                  \
         if (step == nsteps) break;                                                            \
         process(ring[S], tk[S]);                                                              \
+        if (step == 0u) LAMPI_DIAG_STAMP(2);                                                  \
         ++step;                                                                               \
         {                                                                                     \
             AddrN<NL> A[kK];                                                                  \
@@ -1827,7 +1842,8 @@ __device__ __forceinline__ void stream_body(const uint32_t *lds, const StreamDes
 // compiler for that many waves per SIMD.  (Round 1's ablated variants -- loads and task walk
 // only, no piece lookups -- ran as a template switch here until commit d95cfff:
 // profiles/r01_stream_ablation.txt.)
-template <class Src, int kD = 3, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0>
+template <class Src, int kD = 3, int kK = 2, bool kSum = false, int kWv = 8 / kK, int kWaveCap = 0,
+          bool kDiag = false>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kWaveCap > 0 ? kWaveCap : 1)))
 crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ img, uint32_t *__restrict__ out,
                   const uint32_t *__restrict__ plan) {
@@ -1848,6 +1864,13 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     __shared__ uint64_t wpieces[kWv];
     __shared__ uint32_t wcount[kWv];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, t = threadIdx.x;
+    LAMPI_DIAG_STAMP(0);
+    if constexpr (kDiag) {
+        if (t == 0) {
+            g_stream_diag[(size_t)blockIdx.x * 16 + 5] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (31 << 11));
+            g_stream_diag[(size_t)blockIdx.x * 16 + 6] = (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (31 << 11));
+        }
+    }
     size_t base = (size_t)blockIdx.x * fpg;
     uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
     if constexpr (IsSeg<Src>::value) {  // the plan's workgroups: plan[0] of them, segments [plan[1+i], plan[2+i])
@@ -1878,6 +1901,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
         }
         __syncthreads();
     }
+    LAMPI_DIAG_STAMP(7);
     const bool ne = t < nwg && mine.len != 0u;              // list entries: the non-empty fragments
     if (t < nwg && mine.len == 0u) sres[t] = kSum ? 0u : mine.partial;  // uicrc(p, 0, s) == s, uicsum(p, 0) == 0
     const uint64_t np = ne ? (((uint64_t)mine.len + (kPB - 1)) / kPB) : 0ull;
@@ -1928,6 +1952,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     }
     if (t == 0) sstart[nne] = total;
     __syncthreads();
+    LAMPI_DIAG_STAMP(8);
     if (t < kChains) {
         StreamChain ch;
         ch.rs = 64u * ((t * R) / kChains);
@@ -1947,13 +1972,15 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     for (uint32_t i = t; i < kChains * 64; i += kThreads) marks[i] = 0u;
     const bool anymis = __syncthreads_or(mis) != 0;
     gbyte *zero = (gbyte *)(img + kImgZero);
+    LAMPI_DIAG_STAMP(1);
     if (anymis)  // five loads per row: a one-slot ring keeps its registers within the aligned variant's
-        stream_body<true, 1, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+        stream_body<true, 1, kK, kSum, kDiag>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                              sopen + kK * wave, shead + kK * wave, zero, sres, out);
     else
-        stream_body<false, kD, kK, kSum>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
+        stream_body<false, kD, kK, kSum, kDiag>(lds, sdesc, sstart, sj, marks + 64 * kK * wave, schain + kK * wave,
                                                sopen + kK * wave, shead + kK * wave, zero, sres, out);
     __syncthreads();
+    LAMPI_DIAG_STAMP(3);
     // stream_join: fragments crossing chain starts, every chain's part at once.  A fragment f
     // crossing chains a (where it starts) .. b (where it ends) is the XOR (SUM: sum) of each
     // chain's part shifted past the rest of f: chains a..b-1 leave their open value (sopen),
@@ -2007,6 +2034,7 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
     } else {
         emit(src, out, base + t, sres[t], mine);
     }
+    LAMPI_DIAG_STAMP(4);
 }
 
 // The byte-balanced plan of a descriptor batch (n <= kPlanMax fragments, one 1024-thread workgroup):
@@ -2898,8 +2926,6 @@ template <class Src>
 static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uint32_t *img, uint32_t *out,
                                              hipStream_t s, uint32_t *shape_nhalf) {
     uint32_t *left = nullptr, *next_left = nullptr, *list = nullptr;
-    hipError_t e = pair_counters(s, &left, &next_left);
-    if (e != hipSuccess) return e;
     static const int kWv = [] {
         const char *e = std::getenv("LAMPI_PAIR_WAVES");
         return e && e[0] == '1' ? 16 : e && e[0] == '4' ? 4 : 8;
@@ -2907,8 +2933,11 @@ static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uin
     const size_t nwg = (n + 2 * kWv - 1) / (2 * kWv);
     bool pooled = false;
     // (one entry per wave at most: a batch whose shape changed since the census leaves every wave)
-    e = stream_scratch(s, nwg * kWv * sizeof(uint32_t), (void **)&list, &pooled);
+    hipError_t e = stream_scratch(s, nwg * kWv * sizeof(uint32_t), (void **)&list, &pooled);
     if (e != hipSuccess) return e;
+    // the counter pair is taken only now: a failure before this point leaves it untouched
+    e = pair_counters(s, &left, &next_left);
+    if (e != hipSuccess) return scratch_done(s, list, pooled, e);
     if (kWv == 16)
         hipLaunchKernelGGL((crc_light_pair_copy_kernel<Src, 16>), dim3((unsigned)nwg), dim3(1024), 0, s, src, n, img, out,
                            left, list);
@@ -2924,6 +2953,8 @@ static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uin
                            (const uint32_t *)left, next_left, (const uint32_t *)list, shape_nhalf);
         e = hipGetLastError();
     }
+    // a launch that failed left a counter unzeroed (the leftover kernel zeroes the next call's): zero both
+    if (e != hipSuccess) reset_pair_counters(s);
     return scratch_done(s, list, pooled, e);
 }
 
@@ -4268,12 +4299,13 @@ struct ScratchTable {
         uint32_t calls[kShapeKinds] = {};
         uint32_t *left = nullptr;  // the pair kernel's two leftover counters (device, zeroed at creation)
         uint32_t left_calls = 0;
+        bool pair_broken = false;  // the counters could not be re-zeroed after a failed launch
     };
     std::map<std::pair<int, hipStream_t>, Slot> slots;
     ScratchTable() = default;
     ScratchTable(const ScratchTable &) = delete;
     ScratchTable &operator=(const ScratchTable &) = delete;
-    ~ScratchTable() { release_if([](const std::pair<int, hipStream_t> &) { return true; }); }
+    ~ScratchTable();
 
     // Free the slots whose key satisfies pred, each on its own device after its stream drained;
     // errors are ignored (this also runs at thread exit).
@@ -4307,6 +4339,15 @@ struct ScratchTable {
     }
 };
 thread_local ScratchTable t_scratch;
+// Set once this thread's t_scratch has been destroyed.  Thread-local objects are destroyed in
+// reverse order of construction, so the host pipeline's (host_msg.cc, t_pipe) may run after this one and
+// call release_stream_scratch(): that must not touch the destroyed map.  A trivially destructible
+// thread_local stays readable until the thread ends.
+thread_local bool t_scratch_dead = false;
+ScratchTable::~ScratchTable() {
+    release_if([](const std::pair<int, hipStream_t> &) { return true; });
+    t_scratch_dead = true;
+}
 }  // namespace
 
 static hipError_t stream_scratch(hipStream_t s, size_t bytes, void **out, bool *pooled) {
@@ -4359,17 +4400,33 @@ static hipError_t pair_counters(hipStream_t s, uint32_t **cur, uint32_t **next) 
         slot.left = (uint32_t *)p;
         g_scratch_bytes.fetch_add(kLeftBytes, std::memory_order_relaxed);
     }
+    if (slot.pair_broken) return hipErrorNotReady;  // (learned_rows_hint no longer picks pairs here)
     const uint32_t par = slot.left_calls++ & 1u;
     *cur = slot.left + par;
     *next = slot.left + (par ^ 1u);
     return hipSuccess;
 }
 
+// After a failed pair launch: both counters back to zero on the stream (a failing memset too: the pair
+// schedule is then retired for this stream, since a stale count could index past the leftover list).
+static void reset_pair_counters(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    auto it = t_scratch.slots.find({dev, s});
+    if (it == t_scratch.slots.end() || !it->second.left) return;
+    if (hipMemsetAsync(it->second.left, 0, 2 * sizeof(uint32_t), s) != hipSuccess) {
+        (void)hipGetLastError();
+        it->second.pair_broken = true;
+    }
+}
+
 void release_stream_scratch(hipStream_t s) {
+    if (t_scratch_dead) return;  // everything was released when the table went
     t_scratch.release_if([s](const std::pair<int, hipStream_t> &k) { return k.second == s; });
 }
 
 void release_thread_scratch() {
+    if (t_scratch_dead) return;
     t_scratch.release_if([](const std::pair<int, hipStream_t> &) { return true; });
 }
 
@@ -4469,7 +4526,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= min_rows && rmax <= 2 * rmin) W = rmax;
         if (one_row && rmin == 1u && rmax == 1u) *one_row = true;  // every sampled fragment one row (17 B-4 KiB)
-        if (pairs && nhalf == sampled) {  // every sampled fragment at most 2 KiB: two per wave
+        if (pairs && nhalf == sampled && !slot.pair_broken) {  // every sampled fragment at most 2 KiB: two per wave
             void *dp = nullptr;
             if (nhalf_dev && hipHostGetDevicePointer(&dp, rec, 0) == hipSuccess) {
                 *pairs = true;
@@ -4586,6 +4643,22 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     const uint32_t fpg = frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
                        frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
+    return hipGetLastError();
+}
+
+// Timeline diagnostic of the read-only CRC piece streams (tools/microbench/stream_timeline.py): the
+// product's grid and schedule, the kDiag instantiation stamping 16 words per workgroup into `stamps`
+// (>= 16 * workgroups words); returns the workgroup count in *nwg.  Not on any product path.
+hipError_t diag_stream_timeline(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
+                                uint64_t *stamps, hipStream_t s, uint32_t *nwg) {
+    const uint32_t fpg = frags_per_wg(n);
+    const dim3 wgs = frags_grid(n, fpg);
+    *nwg = wgs.x;
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_stream_diag), &stamps, sizeof(stamps), 0,
+                                          hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap, true>), wgs,
+                       dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
     return hipGetLastError();
 }
 

@@ -58,10 +58,13 @@ struct PlanItem {
 struct PlanRules {
     bool ring = false;
     size_t ring_bytes = 0;
+    size_t pad_in() const;  // chunk bytes the planner charges per source item beyond its length
 };
 
 // Dense 1D runs may carry gaps of at most this many bytes each and 1/16 of their payload in all.
 constexpr size_t kDenseGap = 4096;
+// a 2D row's padding to 16 bytes and a run's 256-byte alignment fit in 272; a ring's dense gap on top
+inline size_t PlanRules::pad_in() const { return 272 + (ring ? kDenseGap : 0); }
 
 // The open run of source bytes being coalesced into one H2D transfer.
 struct InRun {
@@ -71,6 +74,7 @@ struct InRun {
     size_t width = 0;              // the widest member (kPitch rows)
     size_t gaps = 0, payload = 0;  // gap and payload bytes (kDense)
     size_t rows = 0;               // members
+    size_t charge = 0;             // what the planner's capacity bound charged for the members
     size_t size() const {          // device bytes it needs
         if (kind == kNone) return 0;
         if (kind == kPitch) return rows * align_up(width, 16);
@@ -79,6 +83,7 @@ struct InRun {
     // The run with the range [o, o + len) appended, or kind kNone if it cannot take it.
     InRun extended(size_t o, size_t len, const PlanRules &R) const {
         InRun r = *this;
+        r.charge += len + R.pad_in();
         const size_t maxgap = R.ring ? kDenseGap : 0;
         switch (kind) {
             case kNone:
@@ -99,7 +104,9 @@ struct InRun {
                     // elsewhere only rows of one length
                     const size_t w = std::max(width, len);
                     const bool fits = R.ring ? o + w <= R.ring_bytes : len == width;
-                    if (fits && o - last >= w) {
+                    // rows widened to w must stay within the members' charge (short
+                    // fragments then a long one at one slot pitch overran the chunk buffer)
+                    if (fits && o - last >= w && 2 * align_up(w, 16) <= r.charge) {
                         r.kind = kPitch;
                         r.pitch = o - last;
                         r.width = w;
@@ -112,7 +119,7 @@ struct InRun {
             case kPitch: {
                 const size_t w = std::max(width, len);
                 const bool fits = R.ring ? o + w <= R.ring_bytes && len <= pitch : len == width;
-                if (o > last && o - last == pitch && fits) {
+                if (o > last && o - last == pitch && fits && (rows + 1) * align_up(w, 16) <= r.charge) {
                     r.width = w;
                     r.last = o;
                     ++r.rows;
@@ -124,9 +131,10 @@ struct InRun {
         r.kind = kNone;
         return r;
     }
-    static InRun single(size_t o, size_t len) {
+    static InRun single(size_t o, size_t len, const PlanRules &R) {
         InRun r;
         r.kind = kOne;
+        r.charge = len + R.pad_in();
         r.lo = r.last = o;
         r.end = o + len;
         r.width = r.payload = len;
@@ -204,7 +212,7 @@ class StreamPlanner {
         // so it holds at most cap_ plus one indivisible group (each item adding at most its bytes, a
         // dense gap, a 2D row's padding and an alignment)
         uint64_t in_total = 0, out_total = 0, gin = 0, gout = 0, gin_max = 0, gout_max = 0;
-        const uint64_t pad_in = 272 + (R_.ring ? kDenseGap : 0);
+        const uint64_t pad_in = R_.pad_in();
         for (size_t j = 0; j < n_; ++j) {
             if (it_.boundary(j)) gin = gout = 0;
             const PlanItem x = it_.get(j);
@@ -258,7 +266,7 @@ class StreamPlanner {
                 } else {
                     close_in();
                     in_base_ = align_up(in_base_, 256);
-                    run_ = InRun::single(x.src, x.len);
+                    run_ = InRun::single(x.src, x.len, R_);
                 }
                 members_.push_back(j);
                 c.payload += x.len;

@@ -554,6 +554,23 @@ int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_
     return to_int(launch_crc_desc(d_descs, n, d_out, img, crc_grid(dev), s, by_bytes, rows_hint));
 }
 
+// Internal diagnostic (not in include/lampi_csum.h): the read-only CRC piece-stream kernel's timeline,
+// 8 u64 per workgroup into d_stamps (tools/microbench/stream_timeline.py).  Returns the workgroup count
+// or a negative hipError_t.
+int lampi_diag_stream_timeline(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, uint64_t *d_stamps,
+                               void *stream) {
+    if (n == 0 || !d_descs || !d_out || !d_stamps) return -to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return -to_int(e);
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return -to_int(e);
+    uint32_t nwg = 0;
+    e = diag_stream_timeline(d_descs, n, d_out, img, d_stamps, (hipStream_t)stream, &nwg);
+    return e != hipSuccess ? -to_int(e) : (int)nwg;
+}
+
 int lampi_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode,
                                    void *stream) {
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);

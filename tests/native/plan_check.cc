@@ -130,6 +130,26 @@ int main() {
         for (size_t j = 0; j < 200; ++j) v.push_back({72 + j * 65536, 4096, j * 4096, 4096, true});
         run("ring_4k_pitch", v, 200 * 65536, true, 64u << 20, 1, 1);
     }
+    // short payloads then long ones at one constant slot pitch: a 2D run must never widen its
+    // rows past what the planner charged for its members (64 x 100 B then 65,456 B at a 64 KiB pitch once
+    // made a 65-row run of 64 KiB rows in a ~426 KB chunk)
+    {
+        std::vector<Item> v;
+        for (size_t j = 0; j < 64; ++j) v.push_back({72 + j * 65536, 100, j * 100, 100, true});
+        v.push_back({72 + 64 * 65536, 65456, 6400, 65456, true});
+        run("ring_pitch_short_then_long", v, 66 * 65536, true, 32u << 20);
+        for (int rep = 0; rep < 20; ++rep) {
+            std::vector<Item> w;
+            const size_t n = 20 + rng() % 400;
+            size_t apos = 0;
+            for (size_t j = 0; j < n; ++j) {
+                const uint64_t len = rng() % 3 ? 1 + rng() % 300 : 60000 + rng() % 5457;
+                w.push_back({72 + j * 65536, len, apos, len, true});
+                apos += len;
+            }
+            run("ring_pitch_mixed_" + std::to_string(rep), w, (n + 1) * 65536, true, (size_t)(1 + rng() % 32) << 20);
+        }
+    }
     // IB-shaped ring with ragged lengths, truncated copies (AppBufferLen <), skipped fragments
     for (int rep = 0; rep < 20; ++rep) {
         std::vector<Item> v;
