@@ -42,7 +42,14 @@ extern "C" {
  * (src/include/internal/state.h:129-132, mpirun -crc). */
 enum lampi_csum_mode {
     LAMPI_CSUM_CRC32 = 0,   /* uicrc  */
-    LAMPI_CSUM_SUM32 = 1    /* uicsum */
+    LAMPI_CSUM_SUM32 = 1,   /* uicsum */
+    /* Checksumming off: a network whose doChecksum flag is false (mpirun -mf/-if/-qf nochecksum,
+     * src/run/Input.cc:1986-2067; gmState.doChecksum src/path/gm/state.h:140).  Accepted only by the
+     * delivery batches (lampi_copy_to_app_batch, lampi_chain_copy_to_app_batch and their host forms):
+     * the bytes are copied, the checksum output is 0 and every fragment is DataOK, as CopyFunction /
+     * nonContigCopyFunction and CheckData behave with checksumming off (src/path/gm/recvFrag.h:178-181,
+     * :198-199, :231-232). */
+    LAMPI_CSUM_NONE = 2
 };
 
 /* Flag OR'ed into `mode` of lampi_frag_csum_batch[_strided] for batches of up to 32,768 descriptors:
@@ -193,7 +200,8 @@ typedef struct lampi_host_recv_frag {
  * their layout allows (dense runs one copy, a constant slot pitch one 2D copy), the delivered bytes come
  * back in one copy per run of fragments contiguous in the application buffer.  `mode` may carry
  * LAMPI_CSUM_ROWS_HINT(r) to override the row-group count the library derives from the fragments' mean
- * length.  Fragments up to 1 GiB. */
+ * length.  Fragments up to 1 GiB.  mode LAMPI_CSUM_NONE (checksumming off): lengthToCopy bytes copied and
+ * nothing more read, h_csum[i] = 0, every fragment DataOK, `expected` unused. */
 int lampi_host_copy_to_app_batch(const void *h_ring, size_t ring_bytes, const lampi_host_recv_frag *h_frags,
                                  size_t n, int64_t *h_copied, uint32_t *h_csum, uint32_t *h_mask, uint32_t *h_nbad,
                                  int mode);
@@ -242,6 +250,24 @@ typedef struct lampi_host_piece {
 int lampi_host_chain_csum_batch(const lampi_host_piece *h_pieces, size_t npieces, const uint32_t *h_first,
                                 size_t nfrags, uint32_t *h_out, int mode);
 
+/* RecvDesc_t::CopyToApp's non-contiguous branch for a batch of received fragments in host memory (ref
+ * src/path/common/BaseDesc.cc:326-340: non_contiguous_copy :72-163, then CheckData(checkSum, len_copied),
+ * gm/recvFrag.h:213-257): fragment f's pieces h_pieces[h_first[f]] .. [h_first[f+1] - 1] are the typemap
+ * pieces non_contiguous_copy walks (src = the fragment's bytes in the NIC ring, dst = the application buffer,
+ * copylen = csumlen = the piece's length; a fragment whose AppBufferLen <= 0 is delivered with no pieces).
+ * Each piece is copied, the checksum threaded through the pieces as nonContigCopyFunction does (CRC from
+ * CRC_INITIAL_REGISTER -- the pieces' partial is ignored --, SUM from a fresh state) and compared with
+ * h_expected[f] (the header's dataChecksum):
+ *   h_copied[f] = the bytes copied into the pieces (len_copied), or -1 when that is nonzero and the checksum
+ *                 differs (CopyToApp's return value); h_csum[f] = the calculated checksum;
+ *   h_mask (ceil(nfrags/32) words, bit set = corrupt, overwritten) and *h_nbad as lampi_host_copy_to_app_batch.
+ * mode LAMPI_CSUM_NONE (checksumming off): copies only, h_csum 0, every fragment DataOK, h_expected unused.
+ * DMA as lampi_host_chain_csum_batch.  Synchronous; 0 or a hipError_t (invalid arguments:
+ * hipErrorInvalidValue, nothing written). */
+int lampi_host_chain_copy_to_app_batch(const lampi_host_piece *h_pieces, size_t npieces, const uint32_t *h_first,
+                                       size_t nfrags, const uint32_t *h_expected, int64_t *h_copied, uint32_t *h_csum,
+                                       uint32_t *h_mask, uint32_t *h_nbad, int mode);
+
 /* Page-lock [h_ptr, h_ptr+len) for direct DMA by the host paths (hipHostRegister) and undo it:
  * the analogue of registering NIC buffers with the network (GM gm_register_memory).  Return 0
  * or a hipError_t. */
@@ -262,7 +288,12 @@ typedef struct lampi_frag_desc {
 } lampi_frag_desc;
 
 /* out[i] = checksum of fragment d[i] (CRC register or SUM value, as uicrc/uicsum
- * would return for the same bytes).  One wavefront per fragment.
+ * would return for the same bytes).  The schedule follows the batch: by
+ * default the piece streams -- each workgroup's fragments cut into 64-byte pieces packed into full
+ * 4 KiB rows, so mixed sizes keep every lane busy; with LAMPI_CSUM_ROWS_HINT (or the shape the
+ * stream's earlier batches showed) long fragments one wavefront each on the table-light kernel (CRC)
+ * or as row groups on short-lived workgroups (SUM); 1,024-65,536 fragments without a hint split by
+ * size class (CRC).  Results never depend on the schedule.
  * Replaces the per-fragment loop of gmPath::send / gmSendFragDesc::init
  * (src/path/gm/path.cc:98-176, src/path/gm/sendFrag.cc:147-155) and the Quadrics
  * checksum-only send (src/path/quadrics/sendFrag.h:861-872). */
@@ -406,10 +437,26 @@ typedef struct lampi_recv_desc {
  * *d_nbad: number of corrupt fragments.  The schedule follows the batch's shape (the rows hint
  * above, or the shape the stream's earlier batches showed): one wavefront per fragment, row groups
  * joined by a second launch, or two IB-sized fragments per wavefront (CRC) / one workgroup or one
- * wavefront per fragment (SUM); every payload byte is read from HBM once. */
+ * wavefront per fragment (SUM); every payload byte is read from HBM once.  mode LAMPI_CSUM_NONE
+ * (checksumming off): the lengthToCopy bytes copied (the SUM copy schedules), d_csum[i] = 0, every
+ * fragment DataOK, d_expected may be NULL. */
 int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void *d_expected,
                             size_t expected_stride, int64_t *d_copied, uint32_t *d_csum, uint32_t *d_mask,
                             uint32_t *d_nbad, int mode, void *stream);
+
+/* RecvDesc_t::CopyToApp's non-contiguous branch on the device (ref src/path/common/BaseDesc.cc:326-340 --
+ * non_contiguous_copy :72-163 and CheckData gm/recvFrag.h:213-257): lampi_chain_csum_batch's pieces and
+ * fragments (the typemap pieces of each received fragment: src in the received payload, dst in the
+ * application buffer, copylen = csumlen) with the checksum started from CRC_INITIAL_REGISTER (the pieces'
+ * partial is ignored; SUM from a fresh state) and compared with the 32-bit value at
+ * d_expected + f*expected_stride:
+ *   d_copied[f] = the bytes copied (len_copied), or -1 when that is nonzero and the checksum differs;
+ *   d_csum[f] = the calculated checksum; d_mask / *d_nbad as lampi_copy_to_app_batch (zeroed by the call).
+ * mode LAMPI_CSUM_NONE: copies only, d_csum 0, every fragment DataOK (d_expected may be NULL).
+ * Uses 8 * npieces bytes of stream-ordered scratch. */
+int lampi_chain_copy_to_app_batch(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first,
+                                  size_t nfrags, const void *d_expected, size_t expected_stride, int64_t *d_copied,
+                                  uint32_t *d_csum, uint32_t *d_mask, uint32_t *d_nbad, int mode, void *stream);
 
 /* ------------------------------------------------------------------------------------
  * Utilities (bench/test support, device-side).

@@ -10,7 +10,7 @@ kernels for gfx950 behind the C ABI in include/lampi_csum.h (liblampi_csum.so).
 * :mod:`lampi_amd.device` -- batched device-resident checksums over torch tensors
   (imported lazily: it needs torch).
 """
-from ._lib import CRC32, CRC_INITIAL_REGISTER, CRC_POLYNOMIAL, SUM32, FragDesc, lib  # noqa: F401
+from ._lib import CRC32, CRC_INITIAL_REGISTER, CRC_POLYNOMIAL, NONE, SUM32, FragDesc, lib  # noqa: F401
 from .memfunctions import (PartialState, PartialState64, bcopy_csum, bcopy_uicrc, bcopy_uicsum,  # noqa: F401
                            csum, header_checksum, uicrc, uicsum)
 

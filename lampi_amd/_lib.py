@@ -16,6 +16,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lampi_csum.h")
 
 CRC32 = 0  # enum lampi_csum_mode (include/lampi_csum.h)
 SUM32 = 1
+NONE = 2  # checksumming off (doChecksum == false): the delivery batches only
 BY_BYTES = 0x100  # LAMPI_CSUM_BY_BYTES: byte-balanced descriptor batches (OR'ed into the mode)
 
 
@@ -112,6 +113,8 @@ PROTOTYPES = {
                                               c_void_p, c_void_p]),
     "lampi_copy_to_app_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
                                                c_void_p, ctypes.c_int, c_void_p]),
+    "lampi_chain_copy_to_app_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_size_t,
+                                                     c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_msg_csum": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, c_void_p, ctypes.c_int,
                                       c_void_p]),
     "lampi_fill_stream": (ctypes.c_int, [c_void_p, c_size_t, ctypes.c_uint64, ctypes.c_uint64, c_void_p]),
@@ -131,6 +134,8 @@ PROTOTYPES = {
     "lampi_host_header_compare_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.c_uint32,
                                                        ctypes.c_uint32, c_void_p, c_void_p, ctypes.c_int]),
     "lampi_host_chain_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, ctypes.c_int]),
+    "lampi_host_chain_copy_to_app_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p,
+                                                          c_void_p, c_void_p, c_void_p, ctypes.c_int]),
     "lampi_device_scratch_bytes": (ctypes.c_int64, []),
     "lampi_host_register": (ctypes.c_int, [c_void_p, c_size_t]),
     "lampi_host_unregister": (ctypes.c_int, [c_void_p]),

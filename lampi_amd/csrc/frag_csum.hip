@@ -310,6 +310,19 @@ struct RecvSource {
     }
 };
 
+// CopyToApp with checksumming off (LAMPI_CSUM_NONE: the network's doChecksum == false, mpirun -mf/-if/-qf
+// nochecksum, ref src/run/Input.cc:1986-2067): CopyFunction only copies and returns 0
+// (src/path/gm/recvFrag.h:178-181), CheckData passes every fragment (:231-232).  Same copy as RecvSource, no
+// expected value read; d_csum[f] = 0 and d_copied[f] = lengthToCopy (emit).
+struct RecvCopyOnlySource : RecvSource {
+    __device__ FragInfo get(size_t f) const {
+        const lampi_recv_desc x = d[f];
+        const uint32_t c = to_copy(x);
+        return {(gbyte *)(uintptr_t)x.frag, c, 0u, (uint8_t *)(uintptr_t)x.app, c, 0u};
+    }
+    __device__ void verdict(size_t f, uint32_t, const FragInfo &fi) const { copied[f] = (int64_t)fi.copylen; }
+};
+
 // Read-only CRC descriptor batches of moderate size without a row-count hint run in two launches by
 // size class (launch_crc_desc): fragments of 8-16 rows (GM's 65,456-byte payloads) on the table-light
 // kernel, one wave each -- its best shape, 80% with the hint -- (SplitDescSource<true>), the rest on the
@@ -336,6 +349,8 @@ template <class S>
 struct IsRecv : std::false_type {};
 template <>
 struct IsRecv<RecvSource> : std::true_type {};
+template <>
+struct IsRecv<RecvCopyOnlySource> : std::true_type {};
 
 // The receive step's verdicts zeroed by the launch before the one that gives them (row groups: the first
 // launch, whose waves of group 0 zero the mask word of fragments f = 32i and f = 0 the count), instead of
@@ -443,6 +458,7 @@ __device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v, 
     }
     if constexpr (IsSplit<Src>::value)
         if (fi.aux) return;  // the other launch's fragment
+    if constexpr (std::is_same<Src, RecvCopyOnlySource>::value) v = 0;  // no checksum with checksumming off
     out[f] = v;
     if constexpr (IsRecv<Src>::value) src.verdict(f, v, fi);
 }
@@ -3911,6 +3927,25 @@ __global__ void __launch_bounds__(256) chain_small_kernel(const lampi_copy_desc 
     }
 }
 
+// RecvDesc_t::CopyToApp's non-contiguous branch over a chain batch (ref src/path/common/BaseDesc.cc:326-340:
+// non_contiguous_copy, then CheckData(checkSum, len_copied)): with `copied` set, fragment f's verdict --
+// copied[f] = the bytes it copied, or -1 when they were copied but the checksum differs from the expected value
+// at expected + f * exp_stride; mask bit / nbad as lampi_copy_to_app_batch.  init: CRC from
+// CRC_INITIAL_REGISTER (nonContigCopyFunction's firstCall, gm/recvFrag.h:198-200) instead of the first piece's
+// partial; nocheck: checksumming off (copy only, checksum 0, every fragment DataOK).
+// (ChainVerdict: frag_csum_kernels.h)
+__device__ __forceinline__ void chain_result(const ChainVerdict &v, uint32_t f, uint32_t csum, uint64_t copied,
+                                             uint32_t *out) {
+    out[f] = csum;
+    if (!v.copied) return;
+    const bool bad = !v.nocheck && copied != 0 && csum != *(const guint *)(v.expected + (size_t)f * v.exp_stride);
+    v.copied[f] = bad ? -1ll : (int64_t)copied;
+    if (bad) {
+        atomicOr(v.mask + (f >> 5), 1u << (f & 31u));
+        atomicAdd(v.nbad, 1u);
+    }
+}
+
 // C after `len` zero bytes (normal domain), T[e*128 + p*16 + v] = shift_{2^e}(v << 4p)
 __device__ __forceinline__ uint32_t shift_by(const uint32_t *T, uint32_t C, uint32_t len) {
     while (len) {
@@ -3928,7 +3963,8 @@ __device__ __forceinline__ uint32_t shift_by(const uint32_t *T, uint32_t C, uint
 __global__ void __launch_bounds__(256) chain_fold_kernel(const lampi_copy_desc *__restrict__ d,
                                                          const uint32_t *__restrict__ first, uint32_t nfrags,
                                                          const uint32_t *__restrict__ vals, int mode,
-                                                         const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
+                                                         const uint32_t *__restrict__ img, uint32_t *__restrict__ out,
+                                                         const ChainVerdict v) {
     __shared__ uint32_t T[32 * 128];  // 16 KiB: nibble tables of shift by 2^e bytes
     if (mode == LAMPI_CSUM_CRC32) {
         for (uint32_t t = threadIdx.x; t < 32 * 128; t += blockDim.x) {
@@ -3950,11 +3986,21 @@ __global__ void __launch_bounds__(256) chain_fold_kernel(const lampi_copy_desc *
     const uint32_t np = k1 > k0 ? k1 - k0 : 0u;
     const uint32_t per = (np + 63) / 64;  // contiguous run of pieces per lane
     const uint32_t a = k0 + min(np, lane * per), b = k0 + min(np, (lane + 1) * per);
+    // non_contiguous_copy's length: the bytes copied into the typemap pieces (BaseDesc.cc:160-161)
+    uint64_t copied = 0;
+    if (v.copied) {
+        for (uint32_t k = a; k < b; ++k) copied += d[k].copylen;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)copied, o), hi = (uint32_t)__shfl_xor((int)(uint32_t)(copied >> 32), o);
+            copied += ((uint64_t)hi << 32) | lo;
+        }
+    }
     if (mode != LAMPI_CSUM_CRC32) {
         uint32_t acc = 0;
         for (uint32_t k = a; k < b; ++k) acc += vals[k];
         acc = wave_add(acc);
-        if (lane == 0) out[f] = acc;
+        if (lane == 0) chain_result(v, f, v.nocheck ? 0u : acc, copied, out);
         return;
     }
     uint32_t C = 0, L = 0;
@@ -3974,8 +4020,8 @@ __global__ void __launch_bounds__(256) chain_fold_kernel(const lampi_copy_desc *
         }
     }
     if (lane == 0) {
-        const uint32_t partial = np ? d[k0].partial : kCrcInit;
-        out[f] = shift_by(T, partial, L) ^ C;
+        const uint32_t partial = np && !v.init ? d[k0].partial : kCrcInit;
+        chain_result(v, f, shift_by(T, partial, L) ^ C, copied, out);
     }
 }
 
@@ -4850,6 +4896,19 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
     if (!img) return hipErrorInvalidValue;
     const bool crc = mode == LAMPI_CSUM_CRC32;
     const RecvSource src{d, crc ? 0xFFFFFFFFu : 0u, expected, exp_stride, copied, mask, nbad};
+    if (mode == LAMPI_CSUM_NONE) {  // copy only, every fragment DataOK: the SUM copy schedules without the sums
+        const size_t nwords = (n + 31) / 32;
+        hipLaunchKernelGGL(zero_verdicts_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, mask, nwords,
+                           nbad);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        RecvCopyOnlySource co;
+        static_cast<RecvSource &>(co) = src;
+        bool small = false;  // (fragments of at most 2 KiB: a wave each, as SUM)
+        uint32_t *nh = nullptr;
+        rows_hint = learned_rows_hint(co, n, s, 2, rows_hint, &small, &nh, kShapeRowsSum);
+        return launch_sum_copy_groups(co, n, csum, s, rows_hint, small);
+    }
     bool pairs = false;
     uint32_t *nhalf = nullptr;
     rows_hint = learned_rows_hint(src, n, s, 2, rows_hint, &pairs, &nhalf, crc ? kShapeRows : kShapeRowsSum);
@@ -4939,6 +4998,27 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
                           const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
+    // Messages of >= 256 fragments on short-lived 128-thread workgroups, one fragment each (sum_copy_wg_kernel,
+    // the read-only SUM descriptors' shape: VERDICT r4 item 4), whatever the fragment length.  Same box,
+    // interleaved rounds (profiles/r05/sum_msg_ab.txt), against the regular kernel / piece streams: config B
+    // (4 KiB) 80.2-80.4 -> 87.1-87.3% (two fragments per workgroup 83.7%, four 82.1%); 16 KiB 78-79 -> 86.3%,
+    // config D's shard 0 (64 GiB of 16 KiB) 79.8-79.9 -> 86.6-87.2%; 32 KiB 77 -> 86%; GM's 65,456 B 76.6 ->
+    // 84.6%; 1 MiB 77.2 -> 88.4%.  A/B knobs LAMPI_SUM_MSG_WG = fragments per workgroup (0: off),
+    // LAMPI_SUM_MSG_MAX = the longest fragment taken (bytes).
+    static const uint32_t msg_wg = [] {
+        const char *e = std::getenv("LAMPI_SUM_MSG_WG");
+        return e ? (uint32_t)std::atoi(e) : 1u;
+    }();
+    static const size_t msg_max = [] {
+        const char *e = std::getenv("LAMPI_SUM_MSG_MAX");
+        return e ? (size_t)std::atoll(e) : ~(size_t)0;
+    }();
+    if (msg_wg && frag_len <= msg_max && n >= 256) {
+        hipLaunchKernelGGL(sum_copy_wg_kernel<MsgSource>,
+                           dim3((unsigned)std::min<size_t>((n + msg_wg - 1) / msg_wg, kMaxWgGrid)), dim3(kSumWgThreads), 0,
+                           s, MsgSource{base, msg_len, frag_len, 0u}, n, out);
+        return hipGetLastError();
+    }
     if (msg_len != 0 && frag_len % kRowBytes == 0 && msg_len % frag_len == 0 && regular_msg_frag(frag_len, true) &&
         ((uintptr_t)base & 15u) == 0 && n <= 0xFFFFFFFFull) {
         return launch_regular<true>(base, n, frag_len, 0u, out, nullptr, s);
@@ -5086,8 +5166,19 @@ hipError_t launch_scatter_u32(const uint32_t *vals, size_t n, uint8_t *dst, size
 }
 
 hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t *first, size_t nfrags, uint32_t *out,
-                        int mode, const uint32_t *img, uint32_t *vals, uint32_t *phase, hipStream_t s) {
+                        int mode, const uint32_t *img, uint32_t *vals, uint32_t *phase, hipStream_t s,
+                        const ChainVerdict *verdict) {
     if (nfrags == 0) return hipSuccess;
+    ChainVerdict v = verdict ? *verdict : ChainVerdict{};
+    if (mode == LAMPI_CSUM_NONE) {  // copies on the SUM kernels, no checksum
+        v.nocheck = 1;
+        mode = LAMPI_CSUM_SUM32;
+    }
+    if (v.copied) {
+        const size_t nwords = (nfrags + 31) / 32;
+        hipLaunchKernelGGL(zero_verdicts_kernel, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, v.mask, nwords,
+                           v.nbad);
+    }
     constexpr uint32_t kSmall = 256;  // pieces up to this many bytes: one thread each
     const bool sum = mode != LAMPI_CSUM_CRC32;
     if (npieces) {
@@ -5105,7 +5196,7 @@ hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t
                            (uint32_t)npieces, phase, kSmall, mode, img, vals);
     }
     hipLaunchKernelGGL(chain_fold_kernel, dim3((unsigned)((nfrags + kWaves - 1) / kWaves)), dim3(kBlock), 0, s, d, first,
-                       (uint32_t)nfrags, vals, mode, img, out);
+                       (uint32_t)nfrags, vals, mode, img, out, v);
     return hipGetLastError();
 }
 

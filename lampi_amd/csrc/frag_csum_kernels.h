@@ -69,9 +69,22 @@ hipError_t launch_check_data(const uint32_t *calc, const uint8_t *expected, size
                              size_t len_stride, size_t n, uint32_t *mask, uint32_t *nbad, hipStream_t s);
 // dst + i*stride = vals[i] (4-byte aligned records).
 hipError_t launch_scatter_u32(const uint32_t *vals, size_t n, uint8_t *dst, size_t stride, hipStream_t s);
-// Chained checksums over typemap pieces; vals / phase: npieces words of scratch each.
+// The verdict of a chain batch delivered as CopyToApp's non-contiguous branch (launch_chain, chain_fold_kernel):
+// copied == nullptr -- checksums only; otherwise copied[f] / mask / *nbad as lampi_copy_to_app_batch against the
+// 32-bit value at expected + f * exp_stride; init: CRC from CRC_INITIAL_REGISTER, not the first piece's partial.
+struct ChainVerdict {
+    const uint8_t *expected = nullptr;
+    size_t exp_stride = 0;
+    int64_t *copied = nullptr;
+    uint32_t *mask = nullptr;
+    uint32_t *nbad = nullptr;
+    uint32_t init = 0, nocheck = 0;
+};
+// Chained checksums over typemap pieces; vals / phase: npieces words of scratch each.  mode may be
+// LAMPI_CSUM_NONE (copies only, checksums 0).
 hipError_t launch_chain(const lampi_copy_desc *d, size_t npieces, const uint32_t *first, size_t nfrags, uint32_t *out,
-                        int mode, const uint32_t *img, uint32_t *vals, uint32_t *phase, hipStream_t s);
+                        int mode, const uint32_t *img, uint32_t *vals, uint32_t *phase, hipStream_t s,
+                        const ChainVerdict *verdict = nullptr);
 // 64-bit csum: per-descriptor sums (phased: desc.partial = byte phase 0..7) and the chained finish.
 hipError_t launch_sum64_desc(const lampi_frag_desc *d, size_t n, uint64_t *out, bool phased, hipStream_t s);
 // The host path's last kernels (combine / finish / a single piece) store their result, then, when

@@ -53,8 +53,16 @@ struct ChainScratch {
 };
 thread_local ChainScratch t_chain;
 
+// Verdict arrays of lampi_host_chain_copy_to_app_batch (null: checksums only).
+struct HostChainVerdict {
+    const uint32_t *expected = nullptr;
+    int64_t *copied = nullptr;
+    uint32_t *mask = nullptr;
+    uint32_t *nbad = nullptr;
+};
+
 hipError_t host_chain(const lampi_host_piece *pc, size_t npieces, const uint32_t *first, size_t nfrags,
-                      uint32_t *h_out, int mode) {
+                      uint32_t *h_out, int mode, const HostChainVerdict *hv = nullptr) {
     ChainScratch &cs = t_chain;
     if (cs.din.size() < npieces) {
         cs.din.resize(npieces);
@@ -131,9 +139,13 @@ hipError_t host_chain(const lampi_host_piece *pc, size_t npieces, const uint32_t
         TRY(issue_in(cs.in, nullptr, din, p.s_in));
         TRY(hipEventRecord(p.in_done[b], p.s_in));
         TRY(hipStreamWaitEvent(p.s_k, p.in_done[b], 0));
+        // (a delivery batch's fragments start from CRC_INITIAL_REGISTER, nonContigCopyFunction's first call; its
+        // verdicts are taken on the host below from the checksums that come back)
+        ChainVerdict init;
+        init.init = 1;
         if (fb > fa)
             TRY(launch_chain((const lampi_copy_desc *)dm + j0, j1 - j0, dcf, fb - fa, (uint32_t *)(dm + o_out) + fa,
-                             mode, img, dvals + j0, dvals + npieces + j0, p.s_k));
+                             mode, img, dvals + j0, dvals + npieces + j0, p.s_k, hv ? &init : nullptr));
         TRY(hipEventRecord(p.k_done[b], p.s_k));
         TRY(hipStreamWaitEvent(p.s_out, p.k_done[b], 0));
         TRY(issue_out(cs.out, dout, p.s_out));
@@ -146,21 +158,26 @@ hipError_t host_chain(const lampi_host_piece *pc, size_t npieces, const uint32_t
     TRY(hipStreamSynchronize(p.s_out));
     drain.armed = false;
     std::memcpy(h_out, p.hmeta + o_out, nfrags * sizeof(uint32_t));
+    if (hv) {  // CopyToApp's non-contiguous verdict (ref BaseDesc.cc:326-340 with CheckData, gm/recvFrag.h:213-257)
+        std::memset(hv->mask, 0, (nfrags + 31) / 32 * sizeof(uint32_t));
+        uint32_t nbad = 0;
+        for (size_t f = 0; f < nfrags; ++f) {
+            int64_t copied = 0;
+            for (size_t j = first[f]; j < first[f + 1]; ++j) copied += pc[j].copylen;
+            const bool bad = mode != LAMPI_CSUM_NONE && copied != 0 && h_out[f] != hv->expected[f];
+            hv->copied[f] = bad ? -1 : copied;
+            if (bad) {
+                hv->mask[f / 32] |= 1u << (f % 32);
+                ++nbad;
+            }
+        }
+        *hv->nbad = nbad;
+    }
     return hipSuccess;
 }
 
-}  // namespace
-}  // namespace lampi
-
-using namespace lampi;
-
-extern "C" {
-
-int lampi_host_chain_csum_batch(const lampi_host_piece *h_pieces, size_t npieces, const uint32_t *h_first,
-                                size_t nfrags, uint32_t *h_out, int mode) {
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return (int)hipErrorInvalidValue;
-    if (nfrags == 0) return 0;
-    if (!h_first || !h_out || (npieces && !h_pieces) || npieces > 0xFFFFFFFFull || nfrags > 0xFFFFFFFFull)
+int check_chain_args(const lampi_host_piece *h_pieces, size_t npieces, const uint32_t *h_first, size_t nfrags) {
+    if (!h_first || (npieces && !h_pieces) || npieces > 0xFFFFFFFFull || nfrags > 0xFFFFFFFFull)
         return (int)hipErrorInvalidValue;
     if (h_first[nfrags] > npieces) return (int)hipErrorInvalidValue;
     for (size_t f = 0; f < nfrags; ++f) {
@@ -174,7 +191,45 @@ int lampi_host_chain_csum_batch(const lampi_host_piece *h_pieces, size_t npieces
         }
         if (bytes > kHostMaxFrag) return (int)hipErrorInvalidValue;
     }
+    return 0;
+}
+
+}  // namespace
+}  // namespace lampi
+
+using namespace lampi;
+
+extern "C" {
+
+int lampi_host_chain_csum_batch(const lampi_host_piece *h_pieces, size_t npieces, const uint32_t *h_first,
+                                size_t nfrags, uint32_t *h_out, int mode) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return (int)hipErrorInvalidValue;
+    if (nfrags == 0) return 0;
+    if (!h_out) return (int)hipErrorInvalidValue;
+    const int rc = check_chain_args(h_pieces, npieces, h_first, nfrags);
+    if (rc) return rc;
     return (int)host_chain(h_pieces, npieces, h_first, nfrags, h_out, mode);
+}
+
+int lampi_host_chain_copy_to_app_batch(const lampi_host_piece *h_pieces, size_t npieces, const uint32_t *h_first,
+                                       size_t nfrags, const uint32_t *h_expected, int64_t *h_copied, uint32_t *h_csum,
+                                       uint32_t *h_mask, uint32_t *h_nbad, int mode) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32 && mode != LAMPI_CSUM_NONE)
+        return (int)hipErrorInvalidValue;
+    if (!h_nbad) return (int)hipErrorInvalidValue;
+    if (nfrags == 0) {
+        *h_nbad = 0;
+        return 0;
+    }
+    if (!h_copied || !h_csum || !h_mask || (mode != LAMPI_CSUM_NONE && !h_expected)) return (int)hipErrorInvalidValue;
+    const int rc = check_chain_args(h_pieces, npieces, h_first, nfrags);
+    if (rc) return rc;
+    HostChainVerdict v;
+    v.expected = h_expected;
+    v.copied = h_copied;
+    v.mask = h_mask;
+    v.nbad = h_nbad;
+    return (int)host_chain(h_pieces, npieces, h_first, nfrags, h_csum, mode, &v);
 }
 
 }  // extern "C"

@@ -53,14 +53,16 @@ uint32_t to_copy(const lampi_host_recv_frag &x) {
 
 // The batch as the planner sees it: fragment j reads its `length` ring bytes (all checksummed) and
 // writes lengthToCopy of them to its application address -- or nothing at all when lengthToCopy is 0.
+// (checksumming off, LAMPI_CSUM_NONE: only the lengthToCopy bytes are read)
 struct RecvItems {
     const lampi_host_recv_frag *f;
     size_t n;
+    bool copy_only;
     size_t size() const { return n; }
     PlanItem get(size_t j) const {
         const uint32_t c = to_copy(f[j]);
         if (!c) return PlanItem{0, 0, nullptr, 0};
-        return PlanItem{f[j].frag_off, f[j].length, (uint8_t *)f[j].app, c};
+        return PlanItem{f[j].frag_off, copy_only ? c : f[j].length, (uint8_t *)f[j].app, c};
     }
     bool boundary(size_t) const { return true; }
 };
@@ -91,7 +93,7 @@ hipError_t host_recv(const uint8_t *h_ring, size_t ring_bytes, const lampi_host_
         rs.din.resize(n);
         rs.dout.resize(n);
     }
-    const RecvItems items{f, n};
+    const RecvItems items{f, n, mode == LAMPI_CSUM_NONE};
     PlanRules rules;
     rules.ring = true;
     rules.ring_bytes = ring_bytes;
@@ -251,7 +253,8 @@ int lampi_host_copy_to_app_batch(const void *h_ring, size_t ring_bytes, const la
                                  int64_t *h_copied, uint32_t *h_csum, uint32_t *h_mask, uint32_t *h_nbad, int mode) {
     const uint32_t hint = LAMPI_CSUM_ROWS_HINT_OF(mode);
     mode &= ~LAMPI_CSUM_ROWS_HINT_MASK;
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return (int)hipErrorInvalidValue;
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32 && mode != LAMPI_CSUM_NONE)
+        return (int)hipErrorInvalidValue;
     if (!h_nbad || n > 0xFFFFFFFFull) return (int)hipErrorInvalidValue;
     if (n == 0) {
         *h_nbad = 0;

@@ -623,8 +623,10 @@ int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void
                             void *stream) {
     const uint32_t rows_hint = std::max(1u, LAMPI_CSUM_ROWS_HINT_OF(mode));
     mode &= ~LAMPI_CSUM_ROWS_HINT_MASK;
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
-    if (!d_nbad || (n && (!d_descs || !d_expected || !d_copied || !d_csum || !d_mask)) ||
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32 && mode != LAMPI_CSUM_NONE)
+        return to_int(hipErrorInvalidValue);
+    const bool check = mode != LAMPI_CSUM_NONE;  // (checksumming off: no expected values read)
+    if (!d_nbad || (n && (!d_descs || (check && !d_expected) || !d_copied || !d_csum || !d_mask)) ||
         ((uintptr_t)d_expected & 3u) || (expected_stride & 3u) || n > 0xFFFFFFFFull)
         return to_int(hipErrorInvalidValue);
     int dev = 0;
@@ -689,6 +691,45 @@ int lampi_chain_csum_batch(const lampi_copy_desc *d_pieces, size_t npieces, cons
     }
     e = launch_chain(d_pieces, npieces, d_first, nfrags, d_out, mode, img, scratch, scratch ? scratch + npieces : nullptr,
                      s);
+    if (scratch) {
+        const hipError_t f = hipFreeAsync(scratch, s);
+        if (e == hipSuccess) e = f;
+    }
+    return to_int(e);
+}
+
+int lampi_chain_copy_to_app_batch(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first,
+                                  size_t nfrags, const void *d_expected, size_t expected_stride, int64_t *d_copied,
+                                  uint32_t *d_csum, uint32_t *d_mask, uint32_t *d_nbad, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32 && mode != LAMPI_CSUM_NONE)
+        return to_int(hipErrorInvalidValue);
+    const bool check = mode != LAMPI_CSUM_NONE;
+    if (!d_nbad) return to_int(hipErrorInvalidValue);
+    hipStream_t s = (hipStream_t)stream;
+    if (nfrags == 0) return to_int(hipMemsetAsync(d_nbad, 0, sizeof(uint32_t), s));
+    if (!d_first || !d_copied || !d_csum || !d_mask || (check && !d_expected) || (npieces && !d_pieces) ||
+        ((uintptr_t)d_expected & 3u) || (expected_stride & 3u) || npieces > 0xFFFFFFFFull || nfrags > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return to_int(e);
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return to_int(e);
+    uint32_t *scratch = nullptr;
+    if (npieces) {
+        e = hipMallocAsync((void **)&scratch, 2 * npieces * sizeof(uint32_t), s);
+        if (e != hipSuccess) return to_int(e);
+    }
+    ChainVerdict v;
+    v.expected = (const uint8_t *)d_expected;
+    v.exp_stride = expected_stride;
+    v.copied = d_copied;
+    v.mask = d_mask;
+    v.nbad = d_nbad;
+    v.init = 1;  // nonContigCopyFunction's first call starts from CRC_INITIAL_REGISTER
+    e = launch_chain(d_pieces, npieces, d_first, nfrags, d_csum, mode, img, scratch,
+                     scratch ? scratch + npieces : nullptr, s, &v);
     if (scratch) {
         const hipError_t f = hipFreeAsync(scratch, s);
         if (e == hipSuccess) e = f;

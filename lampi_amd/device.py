@@ -9,9 +9,9 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ._lib import BY_BYTES, CRC32, CRC_INITIAL_REGISTER, SUM32, check, lib, rows_hint_bits
+from ._lib import BY_BYTES, CRC32, CRC_INITIAL_REGISTER, NONE, SUM32, check, lib, rows_hint_bits
 
-__all__ = ["CRC32", "SUM32", "frag_csum_batch", "frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
+__all__ = ["CRC32", "SUM32", "NONE", "chain_copy_to_app_batch", "frag_csum_batch", "frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
            "make_descs", "make_copy_descs", "as_u32", "chain_csum_batch", "header_csum_batch", "header_check_batch", "check_data_batch",
            "mask_bits", "make_recv_descs", "copy_to_app_batch"]
 
@@ -225,6 +225,35 @@ def chain_csum_batch(pieces: torch.Tensor, first, mode: int = CRC32, out: torch.
     return out
 
 
+def chain_copy_to_app_batch(pieces: torch.Tensor, first, expected: torch.Tensor | None, expected_stride: int = 4,
+                            mode: int = CRC32, stream: torch.cuda.Stream | None = None):
+    """RecvDesc_t::CopyToApp's non-contiguous branch (src/path/common/BaseDesc.cc:326-340): the typemap
+    pieces of each received fragment copied, the checksum from CRC_INITIAL_REGISTER compared with
+    expected (None with mode NONE).  Returns (copied int64 -- len_copied or -1 --, csum int32, mask, nbad)."""
+    _require_cuda(pieces, "pieces")
+    npieces = pieces.numel() * pieces.element_size() // 32
+    fa = np.asarray(first, dtype=np.uint32) if not isinstance(first, torch.Tensor) else None
+    if fa is not None:
+        if fa.size < 1 or (fa.size > 1 and (np.any(np.diff(fa.astype(np.int64)) < 0) or int(fa[-1]) > npieces)):
+            raise ValueError("first must be nondecreasing and end at most at the piece count")
+        first_t = torch.from_numpy(fa.view(np.int32)).to(pieces.device)
+    else:
+        _require_cuda(first, "first")
+        first_t = first
+    nfrags = first_t.numel() - 1
+    if expected is not None:
+        _records(expected, nfrags, expected_stride, "expected")
+    copied = torch.empty(max(nfrags, 1), dtype=torch.int64, device=pieces.device)
+    csum = torch.empty(max(nfrags, 1), dtype=torch.int32, device=pieces.device)
+    mask = torch.empty(max((nfrags + 31) // 32, 1), dtype=torch.int32, device=pieces.device)
+    nbad = torch.empty(1, dtype=torch.int32, device=pieces.device)
+    check(lib().lampi_chain_copy_to_app_batch(pieces.data_ptr(), npieces, first_t.data_ptr(), nfrags,
+                                              0 if expected is None else expected.data_ptr(), expected_stride,
+                                              copied.data_ptr(), csum.data_ptr(), mask.data_ptr(), nbad.data_ptr(),
+                                              mode, _stream_handle(stream)), "lampi_chain_copy_to_app_batch")
+    return copied[:nfrags], csum[:nfrags], mask, nbad
+
+
 def _records(t: torch.Tensor, n: int, stride: int, what: str) -> None:
     _require_cuda(t, what)
     if n and (n - 1) * stride + 4 > t.numel() * t.element_size():
@@ -327,7 +356,12 @@ def copy_to_app_batch(descs: torch.Tensor, expected: torch.Tensor, expected_stri
     rows_hint: as for frag_bcopy_batch (GM's 65,456-byte payloads: 16)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
-    _records(expected.view(torch.uint8)[expected_offset:] if count else expected, count, expected_stride, "expected")
+    if expected is None:  # (mode NONE: nothing compared)
+        expected = torch.zeros(1, dtype=torch.int32, device=descs.device)
+        expected_stride = expected_offset = 0
+    else:
+        _records(expected.view(torch.uint8)[expected_offset:] if count else expected, count, expected_stride,
+                 "expected")
     copied = torch.empty(max(count, 1), dtype=torch.int64, device=descs.device)
     csum = torch.empty(max(count, 1), dtype=torch.int32, device=descs.device)
     # (the call zeroes the mask words and the count itself: no fill kernels here, except for an empty batch)

@@ -97,6 +97,40 @@ def copy_to_app(api: "_Api", frag: np.ndarray, length: int, app_len: int, expect
     return (n if c == expected else -1), c, dst
 
 
+def copy_to_app_nochecksum(frag: np.ndarray, length: int, app_len: int):
+    """RecvDesc_t::CopyToApp (ref src/path/common/BaseDesc.cc:288-342) with checksumming off
+    (gmState.doChecksum == false, src/path/gm/state.h:140; mpirun -mf nochecksum, src/run/Input.cc:1986-2067):
+    CopyFunction only copies lengthToCopy bytes and returns 0 (src/path/gm/recvFrag.h:178-181), CheckData passes
+    (:231-232).  Returns (bytes copied, 0 -- the checksum output the batch defines --, the bytes delivered)."""
+    if app_len <= 0:
+        return 0, 0, np.zeros(0, np.uint8)
+    n = min(length, app_len)
+    return n, 0, np.array(frag[:n], np.uint8)
+
+
+def non_contiguous_copy_to_app(api: "_Api", pieces: list, expected: int, mode: int):
+    """CopyToApp's non-contiguous branch (ref src/path/common/BaseDesc.cc:326-340): non_contiguous_copy
+    (:72-163) calls nonContigCopyFunction once per typemap piece (GM src/path/gm/recvFrag.h:186-211) -- CRC:
+    the register from CRC_INITIAL_REGISTER on the first call, bcopy_uicrc(piece, len, len, register); SUM:
+    *checkSum = 0 (:124-125), += bcopy_uicsum with the partial-word state threaded; checksumming off: memcpy
+    only -- then CheckData(checkSum, len_copied) (gm/recvFrag.h:213-257).  pieces: the pieces' source bytes
+    in order; mode 0 CRC, 1 SUM, 2 off.  Returns (len_copied or -1, the checksum)."""
+    copied = int(sum(int(p.size) for p in pieces))
+    if mode == 2:
+        return copied, 0
+    if mode == 0:
+        c = CRC_INIT
+        for p in pieces:
+            c = api.bcopy_uicrc(p, np.zeros(max(p.size, 1), np.uint8), p.size, p.size, c)
+    else:
+        c, pi, pl = 0, 0, 0
+        for p in pieces:
+            r, pi, pl = api.bcopy_uicsum(p, np.zeros(max(p.size, 1), np.uint8), p.size, p.size, pi, pl)
+            c = (c + r) & 0xFFFFFFFF
+    ok = copied == 0 or c == expected
+    return (copied if ok else -1), c
+
+
 class Restatement(_Api):
     def __init__(self, path: str = RESTATEMENT_SO):
         if not os.path.exists(path):

@@ -210,6 +210,73 @@ static void run_random(int tid, uint64_t seed) {
     }
 }
 
+// The non-contiguous CopyToApp (lampi_host_chain_copy_to_app_batch): random typemaps of received fragments
+// scattered into an application buffer, ~25% of the expected checksums corrupted (|= 0xA4A4), the pieces'
+// partial garbage (the batch starts CRC from the initial register), fragments with no pieces (AppBufferLen
+// <= 0); every verdict, checksum and delivered byte against the oracle's piece-by-piece chain
+// (ref src/path/common/BaseDesc.cc:72-163, :326-340; src/path/gm/recvFrag.h:186-257), all three modes.
+static void run_deliver(int tid, uint64_t seed) {
+    std::mt19937_64 rng(seed);
+    for (int rep = 0; rep < 4; ++rep) {
+        const size_t nf = 1 + rng() % 500;
+        const size_t src_bytes = 16u << 20;
+        Buf src(src_bytes, rep & 1, 0), dst(src_bytes, rep & 1, 0x5A);
+        oracle_fill_stream(src.p, seed + 31 * rep, 0, src_bytes);
+        std::vector<lampi_host_piece> pcs;
+        std::vector<uint32_t> first{0};
+        size_t dpos = 0;
+        for (size_t f = 0; f < nf; ++f) {
+            const size_t np = rng() % 11 == 0 ? 0 : 1 + rng() % 30;
+            for (size_t i = 0; i < np && dpos + 21000 < dst.n; ++i) {
+                const uint32_t len = rng() % 9 == 0 ? 0u : rng() % 4 ? 1 + rng() % 64 : 200 + rng() % 20000;
+                const size_t so = rng() % (src_bytes - len);
+                pcs.push_back(lampi_host_piece{src.p + so, dst.p + dpos, len, len, (uint32_t)rng(), 0u});
+                dpos += len + rng() % 5;
+            }
+            first.push_back((uint32_t)pcs.size());
+        }
+        for (int mode : {LAMPI_CSUM_CRC32, LAMPI_CSUM_SUM32, LAMPI_CSUM_NONE}) {
+            std::memset(dst.p, 0x5A, dst.n);
+            std::vector<uint8_t> want_dst(dst.n, 0x5A);
+            std::vector<uint32_t> expected(nf), want_csum(nf);
+            std::vector<int64_t> want_copied(nf);
+            std::vector<uint32_t> want_mask((nf + 31) / 32, 0u);
+            uint32_t want_nbad = 0;
+            for (size_t f = 0; f < nf; ++f) {
+                uint32_t crc = ORACLE_CRC_INIT, sum = 0, pi = 0, pl = 0;
+                int64_t copied = 0;
+                for (size_t j = first[f]; j < first[f + 1]; ++j) {
+                    const lampi_host_piece &x = pcs[j];
+                    if (mode == LAMPI_CSUM_CRC32) crc = oracle_uicrc(x.src, x.copylen, crc);
+                    if (mode == LAMPI_CSUM_SUM32) sum += oracle_uicsum(x.src, x.copylen, &pi, &pl);
+                    std::memcpy(want_dst.data() + ((uint8_t *)x.dst - dst.p), x.src, x.copylen);
+                    copied += x.copylen;
+                }
+                const uint32_t c = mode == LAMPI_CSUM_CRC32 ? crc : mode == LAMPI_CSUM_SUM32 ? sum : 0u;
+                expected[f] = rng() % 4 == 0 ? (c | 0xA4A4u) : c;
+                const bool bad = mode != LAMPI_CSUM_NONE && copied != 0 && c != expected[f];
+                want_csum[f] = c;
+                want_copied[f] = bad ? -1 : copied;
+                if (bad) {
+                    want_mask[f / 32] |= 1u << (f % 32);
+                    ++want_nbad;
+                }
+            }
+            std::vector<int64_t> copied(nf, 77);
+            std::vector<uint32_t> csum(nf, 0xDEADBEEFu), mask((nf + 31) / 32, 0xFFFFFFFFu);
+            uint32_t nbad = 12345;
+            const int rc = lampi_host_chain_copy_to_app_batch(pcs.data(), pcs.size(), first.data(), nf, expected.data(),
+                                                              copied.data(), csum.data(), mask.data(), &nbad, mode);
+            const bool ok = rc == 0 && copied == want_copied && csum == want_csum && mask == want_mask &&
+                            nbad == want_nbad && std::memcmp(dst.p, want_dst.data(), dst.n) == 0;
+            report("deliver t" + std::to_string(tid) + " rep " + std::to_string(rep) + " frags " + std::to_string(nf) +
+                       " pieces " + std::to_string(pcs.size()) + " mode " + std::to_string(mode) + " bad " +
+                       std::to_string(want_nbad),
+                   ok);
+        }
+    }
+}
+
 static void run_edges() {
     std::vector<uint8_t> a(4096, 1), b(4096, 0x5A);
     lampi_host_piece x{a.data(), b.data(), 100, 100, ORACLE_CRC_INIT, 0u};
@@ -228,12 +295,24 @@ static void run_edges() {
     ok = lampi_host_chain_csum_batch(nullptr, 0, f_empty, 3, o3, 0) == 0 && o3[0] == ORACLE_CRC_INIT &&
          o3[2] == ORACLE_CRC_INIT && lampi_host_chain_csum_batch(nullptr, 0, f_empty, 3, o3, 1) == 0 && o3[1] == 0;
     report("fragments_without_pieces", ok);
+    // the delivery batch: bad arguments refused before anything is written; no pieces = DataOK whatever expected
+    int64_t cp[3] = {7, 7, 7};
+    uint32_t cs[3] = {1, 1, 1}, mk[1] = {0xFFFFFFFFu}, nb = 9, ex[3] = {1, 2, 3};
+    ok = lampi_host_chain_copy_to_app_batch(&x, 1, f_bad, 1, ex, cp, cs, mk, &nb, 0) != 0 &&
+         lampi_host_chain_copy_to_app_batch(&x, 1, f_ok, 1, nullptr, cp, cs, mk, &nb, 0) != 0 &&
+         lampi_host_chain_copy_to_app_batch(&x, 1, f_ok, 1, ex, cp, cs, mk, &nb, 9) != 0 && cp[0] == 7 && nb == 9;
+    ok = ok && lampi_host_chain_copy_to_app_batch(nullptr, 0, f_empty, 3, ex, cp, cs, mk, &nb, 0) == 0 && nb == 0 &&
+         mk[0] == 0 && cp[0] == 0 && cp[2] == 0 && cs[1] == ORACLE_CRC_INIT &&
+         lampi_host_chain_copy_to_app_batch(nullptr, 0, f_empty, 3, nullptr, cp, cs, mk, &nb, LAMPI_CSUM_NONE) == 0 &&
+         nb == 0 && cs[0] == 0;
+    report("deliver_edges", ok);
 }
 
 static void suite(int tid, const std::vector<Case> *cases) {
     if (cases && !cases->empty()) run_fixtures(tid, *cases);
     run_vectors(tid, 500 + tid);
     run_random(tid, 900 + 17 * tid);
+    run_deliver(tid, 1300 + 7 * tid);
 }
 
 int main(int argc, char **argv) {

@@ -103,6 +103,8 @@ struct Want {
 static Want copy_to_app(const uint8_t *frag, uint32_t length, int64_t app_len, uint32_t expected, int mode,
                         std::vector<uint8_t> &tmp) {
     const uint32_t c = app_len <= 0 ? 0u : (app_len < (int64_t)length ? (uint32_t)app_len : length);
+    // checksumming off: CopyFunction copies and returns 0 (gm/recvFrag.h:178-181), CheckData passes (:231-232)
+    if (mode == LAMPI_CSUM_NONE) return {(int64_t)c, 0u, false};
     if (c == 0) return {0, mode == LAMPI_CSUM_CRC32 ? ORACLE_CRC_INIT : 0u, false};
     tmp.resize(std::max<size_t>(c, 1));
     uint32_t v;
@@ -136,9 +138,11 @@ struct Ring {
 
 // One batch: build and stamp the ring, corrupt some of it, check the headers, deliver the fragments
 // whose headers pass, compare everything with the oracle.
-static void run_batch(int tid, const Shape &s, int mode, bool pin, bool shuffled, uint64_t seed) {
+// dmode: the delivery's mode (LAMPI_CSUM_NONE: checksumming off; the headers are still checked in `mode`)
+static void run_batch(int tid, const Shape &s, int mode, bool pin, bool shuffled, uint64_t seed, int dmode = -1) {
+    if (dmode < 0) dmode = mode;
     char tag[200];
-    std::snprintf(tag, sizeof tag, "t%d %s mode %d ring_%s %s", tid, s.name, mode, pin ? "pinned" : "pageable",
+    std::snprintf(tag, sizeof tag, "t%d %s mode %d/%d ring_%s %s", tid, s.name, mode, dmode, pin ? "pinned" : "pageable",
                   shuffled ? "shuffled" : "ring_order");
     const size_t n = shuffled ? std::min<size_t>(s.nslots, 300) : s.nslots;
     Ring ring(n * s.S, pin);
@@ -212,14 +216,14 @@ static void run_batch(int tid, const Shape &s, int mode, bool pin, bool shuffled
     std::vector<uint32_t> csum(m + 1, 0xDEADBEEFu), mask((m + 31) / 32 + 1, 0xDEADBEEFu);
     uint32_t nbad = 0xDEADBEEFu;
     rc = lampi_host_copy_to_app_batch(ring.p, ring.bytes, fr.data(), m, copied.data(), csum.data(), mask.data(), &nbad,
-                                      mode);
+                                      dmode);
     ok = rc == 0 && copied[m] == 0x7777 && csum[m] == 0xDEADBEEFu && mask.back() == 0xDEADBEEFu;
     std::vector<uint8_t> want_app(app.size(), 0x5A), tmp;
     uint32_t wbad = 0;
     for (size_t i = 0; ok && i < m; ++i) {
         const lampi_host_recv_frag &x = fr[i];
         const uint8_t *frag = ring.p + x.frag_off;
-        const Want w = copy_to_app(frag, x.length, x.app_len, x.expected, mode, tmp);
+        const Want w = copy_to_app(frag, x.length, x.app_len, x.expected, dmode, tmp);
         ok = copied[i] == w.copied && csum[i] == w.csum && bit(mask, i) == w.bad;
         wbad += w.bad;
         const uint32_t c = x.app_len <= 0 ? 0u : (uint32_t)std::min<int64_t>(x.app_len, x.length);
@@ -237,9 +241,13 @@ static void run_batch(int tid, const Shape &s, int mode, bool pin, bool shuffled
 static void run_suite(int tid, const std::vector<Shape> &shapes) {
     uint64_t seed = 1000 + 97 * (uint64_t)tid;
     for (const Shape &s : shapes)
-        for (int mode : {LAMPI_CSUM_CRC32, LAMPI_CSUM_SUM32})
+        for (int mode : {LAMPI_CSUM_CRC32, LAMPI_CSUM_SUM32, LAMPI_CSUM_NONE})
             for (int pin = 0; pin < 2; ++pin)
-                for (int shuf = 0; shuf < 2; ++shuf) run_batch(tid, s, mode, pin != 0, shuf != 0, ++seed);
+                for (int shuf = 0; shuf < 2; ++shuf)
+                    if (mode == LAMPI_CSUM_NONE)  // checksumming off: headers CRC-checked, delivery copy only
+                        run_batch(tid, s, LAMPI_CSUM_CRC32, pin != 0, shuf != 0, ++seed, LAMPI_CSUM_NONE);
+                    else
+                        run_batch(tid, s, mode, pin != 0, shuf != 0, ++seed);
 }
 
 // Edge cases of one small batch: invalid arguments write nothing, an empty batch, only empty deliveries.

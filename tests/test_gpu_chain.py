@@ -151,3 +151,66 @@ def test_chain_empty_and_zero_length(cuda):
         got = dv.as_u32(dv.chain_csum_batch(pieces, [0, 0, 3, 3], mode=mode))
         assert got[0] == empty and got[2] == empty
         assert got[1] == (0xFFFFFFFF if mode == 0 else 0)  # three empty pieces: the register passes through
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["crc", "sum", "off"])
+def test_chain_copy_to_app_verdicts(cuda, oracle, mode):
+    """CopyToApp's non-contiguous branch (lampi_chain_copy_to_app_batch; ref src/path/common/BaseDesc.cc:326-340,
+    non_contiguous_copy :72-163, CheckData src/path/gm/recvFrag.h:213-257): the reference's 150 chain fixtures
+    as received fragments scattered into typemap pieces of an application buffer, plus fragments with no
+    pieces (AppBufferLen <= 0) and with zero-length pieces.  ~30% of the expected checksums are corrupted
+    (dataChecksum |= 0xA4A4, recvFrag.h:215-229); the pieces' partial is garbage (the batch starts CRC from
+    CRC_INITIAL_REGISTER).  copied / csum / mask / nbad against oracle.non_contiguous_copy_to_app, the delivered
+    bytes against the fragments."""
+    import torch
+
+    from oracle.oracle import non_contiguous_copy_to_app
+
+    dv = _dv()
+    rng = np.random.default_rng(404 + mode)
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fixtures.json")) as f:
+        cases = json.load(f)["chain"]
+    msgs = [oracle.stream(c["seed"], c["off"], c["len"]) for c in cases]
+    # a few extra received fragments: no pieces at all, and zero-length pieces around real ones
+    msgs += [np.zeros(0, np.uint8), np.zeros(0, np.uint8), oracle.stream(9, 0, 300)]
+    cuts = [c["cuts"] for c in cases] + [None, [], [0, 0, 150, 150, 300]]
+    moff = np.concatenate([[0], np.cumsum([m.size + 16 for m in msgs])[:-1]]).astype(np.int64)
+    src_host = np.zeros(int(moff[-1]) + msgs[-1].size + 16, np.uint8)
+    for o, m in zip(moff, msgs):
+        src_host[o:o + m.size] = m
+    src = torch.from_numpy(src_host).to(cuda)
+    so, do, ln, first, want, exp = [], [], [], [0], [], []
+    dpos = 0
+    for m, o, cu in zip(msgs, moff, cuts):
+        parts = []
+        if cu is not None:
+            bounds = [0] + list(cu) + [m.size]
+            for a, b in zip(bounds, bounds[1:]):
+                so.append(int(o) + a)
+                do.append(dpos)
+                ln.append(b - a)
+                parts.append(m[a:b])
+                dpos += b - a + int(rng.integers(1, 9))  # the typemap's holes in the application buffer
+        first.append(len(so))
+        true = non_contiguous_copy_to_app(oracle, parts, 0, mode)[1]
+        e = true | 0xA4A4 if rng.random() < 0.3 else true
+        exp.append(e)
+        want.append(non_contiguous_copy_to_app(oracle, parts, e, mode))
+    dst = torch.full((dpos + 16,), 0x5C, dtype=torch.uint8, device=cuda)
+    partials = rng.integers(0, 1 << 32, size=len(so), dtype=np.uint64)
+    pieces = dv.make_copy_descs(src, so, dst, do, ln, ln, partials)
+    expected = torch.from_numpy(np.array(exp, np.uint32).view(np.int32)).to(cuda)
+    copied, csum, mask, nbad = dv.chain_copy_to_app_batch(pieces, first, None if mode == 2 else expected, 4, mode=mode)
+    nf = len(msgs)
+    want_copied = np.array([w[0] for w in want], np.int64)
+    want_csum = np.array([w[1] for w in want], np.uint32)
+    assert np.array_equal(copied.cpu().numpy(), want_copied), np.nonzero(copied.cpu().numpy() != want_copied)[0][:8]
+    assert np.array_equal(dv.as_u32(csum), want_csum)
+    bad = want_copied == -1
+    assert np.array_equal(dv.mask_bits(mask, nf), bad)
+    assert int(nbad.item()) == int(bad.sum())
+    assert (bad.any() and not bad.all()) if mode != 2 else not bad.any()
+    want_dst = np.full(dpos + 16, 0x5C, np.uint8)
+    for s_, d_, n_ in zip(so, do, ln):
+        want_dst[d_:d_ + n_] = src_host[s_:s_ + n_]
+    assert np.array_equal(dst.cpu().numpy(), want_dst)  # delivered whatever the verdict, holes untouched

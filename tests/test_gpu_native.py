@@ -114,8 +114,8 @@ def test_native_host_receive_path_matches_oracle(cuda):
     caller (tests/native/host_recv_caller.cc): GM rings of 64 KiB buffers with 65,456-byte and 4 KiB
     payloads, IB rings of 2,048-byte buffers behind a 40-byte GRH; ~1% corrupted headers (incl. the
     reference's |= 0xA4A4), ~2% corrupted data checksums, ~1% corrupted payloads; AppBufferLen <= 0 / < /
-    = / >; ragged and empty fragments; ring-order and shuffled batches; pinned and pageable rings; both
-    modes; two threads at once, then the main thread.  Every verdict, checksum, copied count and
+    = / >; ragged and empty fragments; ring-order and shuffled batches; pinned and pageable rings; CRC, SUM
+    and checksumming off (LAMPI_CSUM_NONE, headers checked in CRC); two threads at once, then the main thread.  Every verdict, checksum, copied count and
     application byte is checked against the oracle inside the program."""
     r = subprocess.run([_bin("host_recv_caller"), "2"], capture_output=True, text=True, timeout=600)
     out = r.stdout
@@ -124,8 +124,9 @@ def test_native_host_receive_path_matches_oracle(cuda):
     lines = [ln for ln in out.splitlines() if ln.startswith(("headers ", "copy_to_app ", "invalid", "empty",
                                                                 "nothing"))]
     assert lines and all(ln.endswith(" ok") for ln in lines)
-    # 3 shapes x 2 modes x 2 rings x 2 orders x (headers + copy) on 2 threads + main, + 4 edge lines
-    assert len(lines) == 3 * 2 * 2 * 2 * 2 * (2 + 1) + 4
+    # 3 shapes x 3 delivery modes (CRC, SUM, checksumming off) x 2 rings x 2 orders x (headers + copy) on 2
+    # threads + main, + 4 edge lines
+    assert len(lines) == 3 * 3 * 2 * 2 * 2 * (2 + 1) + 4
     # the batches really held corrupt fragments of every kind
     assert any(" nbad 0 " not in ln and ln.startswith("headers ") for ln in lines)
     assert any(ln.startswith("copy_to_app ") and " nbad 0 " not in ln for ln in lines)
@@ -137,7 +138,10 @@ def test_native_host_typemap_chains_match_reference(cuda, tmp_path):
     reference's 150 chain fixtures (values computed by the compiled MemFunctions.cc, passed to the program
     as text), strided-vector typemaps gathered and scattered (8 B .. 4 KiB elements), random typemaps with
     checksum-only and csumlen > copylen pieces and CRC starting registers; both modes, pinned and pageable
-    buffers, two threads at once, then the main thread.  Every checksum and destination byte is checked."""
+    buffers, two threads at once, then the main thread.  Every checksum and destination byte is checked.
+    Then lampi_host_chain_copy_to_app_batch (CopyToApp's non-contiguous branch, ref BaseDesc.cc:72-163,
+    :326-340): random received fragments scattered into typemap pieces, ~25% corrupted expected values,
+    fragments without pieces, CRC / SUM / checksumming off -- every verdict, checksum and byte."""
     import json
 
     with open(os.path.join(HERE, "golden", "fixtures.json")) as f:
@@ -152,8 +156,11 @@ def test_native_host_typemap_chains_match_reference(cuda, tmp_path):
     assert r.returncode == 0, out[-4000:] + r.stderr[-2000:]
     assert out.strip().endswith("bad 0 done"), out[-2000:]
     assert f"fixture_cases {len(cases)}" in out and len(cases) == 150
-    lines = [ln for ln in out.splitlines() if ln.startswith(("fixtures ", "vector_", "random ", "invalid", "fragments"))]
+    lines = [ln for ln in out.splitlines()
+             if ln.startswith(("fixtures ", "vector_", "random ", "invalid", "fragments", "deliver"))]
     assert lines and all(ln.endswith(" ok") for ln in lines)
-    # per thread: 2 x 2 fixture batches, 6 shapes x 2 buffers x 2 modes x (gather + scatter), 6 x 2 random
-    assert len(lines) == 3 * (4 + 6 * 2 * 2 * 2 + 6 * 2) + 2
+    # per thread: 2 x 2 fixture batches, 6 shapes x 2 buffers x 2 modes x (gather + scatter), 6 x 2 random,
+    # 4 x 3 deliveries; + 3 edge lines
+    assert len(lines) == 3 * (4 + 6 * 2 * 2 * 2 + 6 * 2 + 4 * 3) + 3
+    assert any(ln.startswith("deliver ") and " bad 0 " not in ln for ln in lines)
     assert "pinned_after_release 0 scratch_after_release 0" in out

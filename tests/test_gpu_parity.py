@@ -72,6 +72,30 @@ def test_regular_batches_every_schedule(cuda, oracle, L, mode):
         assert np.array_equal(got, want), (L, n, mode)
 
 
+@pytest.mark.parametrize("L", [1, 3, 15, 16, 17, 63, 64, 1976, 4095, 4096, 4097, 16384, 65456, (1 << 20) + 48])
+def test_sum_messages_short_lived_workgroups(cuda, oracle, L):
+    """lampi_msg_csum SUM of messages of >= 256 fragments (one fragment per short-lived 128-thread workgroup,
+    round 5): lengths around the 16-byte chunk, the 4 KiB row and large fragments, a ragged last fragment, a
+    message start at every offset 0..15 of a 16-byte line; every fragment vs the oracle."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(L)
+    nf = 256 + int(rng.integers(0, 40))
+    for shift in (0, 1, 7, 13):
+        msg_len = (nf - 1) * L + int(rng.integers(1, L + 1))
+        raw = torch.empty(msg_len + 16, dtype=torch.uint8, device=cuda)
+        dv.fill_stream(raw, seed=L + shift)
+        buf = raw[shift:shift + msg_len]
+        got = dv.as_u32(dv.msg_csum(buf, L, mode=dv.SUM32))
+        host = buf.cpu().numpy()
+        offs = np.arange(nf, dtype=np.uint64) * L
+        lens = np.minimum(L, msg_len - offs.astype(np.int64)).astype(np.uint32)
+        want = oracle.desc_batch(host, offs, lens, None, 1)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (L, shift, bad[:8].tolist())
+
+
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 def test_message_with_short_last_fragment(cuda, oracle, mode):
     import torch

@@ -48,7 +48,7 @@ def _batch(rng, n, lengths=None):
 def _run_case(cuda, oracle, mode, lengths, app_len, rng, app_misalign=True, corrupt_frac=0.1, rows_hint=0):
     import torch
 
-    from oracle.oracle import copy_to_app
+    from oracle.oracle import copy_to_app, copy_to_app_nochecksum
 
     dv = _dv()
     usecrc = mode == dv.CRC32
@@ -72,7 +72,8 @@ def _run_case(cuda, oracle, mode, lengths, app_len, rng, app_misalign=True, corr
         if rng.random() < corrupt_frac:
             e = true | 0xA4A4
         exp[i] = e
-        r = copy_to_app(oracle, frag, L, int(app_len[i]), e, usecrc)
+        r = (copy_to_app_nochecksum(frag, L, int(app_len[i])) if mode == dv.NONE else
+             copy_to_app(oracle, frag, L, int(app_len[i]), e, usecrc))
         ref.append(r)
         bad_want[i] = r[0] == -1
     hv = host.copy()
@@ -163,6 +164,33 @@ def test_copy_to_app_row_groups(cuda, oracle, rows_hint, mode):
     assert bad.any() and not bad.all()
 
 
+@pytest.mark.parametrize("rows_hint", [0, 16])
+def test_copy_to_app_checksum_off(cuda, oracle, rows_hint):
+    """LAMPI_CSUM_NONE (doChecksum == false, ref src/path/gm/recvFrag.h:178-181, :231-232): the delivered
+    bytes are exactly min(length, AppBufferLen) of every fragment (also those whose header checksum is
+    corrupt), the checksum output 0, every fragment DataOK -- the edge lengths, a random batch, GM payloads
+    (with and without the rows hint) and IB-sized payloads (the learned wave-per-fragment schedule)."""
+    dv = _dv()
+    rng = np.random.default_rng(77 + rows_hint)
+    L = [0, 1, 3, 4, 5, 63, 64, 65, 1975, 1976, 2048, 4095, 4096, 4097, 65456, 200003]
+    lengths, app_len = [], []
+    for ln in L:
+        for a in sorted({-1, 0, 1, ln - 1, ln, ln + 1, 1 << 33}):
+            lengths.append(ln)
+            app_len.append(a)
+    bad = _run_case(cuda, oracle, dv.NONE, np.array(lengths), np.array(app_len), rng, corrupt_frac=0.5,
+                    rows_hint=rows_hint)
+    assert not bad.any()
+    lengths, app_len = _batch(rng, 2000)
+    _run_case(cuda, oracle, dv.NONE, lengths, app_len, rng, corrupt_frac=0.3, rows_hint=rows_hint)
+    n = 600
+    for _ in range(3):  # the same shape again: the learned schedule takes over
+        _run_case(cuda, oracle, dv.NONE, np.full(n, 65456), np.full(n, 1 << 20), rng, corrupt_frac=0.3,
+                  rows_hint=rows_hint)
+        _run_case(cuda, oracle, dv.NONE, np.full(n, 1976), np.full(n, 1 << 20), rng, corrupt_frac=0.3,
+                  rows_hint=rows_hint)
+
+
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 def test_copy_to_app_uniform_gm_slots(cuda, oracle, mode):
     """The common case: 4 KiB fragments in 72-byte-header slots, posted buffer large enough."""
@@ -182,6 +210,8 @@ def test_copy_to_app_rejects_bad_args(cuda):
     b = torch.zeros(64, dtype=torch.int64, device=cuda)
     p = b.data_ptr()
     assert lib().lampi_copy_to_app_batch(p, 1, p, 4, p, p, p, p, 7, None) != 0          # bad mode
+    assert lib().lampi_copy_to_app_batch(p, 1, None, 4, p, p, p, p, 0, None) != 0       # CRC needs expected
+    assert lib().lampi_copy_to_app_batch(p, 0, None, 4, None, None, None, p, 2, None) == 0  # NONE: none needed
     assert lib().lampi_copy_to_app_batch(p, 1, p + 2, 4, p, p, p, p, 0, None) != 0      # misaligned expected
     assert lib().lampi_copy_to_app_batch(p, 1, p, 6, p, p, p, p, 0, None) != 0          # misaligned stride
     assert lib().lampi_copy_to_app_batch(p, 0, None, 4, None, None, None, p, 0, None) == 0  # empty batch

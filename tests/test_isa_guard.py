@@ -5,7 +5,8 @@ frag_csum.hip (built with the library's flags by lampi_amd/csrc/Makefile) and fa
 instruction reads, copies or overwrites the destination registers of an asm-issued load before
 the asm wait that names them (or a full vmcnt(0)).  tools/isa_guard/broken_ring.hip holds the
 two round-1 failure shapes on purpose -- a copy of an in-flight load, and a ring waited by two
-asm statements on two branches (the pre-fix wait selection) -- and must be flagged.
+asm statements on two branches (the pre-fix wait selection) -- and round 4's ring drain (a refill
+skipped under a branch, its wait chosen on two branches); all must be flagged.
 """
 import os
 import subprocess
@@ -51,3 +52,4 @@ def test_guard_flags_the_round1_failure_shapes(tmp_path):
     kernels = {k for k, *_ in bad}
     assert any("copy_before_wait" in k for k in kernels), bad
     assert any("two_branch_waits" in k for k in kernels), bad
+    assert any("refill_skipped" in k for k in kernels), bad  # round 4's ring drain
