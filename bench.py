@@ -115,6 +115,9 @@ def parse():
                     help="fused copy + checksum batch (lampi_frag_bcopy_batch) on the config B shape")
     ap.add_argument("--recv", action="store_true",
                     help="batched receive step (lampi_copy_to_app_batch) on the config B shape in GM slots")
+    ap.add_argument("--alternate", action="store_true",
+                    help="with --recv: one stream alternating GM (65,456 B) and IB (1,976 B) receive batches, each "
+                         "from its own descriptor array, beside each alone (learned shapes per array)")
     ap.add_argument("--rows-hint", type=int, default=0,
                     help="LAMPI_CSUM_ROWS_HINT(r) for the descriptor batches of --desc, --bcopy and --recv: the "
                          "fragments' 4 KiB rows (e.g. 16 for GM's 65,456-byte payloads); 0 = none")
@@ -1070,6 +1073,92 @@ def run_recv(args):
         "cpu_baseline": None}), flush=True)
 
 
+def run_recv_alternate(args):
+    """The receive step on one stream that alternates two shapes: GM batches (16,384 x
+    65,456-byte payloads in 64 KiB-ish slots, 1 GiB) and IB batches (262,144 x 1,976 bytes, 0.5 GiB), each from
+    its own descriptor array.  The library learns a batch's shape per descriptor array (round 5), so each
+    should keep the schedule it gets alone.  Reported: each shape alone without a hint (learned), GM with
+    LAMPI_CSUM_ROWS_HINT(16), and each inside the alternating sequence (HIP events around every call);
+    roofline bytes = payload read + written."""
+    import numpy as np
+    import torch
+
+    from lampi_amd import device as dv
+
+    rank, world, _ = dist_setup(args)
+    if world != 1:
+        raise SystemExit("--recv --alternate is a single-GPU measurement")
+    mode = dv.CRC32 if args.mode == "crc" else dv.SUM32
+
+    def build(n, L, seed):
+        stride = 72 + L + 8
+        src = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+        dv.fill_stream_frags(src, n, L, seed)
+        nic = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+        sent = dv.msg_bcopy(src, L, nic[72:], dst_stride=stride, mode=mode)
+        nic.view(n, stride)[:, 64:68].copy_(sent.view(torch.uint8).view(n, 4))
+        del src
+        app = torch.zeros(n * L, dtype=torch.uint8, device="cuda")
+        offs = np.arange(n, dtype=np.uint64)
+        descs = dv.make_recv_descs(nic, offs * np.uint64(stride) + np.uint64(72), app, offs * np.uint64(L),
+                                   np.full(n, L), np.full(n, 1 << 40, dtype=np.int64))
+        return dict(n=n, L=L, stride=stride, nic=nic, app=app, descs=descs)
+
+    gm, ib = build(16384, 65456, 7), build(262144, 1976, 8)
+
+    def call(b, hint=0):
+        return dv.copy_to_app_batch(b["descs"], b["nic"], expected_stride=b["stride"], expected_offset=64, n=b["n"],
+                                    mode=mode, rows_hint=hint)
+
+    stream = torch.cuda.current_stream()
+
+    def alone(fn):
+        _warm(fn, args.warmup)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.steps / 1e3
+
+    t_gm_hint = alone(lambda: call(gm, 16))
+    t_gm = alone(lambda: call(gm))
+    t_ib = alone(lambda: call(ib))
+    _warm(lambda: (call(gm), call(ib)), args.warmup)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
+    ev[0].record(stream)
+    for i in range(args.steps):
+        call(gm)
+        ev[2 * i + 1].record(stream)
+        call(ib)
+        ev[2 * i + 2].record(stream)
+    torch.cuda.synchronize()
+    a_gm = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.steps)) / args.steps / 1e3
+    a_ib = sum(ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.steps)) / args.steps / 1e3
+    ok = True
+    for b in (gm, ib):
+        copied, csum, mask, nbad = call(b)
+        ok = ok and int(nbad.item()) == 0 and bool((copied == b["L"]).all().item()) and bool(
+            torch.equal(b["app"].view(b["n"], b["L"]), b["nic"].view(b["n"], b["stride"])[:, 72:72 + b["L"]]))
+    frac = lambda b, t: round(2.0 * b["n"] * b["L"] / t / 1e9 / HBM_PEAK_GBS, 4)  # noqa: E731
+    print(json.dumps({
+        "metric": "device-resident batched receive step on a stream alternating GM and IB batches; % of HBM roofline",
+        "value": round((gm["n"] * gm["L"] + ib["n"] * ib["L"]) / GIB / (a_gm + a_ib), 2), "unit": "GiB/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "dtype": "u8",
+        "data": "synthetic: splitmix64 streams seeds 7 / 8 in GM / IB receive slots (72-byte header + payload)",
+        "config": {"workload": "alternating lampi_copy_to_app_batch calls on one stream: 16,384 x 65,456 B (GM) and "
+                               "262,144 x 1,976 B (IB), separate descriptor arrays, no hint",
+                   "mode": args.mode},
+        "gm": {"alone_hint16_frac": frac(gm, t_gm_hint), "alone_learned_frac": frac(gm, t_gm),
+               "alternating_frac": frac(gm, a_gm), "alternating_ms": round(a_gm * 1e3, 4)},
+        "ib": {"alone_learned_frac": frac(ib, t_ib), "alternating_frac": frac(ib, a_ib),
+               "alternating_ms": round(a_ib * 1e3, 4)},
+        "parity": {"check": "nbad == 0, every fragment fully copied, app == slot payloads (checksums verified "
+                            "against the send side's, stamped by lampi_msg_bcopy)", "ok": bool(ok)},
+        "cpu_baseline": None}), flush=True)
+
+
 def run_latency(args):
     """Small batches: per-call time of lampi_frag_csum_batch over n 4 KiB descriptor
     fragments, three ways -- stream-ordered back-to-back calls (device time per call, HIP events),
@@ -1194,6 +1283,9 @@ def main():
         return
     if args.bcopy:
         run_bcopy(args)
+        return
+    if args.recv and args.alternate:
+        run_recv_alternate(args)
         return
     if args.recv:
         run_recv(args)

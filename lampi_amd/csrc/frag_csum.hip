@@ -4335,14 +4335,24 @@ struct BatchShape {
     uint32_t pad[3];
 };
 constexpr int kShapeKinds = 3;  // read-only descriptors, copy descriptors, receive descriptors
+constexpr int kShapeSlots = 8;  // shape records per (thread, device, stream): descriptor arrays remembered
 constexpr int64_t kLeftBytes = 256;
 
 struct ScratchTable {
     struct Slot {
         void *p = nullptr;
         size_t cap = 0;
-        BatchShape *shape[kShapeKinds] = {};  // host-mapped (coherent), lazily allocated
-        uint32_t calls[kShapeKinds] = {};
+        // learned batch shapes, one record per (entry-point kind, descriptor array): a stream that
+        // alternates batches from different arrays (GM's and IB's receive rings) keeps one shape each
+        struct ShapeRec {
+            const void *key = nullptr;  // the batch's descriptor array
+            int kind = -1;
+            BatchShape *rec = nullptr;  // host-mapped (coherent), lazily allocated; reused on eviction
+            uint32_t calls = 0;
+            uint64_t used = 0;          // the slot's call count at its last use (least recently used: evicted)
+        };
+        ShapeRec shapes[kShapeSlots];
+        uint64_t shape_tick = 0;
         uint32_t *left = nullptr;  // the pair kernel's two leftover counters (device, zeroed at creation)
         uint32_t left_calls = 0;
         bool pair_broken = false;  // the counters could not be re-zeroed after a failed launch
@@ -4373,11 +4383,11 @@ struct ScratchTable {
                 (void)hipFree(it->second.left);
                 g_scratch_bytes.fetch_sub(kLeftBytes, std::memory_order_relaxed);
             }
-            for (BatchShape *&b : it->second.shape)
-                if (b) {
-                    (void)hipHostFree(b);
+            for (auto &r : it->second.shapes)
+                if (r.rec) {
+                    (void)hipHostFree(r.rec);
                     g_scratch_bytes.fetch_sub((int64_t)sizeof(BatchShape), std::memory_order_relaxed);
-                    b = nullptr;
+                    r.rec = nullptr;
                 }
             it = slots.erase(it);
         }
@@ -4552,7 +4562,29 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return rows_hint;
     ScratchTable::Slot &slot = t_scratch.slots[{dev, s}];
-    BatchShape *&rec = slot.shape[kind];
+    // this batch's record: the one of its descriptor array, else the least recently used one, reset
+    static const bool keyed = [] {  // (A/B knob LAMPI_SHAPES_UNKEYED=1: one record per kind, as in round 4)
+        const char *e = std::getenv("LAMPI_SHAPES_UNKEYED");
+        return !(e && e[0] == '1');
+    }();
+    const void *key = keyed ? (const void *)src.d : nullptr;
+    ScratchTable::Slot::ShapeRec *sr = nullptr, *lru = &slot.shapes[0];
+    for (auto &r : slot.shapes) {
+        if (r.key == key && r.kind == kind) {
+            sr = &r;
+            break;
+        }
+        if (r.used < lru->used) lru = &r;
+    }
+    if (!sr) {
+        sr = lru;
+        sr->key = key;
+        sr->kind = kind;
+        sr->calls = 0;
+        if (sr->rec) std::memset(sr->rec, 0, sizeof(BatchShape));  // (a census still in flight only costs speed)
+    }
+    sr->used = ++slot.shape_tick;
+    BatchShape *&rec = sr->rec;
     if (!rec) {
         void *p = nullptr;
         if (hipHostMalloc(&p, sizeof(BatchShape), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
@@ -4567,8 +4599,9 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     const volatile BatchShape *v = rec;
     uint32_t W = rows_hint;
     const uint32_t q0 = v->seq;
+    std::atomic_thread_fence(std::memory_order_acquire);  // the fields are read after the first seq ...
     const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf;
-    std::atomic_thread_fence(std::memory_order_acquire);
+    std::atomic_thread_fence(std::memory_order_acquire);  // ... and before the second (a seqlock read)
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= min_rows && rmax <= 2 * rmin) W = rmax;
         if (one_row && rmin == 1u && rmax == 1u) *one_row = true;  // every sampled fragment one row (17 B-4 KiB)
@@ -4582,7 +4615,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
             }
         }
     }
-    const uint32_t c = slot.calls[kind]++;
+    const uint32_t c = sr->calls++;
     if (c % kShapeEvery == 0) {
         void *dp = nullptr;
         if (hipHostGetDevicePointer(&dp, rec, 0) == hipSuccess) {

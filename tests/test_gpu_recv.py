@@ -217,3 +217,53 @@ def test_copy_to_app_rejects_bad_args(cuda):
     assert lib().lampi_copy_to_app_batch(p, 0, None, 4, None, None, None, p, 0, None) == 0  # empty batch
     torch.cuda.synchronize()
     assert dv is not None
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_copy_to_app_alternating_shapes(cuda, oracle, mode):
+    """One stream alternating GM receive batches (65,456-byte payloads) and IB ones (1,976 bytes), each from
+    its own descriptor array, 48 calls: the learned shapes are kept per descriptor array (round 5), so each
+    batch runs its own schedule (row groups / two per wave); every call's copies, checksums and verdicts
+    against the oracle (results never depend on the schedule)."""
+    import torch
+
+    from oracle.oracle import copy_to_app
+
+    dv = _dv()
+    rng = np.random.default_rng(900 + mode)
+    usecrc = mode == dv.CRC32
+
+    def build(n, L):
+        slot = HDR + ((L + 7) // 8) * 8 + 8
+        nic = torch.empty(n * slot + 64, dtype=torch.uint8, device=cuda)
+        dv.fill_stream(nic, seed=int(rng.integers(0, 1 << 30)))
+        host = nic.cpu().numpy()
+        soff = np.arange(n, dtype=np.int64) * slot
+        exp = np.zeros(n, np.uint32)
+        want_copied = np.zeros(n, np.int64)
+        want_csum = np.zeros(n, np.uint32)
+        for i in range(n):
+            frag = host[soff[i] + HDR:soff[i] + HDR + L]
+            true = oracle.uicrc(frag, L) if usecrc else oracle.uicsum(frag, L)[0]
+            exp[i] = true | 0xA4A4 if rng.random() < 0.05 else true
+            host[soff[i] + DCSUM_OFF:soff[i] + DCSUM_OFF + 4] = np.frombuffer(np.uint32(exp[i]).tobytes(), np.uint8)
+            r = copy_to_app(oracle, frag, L, 1 << 30, int(exp[i]), usecrc)
+            want_copied[i], want_csum[i] = r[0], r[1]
+        nic.copy_(torch.from_numpy(host).to(cuda))
+        app = torch.zeros(n * L + 64, dtype=torch.uint8, device=cuda)
+        descs = dv.make_recv_descs(nic, soff + HDR, app, np.arange(n, dtype=np.int64) * L, np.full(n, L),
+                                   np.full(n, 1 << 30, np.int64))
+        return dict(n=n, L=L, slot=slot, nic=nic, app=app, descs=descs, copied=torch.from_numpy(want_copied).to(cuda),
+                    csum=torch.from_numpy(want_csum.view(np.int32)).to(cuda),
+                    payload=nic[:n * slot].view(n, slot)[:, HDR:HDR + L])
+
+    gm, ib = build(600, 65456), build(3000, 1976)
+    for call in range(48):
+        b = gm if call % 2 == 0 else ib
+        b["app"].zero_()
+        copied, csum, mask, nbad = dv.copy_to_app_batch(b["descs"], b["nic"], expected_stride=b["slot"],
+                                                        expected_offset=DCSUM_OFF, n=b["n"], mode=mode)
+        assert torch.equal(copied, b["copied"]), (call, b["L"])
+        assert torch.equal(csum, b["csum"]), (call, b["L"])
+        assert int(nbad.item()) == int((b["copied"] == -1).sum().item())
+        assert torch.equal(b["app"][:b["n"] * b["L"]].view(b["n"], b["L"]), b["payload"]), (call, b["L"])
