@@ -300,12 +300,6 @@ typedef struct lampi_frag_desc {
 int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out,
                           int mode, void *stream);
 
-/* The same results as lampi_frag_csum_batch, computed on the one-wavefront-per-fragment schedule
- * (each wave walks its fragments in 4 KiB rows): the north_star's baseline design, kept beside the
- * default piece-stream kernel, which balances mixed sizes better. */
-int lampi_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode,
-                                   void *stream);
-
 /* As lampi_frag_csum_batch, with checksum i written to (char *)d_out + i*out_stride (d_out and
  * out_stride 4-byte aligned, out_stride >= 4) -- e.g. straight into the dataChecksum field of
  * an array of 72-byte gmHeaderData records: d_out = hdrs + 64, out_stride = 72

@@ -96,7 +96,6 @@ PROTOTYPES = {
     "lampi_bcopy_csum": (c_ulong, [c_void_p, c_void_p, c_ulong, c_ulong, PULONG, PULONG]),
     "lampi_frag_csum64_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_void_p]),
     "lampi_frag_csum_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
-    "lampi_frag_csum_batch_per_wave": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_frag_bcopy_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_msg_bcopy": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, ctypes.c_uint32, c_void_p,
                                        ctypes.c_int, c_void_p]),

@@ -571,8 +571,11 @@ int lampi_diag_stream_timeline(const lampi_frag_desc *d_descs, size_t n, uint32_
     return e != hipSuccess ? -to_int(e) : (int)nwg;
 }
 
-int lampi_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode,
-                                   void *stream) {
+// Internal diagnostic (retired from include/lampi_csum.h in round 5): lampi_frag_csum_batch's
+// results on the north_star's baseline schedule, one wavefront walking each fragment's 4 KiB rows
+// (crc_rows_kernel / sum_rows_kernel) -- kept for bench.py's config C comparison and the parity tests only.
+int lampi_diag_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode,
+                                        void *stream) {
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;
     if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);

@@ -11,7 +11,7 @@ import torch
 
 from ._lib import BY_BYTES, CRC32, CRC_INITIAL_REGISTER, NONE, SUM32, check, lib, rows_hint_bits
 
-__all__ = ["CRC32", "SUM32", "NONE", "chain_copy_to_app_batch", "frag_csum_batch", "frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
+__all__ = ["CRC32", "SUM32", "NONE", "chain_copy_to_app_batch", "frag_csum_batch", "diag_frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
            "make_descs", "make_copy_descs", "as_u32", "chain_csum_batch", "header_csum_batch", "header_check_batch", "check_data_batch",
            "mask_bits", "make_recv_descs", "copy_to_app_batch"]
 
@@ -118,9 +118,17 @@ def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32
     return out
 
 
-def frag_csum_batch_per_wave(descs: torch.Tensor, n: int | None = None, mode: int = CRC32,
-                             out: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
-    """lampi_frag_csum_batch on the one-wavefront-per-fragment schedule (same results)."""
+def diag_frag_csum_batch_per_wave(descs: torch.Tensor, n: int | None = None, mode: int = CRC32,
+                                  out: torch.Tensor | None = None,
+                                  stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """lampi_frag_csum_batch's results on the one-wavefront-per-fragment schedule: the internal diagnostic
+    lampi_diag_frag_csum_batch_per_wave (not part of include/lampi_csum.h since round 5; bench.py's config C
+    comparison and the parity tests)."""
+    import ctypes
+
+    fn = lib().lampi_diag_frag_csum_batch_per_wave
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 16 if n is None else int(n)
     if out is None:
@@ -128,8 +136,8 @@ def frag_csum_batch_per_wave(descs: torch.Tensor, n: int | None = None, mode: in
     _require_cuda(out, "out")
     if out.numel() < count:
         raise ValueError("out is too small")
-    check(lib().lampi_frag_csum_batch_per_wave(descs.data_ptr(), count, out.data_ptr(), mode, _stream_handle(stream)),
-          "lampi_frag_csum_batch_per_wave")
+    check(fn(descs.data_ptr(), count, out.data_ptr(), mode, _stream_handle(stream)),
+          "lampi_diag_frag_csum_batch_per_wave")
     return out
 
 

@@ -199,7 +199,7 @@ def test_descriptor_batch_edges_and_alignment(cuda, oracle, mode):
     want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
     by_bytes = lambda d, mode: dv.frag_csum_batch(d, mode=mode, by_bytes=True)  # noqa: E731
     # piece streams (count split, byte plan) / one wave per fragment
-    for name, fn in (("count", dv.frag_csum_batch), ("bytes", by_bytes), ("per_wave", dv.frag_csum_batch_per_wave)):
+    for name, fn in (("count", dv.frag_csum_batch), ("bytes", by_bytes), ("per_wave", dv.diag_frag_csum_batch_per_wave)):
         got = dv.as_u32(fn(descs, mode=mode))
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (name, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
@@ -284,7 +284,7 @@ def test_descriptor_batch_fragments_across_chains(cuda, oracle, case, mode):
     want = oracle.desc_batch(host, offs, lens, parts.astype(np.uint32) if mode == 0 else None, mode)
     by_bytes = lambda d, mode: dv.frag_csum_batch(d, mode=mode, by_bytes=True)  # noqa: E731
     # piece streams (count split, byte plan) / one wave per fragment
-    for name, fn in (("count", dv.frag_csum_batch), ("bytes", by_bytes), ("per_wave", dv.frag_csum_batch_per_wave)):
+    for name, fn in (("count", dv.frag_csum_batch), ("bytes", by_bytes), ("per_wave", dv.diag_frag_csum_batch_per_wave)):
         got = dv.as_u32(fn(descs, mode=mode))
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (name, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]])
@@ -746,8 +746,8 @@ def test_config_c_mixed_sizes_full_digest(cuda, oracle):
     s = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.SUM32))
     assert (int(np.sum(s, dtype=np.uint64) & 0xFFFFFFFF), digest(s)[1]) == (gold["sum_total"], gold["sum_wsum"])
     # the one-wavefront-per-fragment schedule on the same batch (bench.py --config C reports both)
-    assert np.array_equal(dv.as_u32(dv.frag_csum_batch_per_wave(descs, mode=dv.CRC32)), crc)
-    assert np.array_equal(dv.as_u32(dv.frag_csum_batch_per_wave(descs, mode=dv.SUM32)), s)
+    assert np.array_equal(dv.as_u32(dv.diag_frag_csum_batch_per_wave(descs, mode=dv.CRC32)), crc)
+    assert np.array_equal(dv.as_u32(dv.diag_frag_csum_batch_per_wave(descs, mode=dv.SUM32)), s)
     del buf
     torch.cuda.empty_cache()
 

@@ -23,7 +23,7 @@ import json
 import os
 
 
-def per_dispatch(root, kernel_substr, skip=0, take=None):
+def per_dispatch(root, kernel_substr, skip=0, take=None, last=None):
     files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
     if os.path.isfile(root):
         files = [root]
@@ -34,6 +34,8 @@ def per_dispatch(root, kernel_substr, skip=0, take=None):
                 continue
             vals[(f, int(r["Dispatch_Id"]))][r["Counter_Name"]] += float(r["Counter_Value"])
     out = [vals[k] for k in sorted(vals)][skip:]
+    if last:
+        out = out[-last:]
     return out if take is None else out[:take]
 
 
@@ -44,13 +46,14 @@ def main():
     ap.add_argument("--write", help="WRITE_SIZE pass (fused copies: traffic = read + written bytes)")
     ap.add_argument("--skip", type=int, default=0)
     ap.add_argument("--take", type=int, default=None)
+    ap.add_argument("--last", type=int, default=None, help="only the last N matching dispatches (after warm-ups)")
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--key", required=True)
     ap.add_argument("--algorithmic-bytes", type=int, required=True)
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--source", default="")
     a = ap.parse_args()
-    fd = per_dispatch(a.fetch, a.kernel, a.skip, a.take)
+    fd = per_dispatch(a.fetch, a.kernel, a.skip, a.take, a.last)
     if not fd:
         raise SystemExit(f"no dispatches of {a.kernel} in {a.fetch}")
     fetch_kb = sum(d["FETCH_SIZE"] for d in fd) / len(fd)
@@ -64,7 +67,7 @@ def main():
         "source": a.source,
     }
     if a.write:
-        wd = per_dispatch(a.write, a.kernel, a.skip, a.take)
+        wd = per_dispatch(a.write, a.kernel, a.skip, a.take, a.last)
         if not wd:
             raise SystemExit(f"no dispatches of {a.kernel} in {a.write}")
         write_kb = sum(d["WRITE_SIZE"] for d in wd) / len(wd)
