@@ -4334,7 +4334,6 @@ struct BatchShape {
     uint32_t nhalf;    // how many were at most 2 KiB
     uint32_t pad[3];
 };
-constexpr int kShapeKinds = 3;  // read-only descriptors, copy descriptors, receive descriptors
 constexpr int kShapeSlots = 8;  // shape records per (thread, device, stream): descriptor arrays remembered
 constexpr int64_t kLeftBytes = 256;
 
@@ -4978,28 +4977,56 @@ hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t 
     return hipGetLastError();
 }
 
+// Read-only SUM batches of fragments of R > 1 rows (descriptors: the caller's or learned hint; messages:
+// the fragment length): 1 = one fragment per short-lived 128-thread workgroup (sum_copy_wg_kernel), W > 1 =
+// W row groups per fragment joined by sum_group_join_kernel, ~0u = neither (the row segments).
+//  - R <= 8 in batches of >= 4096 fragments: one per workgroup.  Same box, interleaved
+//    (profiles/r05/sum_ro_sched_ab.txt), against the piece streams / eight one-row groups before: 8 KiB
+//    77.5 -> 88.8%, 16 KiB 76.7 -> 89.1%, 32 KiB 77.4 -> 88.0%.
+//  - otherwise min(R, 8) groups, doubled while each group keeps >= 2 rows and the launch has under 65,536
+//    workgroups: 1 MiB x 1,024 72.9 -> 83.9%, 2 MiB x 1,024 74.6 -> 83+%, 4 MiB x 2,048 81.1 -> 87.0%,
+//    16 MiB x 256 77.1 -> 84.6%; GM's 65,456 B and 1 MiB x 4,096 unchanged (86.5, 85%).  One workgroup
+//    per fragment above 8 rows loses wherever the grid needs more than one round of workgroups (512 KiB
+//    x 8,192 86.9 -> 75.4%, GM 86.7 -> 84.8%).
+//  - fragments over 256 rows were row segments before (2 MiB x 4,096 76.6 -> 84.8% as groups).
+// A/B knobs: LAMPI_SUM_RO_ONEWG = fewest fragments for one per workgroup (0: never), LAMPI_SUM_RO_WGS = the
+// workgroup target, LAMPI_SUM_RO_GROUPS=0 = the round-4 schedules (groups of <= 8 up to 256 rows, segments above).
+static uint32_t sum_ro_groups(size_t n, uint32_t R) {
+    static const size_t onewg = [] {
+        const char *e = std::getenv("LAMPI_SUM_RO_ONEWG");
+        return e ? (size_t)std::atoll(e) : (size_t)4096;
+    }();
+    static const size_t wgs = [] {
+        const char *e = std::getenv("LAMPI_SUM_RO_WGS");
+        return e ? (size_t)std::atoll(e) : (size_t)65536;
+    }();
+    static const bool r5 = [] {
+        const char *e = std::getenv("LAMPI_SUM_RO_GROUPS");
+        return !(e && e[0] == '0');
+    }();
+    if (!r5) return R <= 256u && sum_groups(n, min(R, 8u)) > 1 ? min(R, 8u) : 0xFFFFFFFFu;
+    if (onewg && R <= 8u && n >= onewg) return 1u;
+    uint32_t W = min(R, 8u);
+    while (W < R / 2 && (size_t)n * W < wgs) W *= 2;
+    W = sum_groups(n, W);
+    return W > 1 ? W : 0xFFFFFFFFu;
+}
+
 hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
                            hipStream_t s, bool plan, uint32_t rows_hint) {
     (void)grid;
     if (n == 0) return hipSuccess;
     if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
     bool one_row = false;
-    if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, kShapeRows, &one_row);
-    static const bool ro_groups = [] {  // (A/B knob)
-        const char *e = std::getenv("LAMPI_SUM_RO_GROUPS");
-        return !(e && e[0] == '0');
-    }();
-    // row groups on short-lived workgroups, at most eight per fragment (profiles/r04/sum_ro_groups_ab.txt: 16 KiB
-    // with hint 4 73.7 -> 75.6%, 32 KiB learned 73.3 -> 76.1%; sum_group_cap_ab.txt: GM's 65,456-byte fragments
-    // as eight groups of two rows 74 -> 86.4%, as sixteen of one 71.6%, four of four 84.2%; 1 MiB as eight of
-    // 32 rows 69.6 -> 73%, sum_ro_groups2.txt); fragments over 256 rows keep the row segments (A/B knob
-    // LAMPI_SUM_RO_MAXROWS)
-    static const uint32_t ro_max = [] {
-        const char *e = std::getenv("LAMPI_SUM_RO_MAXROWS");
-        return e ? (uint32_t)std::atoi(e) : 256u;
-    }();
-    if (img && ro_groups && rows_hint > 1 && rows_hint <= ro_max && sum_groups(n, min(rows_hint, 8u)) > 1)
-        return launch_sum_copy_groups(DescSource{d}, n, out, s, min(rows_hint, 8u));
+    if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, 2u, &one_row);
+    if (img && rows_hint > 1) {
+        const uint32_t W = sum_ro_groups(n, rows_hint);
+        if (W <= 1) {
+            launch_sum_copy(DescSource{d}, n, out, s);
+            return hipGetLastError();
+        }
+        if (W < 0xFFFFFFFFu) return launch_sum_copy_groups(DescSource{d}, n, out, s, W);
+    }
     if (img && rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<true, kSumWv, kSumCap>(d, n, out, img, s, rows_hint);
     // batches of one-row fragments (the census: every sampled fragment 1-4096 bytes) on short-lived 128-thread
@@ -5046,7 +5073,20 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
         const char *e = std::getenv("LAMPI_SUM_MSG_MAX");
         return e ? (size_t)std::atoll(e) : ~(size_t)0;
     }();
-    if (msg_wg && frag_len <= msg_max && n >= 256) {
+    const uint32_t R = (uint32_t)std::min<size_t>((frag_len + kRowBytes - 1) / kRowBytes, 0xFFFFFFFFu);
+    if (msg_wg && frag_len <= msg_max && n >= 256 && R > 1 && img) {
+        // fragments over one row: the read-only descriptors' schedule (sum_ro_groups), as one workgroup
+        // per fragment in batches under 4,096 fragments ran a single round of too few workgroups (1 MiB x 1,024
+        // 74.6 -> 46.7%, profiles/r05/sum_ro_sched_ab.txt)
+        const uint32_t W = sum_ro_groups(n, R);
+        const MsgSource src{base, msg_len, frag_len, 0u};
+        if (W <= 1) {
+            launch_sum_copy(src, n, out, s);
+            return hipGetLastError();
+        }
+        if (W < 0xFFFFFFFFu) return launch_sum_copy_groups(src, n, out, s, W);
+    }
+    if (msg_wg && frag_len <= msg_max && n >= 256 && R <= 1) {
         hipLaunchKernelGGL(sum_copy_wg_kernel<MsgSource>,
                            dim3((unsigned)std::min<size_t>((n + msg_wg - 1) / msg_wg, kMaxWgGrid)), dim3(kSumWgThreads), 0,
                            s, MsgSource{base, msg_len, frag_len, 0u}, n, out);

@@ -96,6 +96,40 @@ def test_sum_messages_short_lived_workgroups(cuda, oracle, L):
         assert bad.size == 0, (L, shift, bad[:8].tolist())
 
 
+@pytest.mark.parametrize("L,nf", [(4097, 4100), (16384, 4096), (32767, 4111), (36864, 4096), (16384, 300),
+                                  (65456, 700), ((1 << 20) + 48, 300), (3 << 20, 40)])
+def test_sum_multirow_schedules(cuda, oracle, L, nf):
+    """Read-only SUM of fragments over one 4 KiB row (sum_ro_groups, round 5): 2-8 rows in batches of
+    >= 4,096 one per short-lived workgroup; otherwise row groups widened until the launch has 65,536
+    workgroups (groups of >= 2 rows).  Messages (ragged last fragment, odd start) and descriptors at random
+    byte offsets with the caller's rows hint; every fragment vs the oracle."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(L + nf)
+    msg_len = (nf - 1) * L + int(rng.integers(1, L + 1))
+    raw = torch.empty(msg_len + 16, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(raw, seed=L ^ nf)
+    buf = raw[5:5 + msg_len]
+    host = buf.cpu().numpy()
+    offs = np.arange(nf, dtype=np.uint64) * L
+    lens = np.minimum(L, msg_len - offs.astype(np.int64)).astype(np.uint64)
+    want = oracle.desc_batch(host, offs, lens.astype(np.uint32), None, 1)
+    got = dv.as_u32(dv.msg_csum(buf, L, mode=dv.SUM32))
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, ("msg", L, nf, bad[:8].tolist())
+    # descriptors: the same fragments shuffled, lengths trimmed by up to 15 bytes, the caller's hint
+    perm = rng.permutation(nf)
+    offs2, lens2 = offs[perm], lens[perm]
+    lens2 = lens2 - np.minimum(lens2, rng.integers(0, 16, size=nf).astype(np.uint64))
+    descs = dv.make_descs(buf, offs2, lens2, np.zeros(nf, np.uint64))
+    want2 = oracle.desc_batch(host, offs2, lens2.astype(np.uint32), None, 1)
+    rows = (L + 4095) // 4096
+    got2 = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.SUM32, rows_hint=rows))
+    bad = np.nonzero(got2 != want2)[0]
+    assert bad.size == 0, ("desc", L, nf, bad[:8].tolist())
+
+
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 def test_message_with_short_last_fragment(cuda, oracle, mode):
     import torch
