@@ -499,19 +499,6 @@ __device__ __forceinline__ void issue_row(gbyte *p, Row &r) {
         : "memory");
 }
 
-// the same four chunks through a raw buffer descriptor rs (SGPRs) at the byte offsets o[0..3]
-// (offsets of padding before a fragment's start wrap to huge values: out of range, read as zeros)
-__device__ __forceinline__ void issue_row_buf(const u32x4 &rs, const uint32_t (&o)[4], Row &r) {
-    asm volatile(
-        "buffer_load_dwordx4 %0, %4, %8, 0 offen\n\t"
-        "buffer_load_dwordx4 %1, %5, %8, 0 offen\n\t"
-        "buffer_load_dwordx4 %2, %6, %8, 0 offen\n\t"
-        "buffer_load_dwordx4 %3, %7, %8, 0 offen"
-        : "=&v"(r.q[0]), "=&v"(r.q[1]), "=&v"(r.q[2]), "=&v"(r.q[3])
-        : "v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "s"(rs)
-        : "memory");
-}
-
 template <int N>
 __device__ __forceinline__ void wait_row(Row &r) {
     asm volatile("s_waitcnt vmcnt(%4) ; lampi-wait %0 %1 %2 %3" : "+v"(r.q[0]), "+v"(r.q[1]), "+v"(r.q[2]), "+v"(r.q[3]) : "n"(N) : "memory");
@@ -3182,25 +3169,18 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // 79.6-79.7%, 16 KiB fragments 79.1-79.2 -> 78.5%; profiles/r02_sum_regular/).
 // kWv: waves per workgroup (the table builders use the first 256 threads); kCap > 0 asks the
 // compiler for that many waves per SIMD.
-// kFrame (read-only CRC, kV = 1): fragments that are not whole rows -- frag_len a multiple of 16, the
-// message msg_len long (its last fragment may be shorter).  Fragment f is right-aligned in a frame of
-// R = ceil(frag_len / 4096) rows (front padding P_f = 4096R - L_f, a multiple of 16) and read through a
-// buffer descriptor of its L_f bytes (issue_row_buf): the padding reads as zeros -- before the
-// message's start too -- and the register enters as data at frame offset P_f (row 0) instead of as
-// lane 0's starting value.  Every fragment has the same R, so the chains stay in step.
 template <int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
-          bool kSum = false, int kWv = kWaves, int kCap = 0, bool kFrame = false>
+          bool kSum = false, int kWv = kWaves, int kCap = 0>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kCap > 0 ? kCap : 1)))
 crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, size_t frag_len, uint32_t partial,
                    const uint32_t *__restrict__ img, uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
-                   size_t dst_stride, size_t msg_len) {
+                   size_t dst_stride) {
     constexpr int K = kChains;
     static_assert(kWv >= kWaves, "the table builders need 256 threads");
-    static_assert(!kFrame || (!kCopy && !kSum && kV == 1), "frames: read-only CRC in fragment order");
     constexpr int kS = kCoal ? kRowBytes / 4 : 16;  // chunk stride of a lane
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
-    const uint32_t R = (uint32_t)(kFrame ? (frag_len + kRowBytes - 1) / kRowBytes : frag_len / kRowBytes);
+    const uint32_t R = (uint32_t)(frag_len / kRowBytes);
     const uint32_t f0 = uniform(blockIdx.x * kWv * fpw + (threadIdx.x >> 6));
     // fragments of this wave: f0 + kWv*j, j < nfr; processed in groups of K
     const uint32_t nfr = f0 < n ? min(fpw, (n - f0 + kWv - 1) / kWv) : 0u;
@@ -3222,25 +3202,10 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     auto row_ptr = [&](uint32_t f, uint32_t r) -> gbyte * {
         return (gbyte *)(base + ((uint64_t)(nfr ? f : 0u) * frag_len + (uint64_t)r * kRowBytes + lane_off));
     };
-    // kFrame: fragment f's length and frame padding (wave-uniform)
-    auto frag_len_of = [&](uint32_t f) -> uint32_t {
-        return (uint32_t)min((uint64_t)frag_len, (uint64_t)msg_len - (uint64_t)f * frag_len);
-    };
     auto issue = [&](const GroupTask &t, RowsK<K> &b) {
 #pragma unroll
         for (int c = 0; c < K; ++c) {
-            if constexpr (kFrame) {
-                const uint32_t f = nfr ? frag(t.i, c) : 0u;
-                const uint32_t L = frag_len_of(f), P = R * (uint32_t)kRowBytes - L;
-                const uint64_t a = (uint64_t)(uintptr_t)(base + (uint64_t)f * frag_len);
-                const u32x4 rs{uniform((uint32_t)a), uniform((uint32_t)(a >> 32) & 0xFFFFu), uniform(L), 0x00020000u};
-                uint32_t o[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] = t.r * (uint32_t)kRowBytes + lane_off + 16u * q - P;
-                issue_row_buf(rs, o, b.x[c]);
-            } else {
-                issue_row<kS>(row_ptr(frag(t.i, c), t.r), b.x[c]);
-            }
+            issue_row<kS>(row_ptr(frag(t.i, c), t.r), b.x[c]);
         }
     };
 
@@ -3308,28 +3273,7 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
         if constexpr (kCoal) {
             crc_chunks<K>(lds, k, C, b, t.r == 0, (lane == 0) ? vinit : 0u);
         } else {
-            if constexpr (kFrame) {
-                // the register enters as data at frame offset P (a multiple of 16: row P / 4096, lane
-                // (P / 64) % 64, word (P % 64) / 4 of its piece -- a row past 0 only in a short last
-                // fragment); the padding before it reads as zeros, so every lane starts from 0
-#pragma unroll
-                for (int c = 0; c < K; ++c) {
-                    C[c] = t.r == 0 ? 0u : horner_shift(lds, C[c]);
-                    const uint32_t P = R * (uint32_t)kRowBytes - frag_len_of(frag(t.i, c));
-                    if ((P >> 12) == t.r) {  // (uniform)
-                        const uint32_t m = (uint32_t)lane == ((P >> 6) & 63u) ? vinit : 0u;
-                        const uint32_t w = (P >> 2) & 15u;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            u32x4 &x = b.x[c].q[q];
-                            x.x ^= w == 4u * q ? m : 0u;
-                            x.y ^= w == 4u * q + 1 ? m : 0u;
-                            x.z ^= w == 4u * q + 2 ? m : 0u;
-                            x.w ^= w == 4u * q + 3 ? m : 0u;
-                        }
-                    }
-                }
-            } else if (kV > 1 || t.r == 0) {
+            if (kV > 1 || t.r == 0) {
 #pragma unroll
                 for (int c = 0; c < K; ++c) C[c] = (lane == 0) ? vinit : 0u;
             } else {
@@ -4756,44 +4700,21 @@ hipError_t launch_desc_per_wave(const lampi_frag_desc *d, size_t n, uint32_t *ou
     return hipGetLastError();
 }
 
-// Read-only CRC of messages whose fragments are not whole rows on the regular kernel's schedule
-// (crc_regular_kernel<..., kFrame>): 16-byte-aligned message, fragments and message length multiples
-// of 16 bytes.  Measured (tools/microbench/walk_probe.py, profiles/r03/frames_ab.txt) against the
-// piece streams: GM's 65,456-byte fragments 62.5 -> 65.6% (1 GiB) and 74.4 -> 76.6% (4 GiB); 12,368
-// bytes (a quarter of each frame padding) a point slower; 1 MiB / 4 MiB fragments starve the grid
-// (one fragment per chain: 35% / 9%).  So frames take 32-128 KiB fragments in batches of >= 256 MiB.
-constexpr size_t kFrameMinFrag = 32768, kFrameMaxFrag = 131072, kFrameMinBytes = 256u << 20;
-static uint32_t pick_regular_fpw(size_t n, size_t span);
-static bool frame_ok(const uint8_t *base, size_t msg_len, size_t frag_len, size_t n) {
-    return msg_len >= kFrameMinBytes && frag_len >= kFrameMinFrag && frag_len <= kFrameMaxFrag &&
-           frag_len % 16 == 0 && msg_len % 16 == 0 && ((uintptr_t)base & 15u) == 0 && n <= 0xFFFFFFFFull;
-}
-
-static hipError_t launch_crc_frames(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, size_t n,
-                                    uint32_t *out, const uint32_t *img, hipStream_t s) {
-    const size_t span = (frag_len + kRowBytes - 1) / kRowBytes * kRowBytes;
-    const uint32_t fpw = pick_regular_fpw(n, span);
-    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 1, false, kWaves, 0, true>),
-                       grid_for(n, fpw), dim3(kBlock), 0, s, base, (uint32_t)n, fpw, frag_len, partial, img, out,
-                       nullptr, (size_t)0, msg_len);
-    return hipGetLastError();
-}
-
 hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, size_t n,
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
     if (n == 0) return hipSuccess;
     // the read-only table-light kernel (tools/microbench/msg_light.py, profiles/r03/msg_light_ab.txt):
     // fragments of 8-16 rows (GM's 65,456-byte payloads, 64 KiB) one wave each -- 4 GiB of 64 KiB
-    // fragments 67.7 -> 78.4%, of 65,456 B 76.9 -> 78.3% -- and longer ones in messages up to 2 GiB
-    // (crc_light_msg) as 8-row groups: 1 GiB of 1 MiB fragments 40% on the regular kernel, whose
-    // chains are fragments; larger messages keep the framed regular kernel (131,056 B at 4 GiB
-    // 76.8% against 75.7%)
+    // fragments 67.7 -> 78.4%, of 65,456 B 76.9 -> 78.3% -- and longer ones as 8-row groups joined.
+    // Since round 5 at every message length (profiles/r05/crc_light_msg_ab.txt): 4 GiB messages of
+    // 128 KiB-2 MiB fragments on the regular kernel 73-74 -> 80.7-83.4%, 4 MiB 40.9 -> 80.7%, 16 MiB
+    // 10.5 -> 80.9% (the regular kernel's chains are fragments: 256 of them starve the grid), and of
+    // non-whole-row 65,552-131,056 B on the framed regular kernel (removed) 71-76.5 -> 76-82%.
     const size_t R = (frag_len + kRowBytes - 1) / kRowBytes;
     if (crc_light_msg(frag_len, msg_len))
         return launch_crc_light_frag_copy(MsgSource{base, msg_len, frag_len, partial}, n, img, out, s,
                                           R <= kSegRows ? 1u : (uint32_t)((R + kLightRoRows - 1) / kLightRoRows));
-    if (frame_ok(base, msg_len, frag_len, n)) return launch_crc_frames(base, msg_len, frag_len, partial, n, out, img, s);
     const uint32_t fpg = frags_per_wg(n, frag_len);
     hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
                        MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out, nullptr);
@@ -4826,7 +4747,7 @@ static hipError_t launch_regular(const uint8_t *base, size_t n, size_t frag_len,
         const uint32_t fpw = pick_regular_fpw(nv, kV * frag_len);
         hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, kV, kSum>), grid_for(nv, fpw),
                            dim3(kBlock), 0, s, base, (uint32_t)nv, fpw, kV * frag_len, partial, img, out, nullptr,
-                           (size_t)0, (size_t)0);
+                           (size_t)0);
         done = nv * kV;
         if (done == n) return hipGetLastError();
     }
@@ -4834,7 +4755,7 @@ static hipError_t launch_regular(const uint8_t *base, size_t n, size_t frag_len,
     const uint32_t fpw = pick_regular_fpw(m, frag_len);
     hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 1, kSum>), grid_for(m, fpw),
                        dim3(kBlock), 0, s, base + done * frag_len, (uint32_t)m, fpw, frag_len, partial, img, out + done,
-                       nullptr, (size_t)0, (size_t)0);
+                       nullptr, (size_t)0);
     return hipGetLastError();
 }
 
@@ -4855,7 +4776,7 @@ hipError_t launch_crc_regular_copy(const uint8_t *base, size_t n, size_t frag_le
     const uint32_t fpw = std::max(1u, pick_fpw(n, (uint32_t)(frag_len / kRowBytes)) / 2);  // half the read kernel's
     // (one chain per wave and / or a two-deep ring: within a point of this, profiles/r02_crc_copy_fpw/chains/)
     hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, true>), grid_for(n, fpw), dim3(kBlock), 0, s, base,
-                       (uint32_t)n, fpw, frag_len, partial, img, out, dst, dst_stride, (size_t)0);
+                       (uint32_t)n, fpw, frag_len, partial, img, out, dst, dst_stride);
     return hipGetLastError();
 }
 
@@ -4898,6 +4819,28 @@ static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out
     }
     return scratch_done(s, groups, pooled, e);
 }
+
+// SUM message copies of fragments of R rows: the row groups to run (1: sum_copy_row_kernel's row items).
+// Row groups of one row each (GroupSource<MsgCopySource> on sum_copy_wg_kernel, joined by
+// sum_group_join_kernel) instead of row items whose sums meet in one atomicAdd per row on the fragment's
+// word -- 256+ same-address atomics per fragment serialize at L2 -- for fragments of whole rows and for any
+// of >= 64 rows (profiles/r05/sum_msg_copy_ab.txt): 16 KiB 77.4 -> 79.9%, 128 KiB 76.7 -> 79.5%, 512 KiB
+// 65.7 -> 79.2%, 1 MiB 60.2 -> 78.7%, 4 MiB 49.0 -> 76.0%, 16 MiB 32.2 -> 67%.  GM's 65,456-byte fragments
+// (rows off the 16-byte grid) stay on the row items (77.2% against 71.3%).  A/B knobs LAMPI_SUM_CP_GRP_MIN
+// (fewest rows for fragments that are not whole rows, 0 = never groups), LAMPI_SUM_CP_GRP_ROWS (rows per group).
+static uint32_t sum_copy_groups(uint32_t R, bool whole_rows) {
+    static const uint32_t grp_min = [] {
+        const char *e = std::getenv("LAMPI_SUM_CP_GRP_MIN");
+        return e ? (uint32_t)std::atoi(e) : 64u;
+    }();
+    static const uint32_t grp_rows = [] {
+        const char *e = std::getenv("LAMPI_SUM_CP_GRP_ROWS");
+        return e ? (uint32_t)std::max(1, std::atoi(e)) : 1u;
+    }();
+    if (!grp_min || R < 2 || (!whole_rows && R < grp_min)) return 1u;
+    return (R + grp_rows - 1) / grp_rows;
+}
+
 
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                              hipStream_t s, uint32_t rows_hint) {
@@ -5170,6 +5113,9 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                                           out, s);
     }
     const uint64_t rpf = (frag_len + kRowBytes - 1) / kRowBytes;
+    const uint32_t W = msg_len != 0 && rpf < 0xFFFFFFFFull ? sum_copy_groups((uint32_t)rpf, frag_len % kRowBytes == 0)
+                                                            : 1u;
+    if (W > 1) return launch_sum_copy_groups(MsgCopySource{base, msg_len, frag_len, 0u, dst, dst_stride}, n, out, s, W);
     if (msg_len != 0 && frag_len >= kRowBytes && frag_len % 16 == 0 && msg_len % 16 == 0 &&
         ((uintptr_t)base & 15u) == 0 && ((uintptr_t)dst & 3u) == 0 && dst_stride % 4 == 0 &&
         n * rpf <= 0xFFFFFFFFull) {

@@ -21,8 +21,9 @@ inline bool regular_msg_frag(size_t frag_len, bool sum) {
 // CRC messages whose fragments run on the read-only table-light kernel (launch_crc_msg): 8-16 rows,
 // or longer in messages of at most 2 GiB (row groups; the regular kernel keeps the larger ones)
 inline bool crc_light_msg(size_t frag_len, size_t msg_len) {
+    (void)msg_len;  // (up to round 4: > 16 rows only in messages up to 2 GiB; profiles/r05/crc_light_msg_ab.txt)
     const size_t rows = (frag_len + 4095) / 4096;
-    return rows >= 8 && (rows <= 16 || (msg_len <= ((size_t)1 << 31) && rows < ((size_t)1 << 32)));
+    return rows >= 8 && rows < ((size_t)1 << 32);
 }
 
 // Workgroups for the persistent CRC kernel on `device` (one 1024-thread WG per CU).

@@ -242,11 +242,14 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     (40000 * 1500 + 12345, 40000, 40000, 0),  # a short last fragment with fewer rows
     (20001 * 777, 20001, 20480, 8),           # odd length, destinations at +8
     # SUM: 16-byte-multiple fragments of 4 KiB and more go one workgroup per 4 KiB row
-    # (sum_copy_row_kernel): partial last rows, short last fragments, dword-aligned slots
+    # (sum_copy_row_kernel) -- whole-row fragments and those of >= 64 rows as one-row groups joined
+    # (round 5): partial last rows, short last fragments, dword-aligned slots
     (65456 * 300, 65456, 65536, 72),          # GM send: 65,456-byte payloads after the 72-byte header
     (65456 * 200 + 4000, 65456, 65536 + 4, 4),  # a last fragment of 4,000 bytes (one partial row)
     (4112 * 3000, 4112, 4112 + 12, 12),       # a second row of 16 bytes per fragment
-    (49152 * 100 + 4096 * 5, 49152, 49152, 0),  # a last fragment of 5 of its 12 rows
+    (49152 * 100 + 4096 * 5, 49152, 49152, 0),  # a last fragment of 5 of its 12 rows (groups)
+    ((1 << 18) * 9 + 4096 * 70 + 16, 1 << 18, (1 << 18) + 4, 4),  # 64-row fragments as groups, the last one 6 rows + 16 B
+    ((300000 // 16 * 16) * 40 + 48, 300000 // 16 * 16, 300032, 0),  # 74 rows, not whole rows: groups
     # CRC: 16-byte-multiple messages of fragments >= 4 KiB take the table-light copy
     # (crc_light_copy_kernel: one row per wave; rows of longer fragments joined by crc_light_join_kernel)
     ((1 << 20) * 40 + 4096 * 3 + 48, 1 << 20, (1 << 20) + 76, 4),  # 256-row fragments, a 3-row last one
@@ -306,8 +309,8 @@ def test_sum_copy_grid_loop(cuda):
     assert not bool(d[~full][:, 37:].any())  # the residue is checksummed, not copied
     del src, dst, descs, d, s
 
-    nf = (1 << 20) + 3  # message rows: 4 rows per 16 KiB fragment, 2^22 + 12 rows
-    F = 16384
+    nf = 900001  # message rows: 5 rows per 16,400-byte fragment (not whole rows: row items), 4,500,005 rows
+    F = 16400
     msg = torch.empty(nf * F, dtype=torch.uint8, device=cuda)
     dv.fill_stream(msg, seed=32)
     out = torch.empty(nf * F + 16, dtype=torch.uint8, device=cuda)
