@@ -345,6 +345,14 @@ struct IsSplit : std::false_type {};
 template <bool B>
 struct IsSplit<SplitDescSource<B>> : std::true_type {};
 
+// Small read-only CRC batches without a hint (launch_crc_desc): every fragment as W row groups, most of
+// them empty for short fragments -- a workgroup whose four waves hold no rows leaves before staging tables.
+struct SparseDescSource : DescSource {};
+template <class S>
+struct IsSparse : std::false_type {};
+template <>
+struct IsSparse<SparseDescSource> : std::true_type {};
+
 template <class S>
 struct IsRecv : std::false_type {};
 template <>
@@ -2680,8 +2688,8 @@ __global__ void __launch_bounds__(64 * kWv) crc_light_frag_copy_kernel(const Src
     // the first row's loads before the table staging (after it: 4 KiB copies 73 -> 66%, profiles/r04/late_loads_ab.txt)
     F.load_row(lane, F.r0, F.live, d, o, F.half);  // (an empty or dead wave's descriptor reads nothing but zeros)
     const u32x4 head = F.load_head();
-    if constexpr (IsSplit<Src>::value)  // the size split's light launch: most workgroups hold no fragment of its
-        if (!__syncthreads_or(F.live)) return;  // class and leave before staging the tables
+    if constexpr (IsSplit<Src>::value || IsSparse<Src>::value)  // the size split's light launch: most workgroups
+        if (!__syncthreads_or(F.live)) return;  // hold no fragment of its class and leave before staging the tables
     build_slices_light<64 * kWv>(reinterpret_cast<char *>(lds), bs);
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[min(t, kNibPieces - 1)] = nib;
     if constexpr (kWv == 4) reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[t2] = nib2;
@@ -3460,17 +3468,20 @@ __global__ void __launch_bounds__(256) sum_copy_waves_kernel(Src src, size_t n, 
 }
 
 // SUM row groups: out[f] = the sum of fragment f's W group sums, then emit (receive sources: the verdict).
+// G = min(64, pow2 >= W) lanes per fragment, lane j adding groups j, j + G, ... (one thread walking a
+// fragment's 4,096 one-row groups waited on 4,096 loads in turn).
 template <class Src>
-__global__ void __launch_bounds__(256) sum_group_join_kernel(const Src src, size_t n, uint32_t W,
+__global__ void __launch_bounds__(256) sum_group_join_kernel(const Src src, size_t n, uint32_t W, uint32_t G,
                                                              const uint32_t *__restrict__ groups,
                                                              uint32_t *__restrict__ out) {
-    const size_t f = (size_t)blockIdx.x * 256 + threadIdx.x;
-    if (f >= n) return;
-    const FragInfo fi = src.get(f);
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x, f = i / G;
+    const uint32_t j = (uint32_t)(i & (G - 1u));
+    if (f >= n) return;  // (the G lanes of a fragment leave or stay together)
     const uint32_t *p = groups + f * W;
     uint32_t sm = 0;
-    for (uint32_t g = 0; g < W; ++g) sm += p[g];
-    emit(src, out, f, sm, fi);
+    for (uint32_t g = j; g < W; g += G) sm += p[g];
+    for (uint32_t o = G >> 1; o >= 1u; o >>= 1) sm += (uint32_t)__shfl_xor((int)sm, (int)o);
+    if (j == 0) emit(src, out, f, sm, src.get(f));
 }
 
 // Acc = uint32_t: uicsum (32-bit words); Acc = uint64_t: csum (64-bit words, ref
@@ -4642,11 +4653,34 @@ static hipError_t launch_row_segments(const lampi_frag_desc *d, size_t n, uint32
 // launches concurrently on a forked stream measured worse (GM 67-68%).
 constexpr size_t kSplitMin = 1024, kSplitMax = 65536;
 
+// Read-only descriptor batches under the learned-shape minimum (kShapeMin fragments) without a rows hint.
+// The lengths are on the device only: the count split gave a whole fragment to one workgroup (16 x 16 MiB
+// 2.3 ms, 1.5% of the roofline; one 64 MiB fragment 3 ms).  Every fragment runs as W row groups instead
+// (k = ceil(R / W) rows each, groups past a fragment's rows empty; CRC: the table-light kernel, a workgroup
+// of four empty waves leaving before its table staging), W the power of two bringing the launch to ~4,096
+// items: 16 x 16 MiB 2,284 -> 60 us (CRC), 1,348 -> 46 us (SUM); 200 x 1 MiB 155 -> 43 / 91 -> 37 us; batches of
+// small fragments pay the join launch, 200 x 4 KiB 8.3 -> 11.3 us (tools/microbench/small_batch.py,
+// profiles/r05/small_batch_ab.txt).  A shape learned per descriptor array would save that join but a stale
+// one-row shape would bring the 100x case back; the caller's LAMPI_CSUM_ROWS_HINT picks the best schedule
+// (one 64 MiB fragment: 168 us as groups, 55 us with the hint).  A/B knob LAMPI_SMALL_BATCH = the item
+// target (0: the count split).
+static uint32_t small_batch_groups(size_t n) {
+    static const size_t target = [] {
+        const char *e = std::getenv("LAMPI_SMALL_BATCH");
+        return e ? (size_t)std::atoll(e) : (size_t)4096;
+    }();
+    uint32_t W = 1;
+    while ((size_t)n * W < target && W < 4096u) W <<= 1;
+    return W;
+}
+
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
                            hipStream_t s, bool plan, uint32_t rows_hint) {  // (defaults: frag_csum_kernels.h)
     (void)grid;
     if (n == 0) return hipSuccess;
     if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
+    if (rows_hint <= 1 && n < kShapeMin && small_batch_groups(n) > 1)
+        return launch_crc_light_frag_copy(SparseDescSource{{d}}, n, img, out, s, small_batch_groups(n));
     rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint);
     if (rows_hint >= kLightDescRows)  // one wave per kSegRows rows of a fragment, read-only
         return launch_crc_light_frag_copy(DescSource{d}, n, img, out, s,
@@ -4813,8 +4847,10 @@ static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out
     launch_sum_copy(GroupSource<Src>{src, W}, n * W, groups, s);
     e = hipGetLastError();
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(sum_group_join_kernel<Src>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, n, W,
-                           groups, out);
+        uint32_t G = 1;
+        while (G < W && G < 64u) G <<= 1;
+        hipLaunchKernelGGL(sum_group_join_kernel<Src>, dim3((unsigned)((n * G + 255) / 256)), dim3(256), 0, s, src, n, W,
+                           G, groups, out);
         e = hipGetLastError();
     }
     return scratch_done(s, groups, pooled, e);
@@ -4960,6 +4996,8 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
+    if (img && rows_hint <= 1 && n < kShapeMin && small_batch_groups(n) > 1)  // (small batches: as launch_crc_desc)
+        return launch_sum_copy_groups(DescSource{d}, n, out, s, small_batch_groups(n));
     bool one_row = false;
     if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, 2u, &one_row);
     if (img && rows_hint > 1) {

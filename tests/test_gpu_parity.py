@@ -417,6 +417,42 @@ def test_descriptor_batch_byte_balanced(cuda, oracle, case, mode):
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("case", ["one_64mib", "n16_ragged", "n255_mixed", "n200_tiny", "n3_rows"])
+def test_descriptor_small_batch_row_groups(cuda, oracle, case, mode):
+    """Read-only descriptor batches under 256 fragments without a rows hint (round 5): every fragment as W
+    row groups (W = 4096 for one fragment down to 16 for 255), groups past a fragment's rows empty; CRC on
+    the table-light kernel (empty workgroups leave before staging tables) joined by the constant-product
+    XOR, SUM groups added.  Odd addresses, ragged and zero lengths, random registers; vs the oracle."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(abs(hash(case)) % 2**32)
+    MiB = 1 << 20
+    if case == "one_64mib":
+        lens = np.array([64 * MiB - 5], np.uint64)
+    elif case == "n16_ragged":
+        lens = (rng.integers(1, 3 * MiB, size=16) | 1).astype(np.uint64)
+        lens[3], lens[7] = 0, 4096 * 4096  # an empty fragment; 4,096 rows: one per group at W = 256
+    elif case == "n255_mixed":
+        lens = rng.integers(0, 5000, size=255).astype(np.uint64)
+        lens[rng.choice(255, size=5, replace=False)] = rng.integers(MiB, 4 * MiB, size=5)
+    elif case == "n200_tiny":
+        lens = rng.integers(0, 4097, size=200).astype(np.uint64)
+    else:  # rows around the group size: 3 fragments at W = 2048
+        lens = np.array([2048 * 4096 + 1, 2047 * 4096, 4095 * 4096 + 4095], np.uint64)
+    offs = (np.concatenate([[0], np.cumsum(lens)[:-1]]) + np.arange(lens.size) * 3 + 1).astype(np.uint64)
+    base = torch.empty(int((offs + lens).max()) + 64, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=lens.size)
+    parts = rng.integers(0, 2**32, size=lens.size, dtype=np.uint64)
+    descs = dv.make_descs(base, offs, lens, parts)
+    got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode))
+    host = base.cpu().numpy()
+    want = oracle.desc_batch(host, offs, lens.astype(np.uint32), parts.astype(np.uint32) if mode == 0 else None, mode)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 def test_descriptor_batch_row_segments(cuda, oracle, mode):
     """LAMPI_CSUM_ROWS_HINT on lampi_frag_csum_batch: workgroups sized by the hinted length, and above 16
     rows ceil(hint / 16) row segments per fragment computed on the device (CRC cut from the end, SUM from
