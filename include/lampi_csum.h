@@ -293,7 +293,9 @@ typedef struct lampi_frag_desc {
  * 4 KiB rows, so mixed sizes keep every lane busy; with LAMPI_CSUM_ROWS_HINT (or the shape the
  * stream's earlier batches showed) long fragments one wavefront each on the table-light kernel (CRC)
  * or as row groups on short-lived workgroups (SUM); 1,024-65,536 fragments without a hint split by
- * size class (CRC).  Results never depend on the schedule.
+ * size class (CRC); under 256 fragments without a hint every fragment runs as row groups sized to the
+ * launch (a few large fragments no longer sit on one workgroup each; LAMPI_CSUM_ROWS_HINT(1) keeps the
+ * count split for batches known to hold small fragments).  Results never depend on the schedule.
  * Replaces the per-fragment loop of gmPath::send / gmSendFragDesc::init
  * (src/path/gm/path.cc:98-176, src/path/gm/sendFrag.cc:147-155) and the Quadrics
  * checksum-only send (src/path/quadrics/sendFrag.h:861-872). */

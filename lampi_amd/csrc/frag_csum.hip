@@ -4679,7 +4679,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
-    if (rows_hint <= 1 && n < kShapeMin && small_batch_groups(n) > 1)
+    if (rows_hint == 0 && n < kShapeMin && small_batch_groups(n) > 1)  // (1: the caller's pieces, count split)
         return launch_crc_light_frag_copy(SparseDescSource{{d}}, n, img, out, s, small_batch_groups(n));
     rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint);
     if (rows_hint >= kLightDescRows)  // one wave per kSegRows rows of a fragment, read-only
@@ -4996,7 +4996,7 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
-    if (img && rows_hint <= 1 && n < kShapeMin && small_batch_groups(n) > 1)  // (small batches: as launch_crc_desc)
+    if (img && rows_hint == 0 && n < kShapeMin && small_batch_groups(n) > 1)  // (small batches: as launch_crc_desc)
         return launch_sum_copy_groups(DescSource{d}, n, out, s, small_batch_groups(n));
     bool one_row = false;
     if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, 2u, &one_row);

@@ -320,10 +320,11 @@ uint32_t device_crc(HostCtx &c, const Staged &st, uint64_t len, uint32_t partial
         LAMPI_CHECK(launch_host_one(st.base, (uint32_t)len, partial, res, LAMPI_CSUM_CRC32, img, c.stream,
                                     signal_word(c, seq), seq));
     } else if (n == 1) {
-        LAMPI_CHECK(launch_crc_desc(upload_descs(c, 1, false), 1, res, img, grid, c.stream, false));
+        LAMPI_CHECK(launch_crc_desc(upload_descs(c, 1, false), 1, res, img, grid, c.stream, false, 1u));
     } else {
         ensure(c.dvals, c.vcap, (size_t)n + 4);
-        LAMPI_CHECK(launch_crc_desc(upload_descs(c, n, st.zero_copy), n, c.dvals, img, grid, c.stream, false));
+        // (rows hint 1: pieces sized for the count split, not a small batch of unknown fragments)
+        LAMPI_CHECK(launch_crc_desc(upload_descs(c, n, st.zero_copy), n, c.dvals, img, grid, c.stream, false, 1u));
         LAMPI_CHECK(launch_crc_combine(c.dvals, n, combine_tables(c, B), next_pow2(n), res, c.stream,
                                        signal_word(c, seq), seq));
     }
@@ -357,7 +358,7 @@ uint32_t device_sum(HostCtx &c, const Staged &st, uint64_t len, unsigned int *pi
     }
     if (n) {
         const lampi_frag_desc *d = upload_descs(c, n, st.zero_copy);
-        LAMPI_CHECK(launch_sum_desc(d, n, c.dvals, nullptr, grid, c.stream, false));
+        LAMPI_CHECK(launch_sum_desc(d, n, c.dvals, nullptr, grid, c.stream, false, 1u));
     }
     LAMPI_CHECK(launch_sum_finish(c.dvals, n, st.base, len, *pint, *plen, out3, c.stream, signal_word(c, seq), seq));
     wait_done(c, seq);
