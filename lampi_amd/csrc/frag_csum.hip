@@ -3177,13 +3177,16 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // 79.6-79.7%, 16 KiB fragments 79.1-79.2 -> 78.5%; profiles/r02_sum_regular/).
 // kWv: waves per workgroup (the table builders use the first 256 threads); kCap > 0 asks the
 // compiler for that many waves per SIMD.
-// kDesc (read-only CRC, kV = 2; round 5): a descriptor batch of 4 KiB fragments on this schedule --
-// `base` is the lampi_frag_desc array, n the number of fragment pairs, each fragment with its own
-// address and register.  A wave loads its 2 * fpw descriptors into lanes (one vector load before the
-// ring), takes each row's address and register by readlane, and checks every fragment: a pair holding
-// a fragment that is not exactly 4 KiB at a 16-byte-aligned address is read at a dummy address (the
-// table image: the ring's load counts stay fixed), not emitted, and listed (atomicAdd on *left) for
-// crc_light_pair_leftover_kernel, which checksums both fragments on the table-light kernel.
+// kDesc (read-only CRC; round 5): a descriptor batch of equal whole-row fragments on this schedule --
+// `base` is the lampi_frag_desc array, each fragment with its own address and register.  kV = 2: 4 KiB
+// fragments in pairs (n = pairs, lane 2j + r holds fragment 2 (f0 + kWv j) + r); kV = 1: fragments of
+// R = frag_len / 4096 rows (n = fragments, lane j holds fragment f0 + kWv j).  A wave loads its
+// descriptors into lanes (one vector load before the ring), takes each row's address and register by
+// readlane, and checks every fragment: a pair (kV = 2) or fragment (kV = 1) that is not exactly
+// frag_len / kV bytes at a 16-byte-aligned address is read at a dummy address (the table image: the
+// ring's load counts stay fixed), not emitted, and listed (atomicAdd on *left) for
+// crc_light_pair_leftover_kernel, which checksums fragments 2e and 2e + 1 of entry e on the table-light
+// kernel (kV = 1 lists f / 2: its neighbour is checksummed again, to the same value).
 template <int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
           bool kSum = false, int kWv = kWaves, int kCap = 0, bool kDesc = false>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kCap > 0 ? kCap : 1)))
@@ -3192,7 +3195,7 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
                    size_t dst_stride, uint32_t *__restrict__ list = nullptr, uint32_t *left = nullptr) {
     constexpr int K = kChains;
     static_assert(kWv >= kWaves, "the table builders need 256 threads");
-    static_assert(!kDesc || (kV == 2 && !kCopy && !kSum), "descriptor pairs: read-only CRC, kV = 2");
+    static_assert(!kDesc || (kV <= 2 && !kCopy && !kSum), "descriptor batches: read-only CRC, kV = 1 or 2");
     constexpr int kS = kCoal ? kRowBytes / 4 : 16;  // chunk stride of a lane
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
@@ -3203,27 +3206,34 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     const uint32_t ngrp = (nfr + K - 1) / K;
     const uint32_t lane_off = (uint32_t)lane * (kCoal ? kChunkBytes : kLaneBytes);
     const uint32_t vinit = __builtin_bswap32(partial);
-    // kDesc: lane 2j + r holds fragment 2 (f0 + kWv j) + r's descriptor; bad bit j: pair j is listed
+    // kDesc: lane kV j + r holds fragment kV (f0 + kWv j) + r's descriptor; bad bit j: item j is listed
     uint32_t da_lo = 0u, da_hi = 0u, dpart = 0u;
     uint64_t bad = 0u;
     if constexpr (kDesc) {
         const lampi_frag_desc *descs = reinterpret_cast<const lampi_frag_desc *>(base);
-        const uint32_t j = (uint32_t)lane >> 1;
+        const uint32_t j = (uint32_t)lane / kV;
         const bool mine = j < nfr;
         uint32_t len = 0u;
         if (mine) {
-            const lampi_frag_desc x = descs[(size_t)(f0 + kWv * j) * 2u + (lane & 1)];
+            const lampi_frag_desc x = descs[(size_t)(f0 + kWv * j) * kV + (kV == 2 ? (lane & 1) : 0)];
             da_lo = (uint32_t)x.addr;
             da_hi = (uint32_t)(x.addr >> 32);
             len = x.length;
             dpart = x.partial;
         }
-        const bool odd = mine && (len != (uint32_t)kRowBytes || (da_lo & 15u) != 0u);
+        const bool odd = mine && (len != (uint32_t)(frag_len / kV) || (da_lo & 15u) != 0u);
         const uint64_t lanes = __ballot(odd);
-        for (uint32_t q = 0; q < 32u; ++q) bad |= ((lanes >> (2u * q)) & 3ull) ? (1ull << q) : 0ull;
+        if constexpr (kV == 2) {
+            for (uint32_t q = 0; q < 32u; ++q) bad |= ((lanes >> (2u * q)) & 3ull) ? (1ull << q) : 0ull;
+        } else {
+            bad = lanes;
+        }
         bad = uniform64(bad);
         if (bad && lane == 0) {
-            for (uint64_t m = bad; m; m &= m - 1) list[atomicAdd(left, 1u)] = f0 + kWv * (uint32_t)__builtin_ctzll(m);
+            for (uint64_t m = bad; m; m &= m - 1) {
+                const uint32_t f = f0 + kWv * (uint32_t)__builtin_ctzll(m);
+                list[atomicAdd(left, 1u)] = kV == 2 ? f : f >> 1;
+            }
         }
     }
 
@@ -3239,15 +3249,16 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
         return f0 + kWv * (j < nfr ? j : K * i);
     };
     auto row_ptr = [&](uint32_t f, uint32_t r) -> gbyte * {
-        if constexpr (kDesc) {  // f = f0 + kWv j: row r is fragment 2f + r, its address in lane 2j + r
-            const uint32_t j = (f - f0) / kWv, L = 2u * j + r;
+        if constexpr (kDesc) {  // f = f0 + kWv j; kV = 2: row r is fragment 2f + r (lane 2j + r), kV = 1: lane j
+            const uint32_t j = (f - f0) / kWv, L = kV == 2 ? 2u * j + r : j;
             // (readlane returns int: each half goes through uint32_t, or a low word >= 2^31 sign-extends
             // into the high one -- the illegal address of this path's first GPU run)
             const uint64_t a = (nfr && !((bad >> j) & 1u))
                                    ? ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(da_hi, L) << 32) |
                                          (uint64_t)(uint32_t)__builtin_amdgcn_readlane(da_lo, L)
                                    : (uint64_t)(uintptr_t)img;
-            return (gbyte *)(a + lane_off);
+            const uint64_t ro = kV == 2 || !(nfr && !((bad >> j) & 1u)) ? 0u : (uint64_t)r * kRowBytes;
+            return (gbyte *)(a + ro + lane_off);
         }
         return (gbyte *)(base + ((uint64_t)(nfr ? f : 0u) * frag_len + (uint64_t)r * kRowBytes + lane_off));
     };
@@ -3322,10 +3333,10 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
         if constexpr (kCoal) {
             crc_chunks<K>(lds, k, C, b, t.r == 0, (lane == 0) ? vinit : 0u);
         } else {
-            if constexpr (kDesc) {  // every row starts a fragment with its own register
+            if (kDesc && (kV > 1 || t.r == 0)) {  // a fragment's first row: its own register
 #pragma unroll
                 for (int c = 0; c < K; ++c) {
-                    const uint32_t L = 2u * ((frag(t.i, c) - f0) / kWv) + t.r;
+                    const uint32_t j = (frag(t.i, c) - f0) / kWv, L = kV == 2 ? 2u * j + t.r : j;
                     const uint32_t v = __builtin_bswap32((uint32_t)__builtin_amdgcn_readlane(dpart, L));
                     C[c] = (lane == 0) ? v : 0u;
                 }
@@ -4336,7 +4347,7 @@ struct BatchShape {
     uint32_t sampled;  // descriptors sampled (up to 64, spread over the batch)
     uint32_t rmin, rmax;  // fewest / most rows (4 KiB) among them
     uint32_t nhalf;    // how many were at most 2 KiB
-    uint32_t nfull;    // how many were exactly 4 KiB at a 16-byte-aligned address
+    uint32_t nwhole;   // how many were whole 4 KiB rows (> 0 bytes) at a 16-byte-aligned address
     uint32_t pad[2];
 };
 constexpr int kShapeSlots = 8;  // shape records per (thread, device, stream): descriptor arrays remembered
@@ -4527,7 +4538,7 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         rmin = R;
         rmax = R;
         half = fi.len <= (uint32_t)kRowBytes / 2u ? 1u : 0u;
-        full = fi.len == (uint32_t)kRowBytes && ((uintptr_t)fi.addr & 15u) == 0 ? 1u : 0u;
+        full = fi.len != 0u && fi.len % (uint32_t)kRowBytes == 0u && ((uintptr_t)fi.addr & 15u) == 0 ? 1u : 0u;
     }
     for (int o = 32; o >= 1; o >>= 1) {
         rmin = min(rmin, (uint32_t)__shfl_xor((int)rmin, o));
@@ -4541,7 +4552,7 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         r->rmin = rmin;
         r->rmax = rmax;
         r->nhalf = half;
-        r->nfull = full;
+        r->nwhole = full;
         __threadfence_system();
         r->seq = seq;
     }
@@ -4609,12 +4620,14 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     uint32_t W = rows_hint;
     const uint32_t q0 = v->seq;
     std::atomic_thread_fence(std::memory_order_acquire);  // the fields are read after the first seq ...
-    const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf, nfull = v->nfull;
+    const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf, nwhole = v->nwhole;
     std::atomic_thread_fence(std::memory_order_acquire);  // ... and before the second (a seqlock read)
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= min_rows && rmax <= 2 * rmin) W = rmax;
         if (one_row && rmin == 1u && rmax == 1u) *one_row = true;  // every sampled fragment one row (17 B-4 KiB)
-        if (full_rows && nfull == sampled) *full_rows = true;  // ... exactly 4 KiB, 16-byte aligned
+        // every sampled fragment the same whole number of rows at a 16-byte-aligned address (*full_rows: the
+        // rows, W the most rows as above)
+        if (full_rows && nwhole == sampled && rmin == rmax) *full_rows = true;
         if (pairs && nhalf == sampled && !slot.pair_broken) {  // every sampled fragment at most 2 KiB: two per wave
             void *dp = nullptr;
             if (nhalf_dev && hipHostGetDevicePointer(&dp, rec, 0) == hipSuccess) {
@@ -4709,28 +4722,34 @@ static hipError_t launch_row_segments(const lampi_frag_desc *d, size_t n, uint32
 // launches concurrently on a forked stream measured worse (GM 67-68%).
 constexpr size_t kSplitMin = 1024, kSplitMax = 65536;
 
-// Read-only CRC descriptor batches the census saw as all 4 KiB fragments at 16-byte-aligned addresses:
-// crc_regular_kernel<kDesc> over fragment pairs (config B's schedule: two chains per wave, each reading
-// two fragments in turn), the pairs holding any other fragment listed by the kernel and checksummed by
-// crc_light_pair_leftover_kernel (the pair kernel's counters and leftover launch), an odd last fragment
-// on the table-light kernel.
+// Read-only CRC descriptor batches the census saw as equal whole-row fragments (R rows) at 16-byte-aligned
+// addresses: crc_regular_kernel<kDesc> on config B's schedule -- 4 KiB fragments in pairs (two chains per
+// wave, each reading a pair in turn; an odd last fragment on the table-light kernel), longer ones one per
+// chain row by row -- the items holding any other fragment listed by the kernel and checksummed by
+// crc_light_pair_leftover_kernel (the pair kernel's counters and leftover launch).
 constexpr size_t kRegDescMinPairs = 2048;
 static uint32_t pick_regular_fpw(size_t n, size_t span);
-static hipError_t launch_crc_desc_pairs(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
-                                        hipStream_t s) {
-    const size_t nv = n / 2;
-    if (nv > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t fpw = pick_regular_fpw(nv, 2 * kRowBytes);
-    if (fpw > 32u) return hipErrorInvalidValue;  // (a wave's 2 fpw descriptors live in its 64 lanes)
+static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
+                                        hipStream_t s, uint32_t R) {
+    const size_t items = R == 1 ? n / 2 : n;  // pairs of 4 KiB fragments, or fragments
+    const size_t span = R == 1 ? 2 * kRowBytes : (size_t)R * kRowBytes;
+    if (items > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t fpw = pick_regular_fpw(items, span);
+    if (fpw > (R == 1 ? 32u : 64u)) return hipErrorInvalidValue;  // (a wave's descriptors live in its 64 lanes)
     uint32_t *list = nullptr, *left = nullptr, *next_left = nullptr;
     bool pooled = false;
-    hipError_t e = stream_scratch(s, nv * sizeof(uint32_t), (void **)&list, &pooled);
+    hipError_t e = stream_scratch(s, (items + 1) * sizeof(uint32_t), (void **)&list, &pooled);
     if (e != hipSuccess) return e;
     e = pair_counters(s, &left, &next_left);
     if (e != hipSuccess) return scratch_done(s, list, pooled, e);
-    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 2, false, kWaves, 0, true>),
-                       grid_for(nv, fpw), dim3(kBlock), 0, s, reinterpret_cast<const uint8_t *>(d), (uint32_t)nv, fpw,
-                       (size_t)(2 * kRowBytes), 0u, img, out, nullptr, (size_t)0, list, left);
+    if (R == 1)
+        hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 2, false, kWaves, 0, true>),
+                           grid_for(items, fpw), dim3(kBlock), 0, s, reinterpret_cast<const uint8_t *>(d),
+                           (uint32_t)items, fpw, span, 0u, img, out, nullptr, (size_t)0, list, left);
+    else
+        hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 1, false, kWaves, 0, true>),
+                           grid_for(items, fpw), dim3(kBlock), 0, s, reinterpret_cast<const uint8_t *>(d),
+                           (uint32_t)items, fpw, span, 0u, img, out, nullptr, (size_t)0, list, left);
     e = hipGetLastError();
     if (e == hipSuccess) {
         hipLaunchKernelGGL(crc_light_pair_leftover_kernel<DescSource>, dim3(kLeftoverWgs), dim3(256), 0, s,
@@ -4740,7 +4759,8 @@ static hipError_t launch_crc_desc_pairs(const lampi_frag_desc *d, size_t n, uint
     }
     if (e != hipSuccess) reset_pair_counters(s);
     e = scratch_done(s, list, pooled, e);
-    if (e == hipSuccess && (n & 1u)) e = launch_crc_light_frag_copy(DescSource{d + n - 1}, 1, img, out + n - 1, s);
+    if (e == hipSuccess && R == 1 && (n & 1u))
+        e = launch_crc_light_frag_copy(DescSource{d + n - 1}, 1, img, out + n - 1, s);
     return e;
 }
 
@@ -4772,13 +4792,20 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
     if (rows_hint == 0 && n < kShapeMin && small_batch_groups(n) > 1)  // (1: the caller's pieces, count split)
         return launch_crc_light_frag_copy(SparseDescSource{{d}}, n, img, out, s, small_batch_groups(n));
-    bool full4k = false;
-    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, kShapeRows, nullptr, &full4k);
-    static const bool reg_desc = [] {  // (A/B knob LAMPI_CRC_DESC_REGULAR=0: the piece streams)
+    bool whole = false;
+    const uint32_t given = rows_hint;
+    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, 1u, nullptr, &whole);
+    // batches of equal whole-row fragments of 1-7 rows on the regular kernel (profiles/r05/crc_desc_pairs_ab.txt:
+    // 4 KiB 76.4-77.8 -> 80.3-80.4%, 8 KiB 74.3 -> 77.8%, 16 KiB 74.7 -> 79.2%, 28 KiB 70.4 -> 75.4%; from 8 rows
+    // the table-light kernel stays ahead, 32 KiB 81 against 73%, 64 KiB 80 against 67%).  A/B knob
+    // LAMPI_CRC_DESC_REGULAR = the most rows taken (0: never).
+    static const uint32_t reg_desc = [] {
         const char *e = std::getenv("LAMPI_CRC_DESC_REGULAR");
-        return !(e && e[0] == '0');
+        return e ? (uint32_t)std::atoi(e) : 7u;
     }();
-    if (full4k && reg_desc && n >= 2 * kRegDescMinPairs) return launch_crc_desc_pairs(d, n, out, img, s);
+    if (whole && rows_hint >= 1u && rows_hint <= reg_desc && n >= 2 * kRegDescMinPairs)
+        return launch_crc_desc_whole(d, n, out, img, s, rows_hint);
+    if (given <= 1 && rows_hint < kShapeRows) rows_hint = given;  // (learned hints under 8 rows: as before)
     if (rows_hint >= kLightDescRows)  // one wave per kSegRows rows of a fragment, read-only
         return launch_crc_light_frag_copy(DescSource{d}, n, img, out, s,
                                           rows_hint <= kSegRows ? 1u : (rows_hint + kLightRoRows - 1) / kLightRoRows);

@@ -279,27 +279,29 @@ def test_learned_pairs_shape_change(cuda, oracle, mode):
             assert torch.equal(dst, want_dst), (i, k)
 
 
-def test_learned_4k_descriptor_pairs(cuda, oracle):
-    """Read-only CRC batches the census saw as all 4 KiB fragments at 16-byte-aligned addresses run on
-    the regular kernel in fragment pairs (crc_regular_kernel<kDesc>, round 5).  The same descriptor array
-    then holds a batch where 1 in 20 fragments is not (lengths 0 / 1 / 4,095 / 4,097 / 8,192, odd
-    addresses): under the stale shape those fragments' pairs are listed by the kernel and checksummed by
-    the leftover launch.  Odd fragment counts end on the table-light kernel.  Every call vs the oracle."""
+@pytest.mark.parametrize("L", [4096, 8192, 16384, 28672])
+def test_learned_whole_row_descriptors(cuda, oracle, L):
+    """Read-only CRC batches the census saw as equal whole-row fragments at 16-byte-aligned addresses run
+    on the regular kernel (crc_regular_kernel<kDesc>, round 5): 4 KiB fragments in pairs, longer ones one
+    per chain.  The same descriptor array then holds a batch where 1 in 20 fragments is not (lengths 0 / 1
+    / L - 1 / L + 1 / 2L, odd addresses): under the stale shape those fragments (and their pair or even
+    neighbour) are listed by the kernel and checksummed by the leftover launch.  Odd fragment counts end
+    on the table-light kernel.  Every call vs the oracle."""
     import torch
 
     dv = _dv()
-    rng = np.random.default_rng(404)
-    n = 2 * 2048 * 2 + 1  # >= the pair path's minimum, odd
-    size = 64 << 20
+    rng = np.random.default_rng(404 + L)
+    n = 2 * 2048 * 2 + 1  # >= the path's minimum, odd
+    size = max(64 << 20, n * (L + 64) * 2)
     base = torch.empty(size, dtype=torch.uint8, device=cuda)
     dv.fill_stream(base, seed=405)
     host = base.cpu().numpy()
-    offs = (rng.integers(0, (size - 16384) // 16, size=n) * 16).astype(np.uint64)
+    offs = (rng.integers(0, (size - 2 * L - 64) // 16, size=n) * 16).astype(np.uint64)
     parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
-    full = np.full(n, 4096, np.uint64)
+    full = np.full(n, L, np.uint64)
     odd_lens, odd_offs = full.copy(), offs.copy()
     pick = rng.choice(n, size=n // 20, replace=False)
-    odd_lens[pick] = rng.choice(np.array([0, 1, 4095, 4097, 8192], np.uint64), size=pick.size)
+    odd_lens[pick] = rng.choice(np.array([0, 1, L - 1, L + 1, 2 * L], np.uint64), size=pick.size)
     odd_offs[pick[::3]] += np.uint64(5)
     cases = {"full": (offs, full), "odd": (odd_offs, odd_lens)}
     prepared = {}
