@@ -4734,7 +4734,15 @@ static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint
     const size_t items = R == 1 ? n / 2 : n;  // pairs of 4 KiB fragments, or fragments
     const size_t span = R == 1 ? 2 * kRowBytes : (size_t)R * kRowBytes;
     if (items > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t fpw = pick_regular_fpw(items, span);
+    static const uint32_t fpw_env = [] {  // (A/B knob LAMPI_DESC_FPW: items per wave)
+        const char *e = std::getenv("LAMPI_DESC_FPW");
+        return e ? (uint32_t)std::atoi(e) : 0u;
+    }();
+    uint32_t fpw = pick_regular_fpw(items, span);
+    if (fpw_env) {
+        fpw = fpw_env;
+        while (fpw > 1 && (size_t)kWaves * fpw * 512 > items) fpw >>= 1;
+    }
     if (fpw > (R == 1 ? 32u : 64u)) return hipErrorInvalidValue;  // (a wave's descriptors live in its 64 lanes)
     uint32_t *list = nullptr, *left = nullptr, *next_left = nullptr;
     bool pooled = false;
