@@ -292,7 +292,9 @@ typedef struct lampi_frag_desc {
  * default the piece streams -- each workgroup's fragments cut into 64-byte pieces packed into full
  * 4 KiB rows, so mixed sizes keep every lane busy; with LAMPI_CSUM_ROWS_HINT (or the shape the
  * stream's earlier batches showed) long fragments one wavefront each on the table-light kernel (CRC)
- * or as row groups on short-lived workgroups (SUM); 1,024-65,536 fragments without a hint split by
+ * or as row groups on short-lived workgroups (SUM); batches the library has seen to hold equal fragments
+ * of 1-7 whole 4 KiB rows at 16-byte-aligned addresses on the message kernel's schedule (CRC; fragments
+ * of another shape in such a batch are found and checksummed by a second launch); 1,024-65,536 fragments without a hint split by
  * size class (CRC); under 256 fragments without a hint every fragment runs as row groups sized to the
  * launch (a few large fragments no longer sit on one workgroup each; LAMPI_CSUM_ROWS_HINT(1) keeps the
  * count split for batches known to hold small fragments).  Results never depend on the schedule.
