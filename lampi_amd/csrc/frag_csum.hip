@@ -4976,16 +4976,7 @@ static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out
     bool pooled = false;
     hipError_t e = stream_scratch(s, n * W * sizeof(uint32_t), (void **)&groups, &pooled);
     if (e != hipSuccess) return e;
-    static const int grp_threads = [] {  // (A/B knob LAMPI_SUM_GRP_THREADS: 256-thread group workgroups)
-        const char *e = std::getenv("LAMPI_SUM_GRP_THREADS");
-        return e ? std::atoi(e) : kSumWgThreads;
-    }();
-    if (grp_threads == 256)
-        hipLaunchKernelGGL((sum_copy_wg_kernel<GroupSource<Src>, 256>),
-                           dim3((unsigned)std::min<size_t>(n * W, kMaxWgGrid)), dim3(256), 0, s, GroupSource<Src>{src, W},
-                           n * W, groups);
-    else
-        launch_sum_copy(GroupSource<Src>{src, W}, n * W, groups, s);
+    launch_sum_copy(GroupSource<Src>{src, W}, n * W, groups, s);  // (256-thread groups: receive 72.5 -> 63%)
     e = hipGetLastError();
     if (e == hipSuccess) {
         uint32_t G = 1;
