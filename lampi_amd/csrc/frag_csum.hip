@@ -353,6 +353,26 @@ struct IsSparse : std::false_type {};
 template <>
 struct IsSparse<SparseDescSource> : std::true_type {};
 
+// A size class of a read-only CRC descriptor batch (config C's partition): entry i of
+// the class is descriptor idx[i]; entries at or past *count (the partition kernel's, on the device) read
+// as not this class's (aux = 1, nothing stored).  emit stores out[idx[i]].
+struct ListSource {
+    static constexpr bool kCopy = false;
+    static constexpr bool kPhase = false;
+    const lampi_frag_desc *d;
+    const uint32_t *idx;
+    const uint32_t *count;
+    __device__ FragInfo get(size_t i) const {
+        if (i >= *count) return {nullptr, 0u, 0u, nullptr, 0u, 1u};
+        const lampi_frag_desc x = d[idx[i]];
+        return {(gbyte *)(uintptr_t)x.addr, x.length, x.partial, nullptr, 0u};
+    }
+};
+template <class S>
+struct IsList : std::false_type {};
+template <>
+struct IsList<ListSource> : std::true_type {};
+
 template <class S>
 struct IsRecv : std::false_type {};
 template <>
@@ -466,6 +486,10 @@ __device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v, 
     }
     if constexpr (IsSplit<Src>::value)
         if (fi.aux) return;  // the other launch's fragment
+    if constexpr (IsList<Src>::value) {  // a size class: entry f is descriptor idx[f]
+        if (!fi.aux) out[src.idx[f]] = v;
+        return;
+    }
     if constexpr (std::is_same<Src, RecvCopyOnlySource>::value) v = 0;  // no checksum with checksumming off
     out[f] = v;
     if constexpr (IsRecv<Src>::value) src.verdict(f, v, fi);
@@ -1883,6 +1907,11 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
         }
     }
     size_t base = (size_t)blockIdx.x * fpg;
+    if constexpr (IsList<Src>::value) {  // a size class: the launch is sized for the whole batch
+        const size_t c = min(n, (size_t)*src.count);
+        if (base >= c) return;
+        n = c;
+    }
     uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
     if constexpr (IsSeg<Src>::value) {  // the plan's workgroups: plan[0] of them, segments [plan[1+i], plan[2+i])
         const uint32_t g = plan[0];
@@ -2680,7 +2709,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_light_frag_copy_kernel(const Src
     FragInfo fi{nullptr, 0u, 0u, nullptr, 0u};
     if (f < n) fi = src.get(f);
     LightFrag F;
-    F.init(fi, f < n && !(IsSplit<Src>::value && fi.aux), W, g);
+    F.init(fi, f < n && !((IsSplit<Src>::value || IsList<Src>::value) && fi.aux), W, g);
     if constexpr (IsRecv<Src>::value)  // row groups: the join kernel gives every verdict, this launch zeroes them
         if (W > 1u && lane == 0u && f < n && g == 0u) zero_verdict_words(src, f);
     u32x4 d[4];
@@ -2688,7 +2717,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_light_frag_copy_kernel(const Src
     // the first row's loads before the table staging (after it: 4 KiB copies 73 -> 66%, profiles/r04/late_loads_ab.txt)
     F.load_row(lane, F.r0, F.live, d, o, F.half);  // (an empty or dead wave's descriptor reads nothing but zeros)
     const u32x4 head = F.load_head();
-    if constexpr (IsSplit<Src>::value || IsSparse<Src>::value)  // the size split's light launch: most workgroups
+    if constexpr (IsSplit<Src>::value || IsSparse<Src>::value || IsList<Src>::value)  // the size split's light launch: most workgroups
         if (!__syncthreads_or(F.live)) return;  // hold no fragment of its class and leave before staging the tables
     build_slices_light<64 * kWv>(reinterpret_cast<char *>(lds), bs);
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[min(t, kNibPieces - 1)] = nib;
@@ -4722,6 +4751,61 @@ static hipError_t launch_row_segments(const lampi_frag_desc *d, size_t n, uint32
 // launches concurrently on a forked stream measured worse (GM 67-68%).
 constexpr size_t kSplitMin = 1024, kSplitMax = 65536;
 
+// Size-class partition of a large mixed read-only CRC batch (VERDICT r4 item 1, A/B knob LAMPI_CRC_PARTITION =
+// d: at most n / d entries in the large class): partition_kernel compacts the descriptor indices of the
+// 8-16-row fragments (split_large) into list A -- up to its capacity -- and the rest into list B (a wave's
+// ballot, one atomicAdd per list per wave); the table-light kernel then walks list A one wave per
+// fragment (its grid is list A's capacity; workgroups past the count leave before staging tables) and the
+// piece streams take list B (grid for the whole batch; workgroups past the count leave at once).
+__global__ void __launch_bounds__(256) partition_kernel(const lampi_frag_desc *__restrict__ d, size_t n,
+                                                       uint32_t capA, uint32_t *__restrict__ idxA,
+                                                       uint32_t *__restrict__ idxB, uint32_t *cnt) {
+    const size_t f = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool valid = f < n;
+    const bool large = valid && split_large(d[f].length);
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint64_t mA = __ballot(large);
+    uint32_t a0 = 0u;
+    if (lane == 0 && mA) a0 = atomicAdd(&cnt[0], (uint32_t)__popcll(mA));
+    a0 = (uint32_t)__shfl((int)a0, 0);
+    const uint32_t ra = a0 + (uint32_t)__popcll(mA & below);
+    const bool toA = large && ra < capA;
+    const bool toB = valid && !toA;
+    const uint64_t mB = __ballot(toB);
+    uint32_t b0 = 0u;
+    if (lane == 0 && mB) b0 = atomicAdd(&cnt[1], (uint32_t)__popcll(mB));
+    b0 = (uint32_t)__shfl((int)b0, 0);
+    if (toA) idxA[ra] = (uint32_t)f;
+    if (toB) idxB[b0 + (uint32_t)__popcll(mB & below)] = (uint32_t)f;
+}
+
+static hipError_t launch_crc_desc_partition(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
+                                            hipStream_t s, uint32_t div) {
+    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t capA = (uint32_t)std::min<size_t>(n, std::max<size_t>(1024, n / div));
+    uint32_t *scratch = nullptr;
+    bool pooled = false;
+    hipError_t e = stream_scratch(s, ((size_t)capA + n + 2) * sizeof(uint32_t), (void **)&scratch, &pooled);
+    if (e != hipSuccess) return e;
+    uint32_t *cnt = scratch, *idxA = scratch + 2, *idxB = idxA + capA;
+    e = hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(partition_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, capA, idxA, idxB,
+                           cnt);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = launch_crc_light_frag_copy(ListSource{d, idxA, cnt}, capA, img, out, s, 1u);
+    if (e == hipSuccess) {
+        const uint32_t fpg = frags_per_wg(n);
+        hipLaunchKernelGGL((crc_stream_kernel<ListSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
+                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, ListSource{d, idxB, cnt + 1}, n, fpg, img, out,
+                           nullptr);
+        e = hipGetLastError();
+    }
+    return scratch_done(s, scratch, pooled, e);
+}
+
 // Read-only CRC descriptor batches the census saw as equal whole-row fragments (R rows) at 16-byte-aligned
 // addresses: crc_regular_kernel<kDesc> on config B's schedule -- 4 KiB fragments in pairs (two chains per
 // wave, each reading a pair in turn; an odd last fragment on the table-light kernel), longer ones one per
@@ -4819,6 +4903,11 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
                                           rows_hint <= kSegRows ? 1u : (rows_hint + kLightRoRows - 1) / kLightRoRows);
     if (rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<false, kStreamWv, kStreamCap>(d, n, out, img, s, rows_hint);
+    static const uint32_t part_div = [] {  // (A/B knob LAMPI_CRC_PARTITION, above)
+        const char *e = std::getenv("LAMPI_CRC_PARTITION");
+        return e ? (uint32_t)std::atoi(e) : 0u;
+    }();
+    if (part_div && rows_hint <= 1 && n > kSplitMax) return launch_crc_desc_partition(d, n, out, img, s, part_div);
     if (n >= kSplitMin && n <= kSplitMax) {  // both size classes, one launch each (SplitDescSource)
         const uint32_t fpg = frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<SplitDescSource<false>, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
