@@ -4795,6 +4795,8 @@ static hipError_t launch_crc_desc_partition(const lampi_frag_desc *d, size_t n, 
                            cnt);
         e = hipGetLastError();
     }
+    // (the list-A launch on a forked stream, concurrent with list B's, took the same 713 us per call:
+    // profiles/r05/configC_partition_ab.txt)
     if (e == hipSuccess) e = launch_crc_light_frag_copy(ListSource{d, idxA, cnt}, capA, img, out, s, 1u);
     if (e == hipSuccess) {
         const uint32_t fpg = frags_per_wg(n);
