@@ -5069,6 +5069,7 @@ static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out
     if (e != hipSuccess) return e;
     // (128 threads per group measured against 256 -- GM receive 72.5 -> 63% -- and a wave per group, four to a
     // workgroup -- 72.5 -> 62.4%)
+    // (two or four groups per workgroup, grid-stride: GM receive 72.5 -> 71.2 / 69.6%)
     launch_sum_copy(GroupSource<Src>{src, W}, n * W, groups, s);
     e = hipGetLastError();
     if (e == hipSuccess) {
