@@ -4869,11 +4869,15 @@ static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint
 // one-row shape would bring the 100x case back; the caller's LAMPI_CSUM_ROWS_HINT picks the best schedule
 // (one 64 MiB fragment: 168 us as groups, 55 us with the hint).  A/B knob LAMPI_SMALL_BATCH = the item
 // target (0: the count split).
-static uint32_t small_batch_groups(size_t n) {
+static uint32_t small_batch_groups(size_t n, hipStream_t s) {
     static const size_t target = [] {
         const char *e = std::getenv("LAMPI_SMALL_BATCH");
         return e ? (size_t)std::atoll(e) : (size_t)4096;
     }();
+    // graph captures keep the count split: the groups' scratch would be a pooled allocation inside the graph
+    // (bench.py --latency: a replayed one-descriptor call 6.9 -> 32 us)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return 1u;
     uint32_t W = 1;
     while ((size_t)n * W < target && W < 4096u) W <<= 1;
     return W;
@@ -4884,8 +4888,10 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (plan && n <= kPlanMax) return launch_planned<false, kStreamWv, kStreamCap>(d, n, out, img, s);
-    if (rows_hint == 0 && n < kShapeMin && small_batch_groups(n) > 1)  // (1: the caller's pieces, count split)
-        return launch_crc_light_frag_copy(SparseDescSource{{d}}, n, img, out, s, small_batch_groups(n));
+    if (rows_hint == 0 && n < kShapeMin) {  // (1: the caller's pieces, count split)
+        const uint32_t W = small_batch_groups(n, s);
+        if (W > 1) return launch_crc_light_frag_copy(SparseDescSource{{d}}, n, img, out, s, W);
+    }
     bool whole = false;
     const uint32_t given = rows_hint;
     rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, 1u, nullptr, &whole);
@@ -5222,8 +5228,10 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     (void)grid;
     if (n == 0) return hipSuccess;
     if (img && plan && n <= kPlanMax) return launch_planned<true, kSumWv, kSumCap>(d, n, out, img, s);
-    if (img && rows_hint == 0 && n < kShapeMin && small_batch_groups(n) > 1)  // (small batches: as launch_crc_desc)
-        return launch_sum_copy_groups(DescSource{d}, n, out, s, small_batch_groups(n));
+    if (img && rows_hint == 0 && n < kShapeMin) {  // (small batches: as launch_crc_desc)
+        const uint32_t W = small_batch_groups(n, s);
+        if (W > 1) return launch_sum_copy_groups(DescSource{d}, n, out, s, W);
+    }
     bool one_row = false;
     if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, 2u, &one_row);
     if (img && rows_hint > 1) {
@@ -5281,7 +5289,8 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
         return e ? (size_t)std::atoll(e) : ~(size_t)0;
     }();
     const uint32_t R = (uint32_t)std::min<size_t>((frag_len + kRowBytes - 1) / kRowBytes, 0xFFFFFFFFu);
-    if (msg_wg && frag_len <= msg_max && n >= 256 && R > 1 && img) {
+    if (msg_wg && frag_len <= msg_max && (n >= 256 || R > 8) && R > 1 && img) {  // (few large fragments too:
+        // 16 x 16 MiB on the regular kernel, one fragment per chain, read 1.9%)
         // fragments over one row: the read-only descriptors' schedule (sum_ro_groups), as one workgroup
         // per fragment in batches under 4,096 fragments ran a single round of too few workgroups (1 MiB x 1,024
         // 74.6 -> 46.7%, profiles/r05/sum_ro_sched_ab.txt)

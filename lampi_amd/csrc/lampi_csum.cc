@@ -538,7 +538,8 @@ int lampi_frag_csum64_batch(const lampi_frag_desc *d_descs, size_t n, uint64_t *
 
 int lampi_frag_csum_batch(const lampi_frag_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
     const bool by_bytes = (mode & LAMPI_CSUM_BY_BYTES) != 0;
-    const uint32_t rows_hint = std::max(1u, LAMPI_CSUM_ROWS_HINT_OF(mode));
+    // (0: no hint -- small batches then run as row groups; 1: the caller's one-row hint keeps the count split)
+    const uint32_t rows_hint = LAMPI_CSUM_ROWS_HINT_OF(mode);
     mode &= ~(LAMPI_CSUM_BY_BYTES | LAMPI_CSUM_ROWS_HINT_MASK);
     if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;

@@ -450,6 +450,15 @@ def test_descriptor_small_batch_row_groups(cuda, oracle, case, mode):
     want = oracle.desc_batch(host, offs, lens.astype(np.uint32), parts.astype(np.uint32) if mode == 0 else None, mode)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
+    if case == "one_64mib":  # the schedule itself: ~0.17 ms (CRC) / 0.03 ms (SUM) as row groups, 3.0 / 1.8 ms on
+        # the count split (one workgroup for the whole fragment) -- a 1.5 ms bound catches a fall-back
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            dv.frag_csum_batch(descs, mode=mode)
+        e1.record()
+        torch.cuda.synchronize()
+        assert e0.elapsed_time(e1) / 5 < 1.5, e0.elapsed_time(e1) / 5
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
