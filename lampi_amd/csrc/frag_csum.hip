@@ -4379,7 +4379,8 @@ struct BatchShape {
     uint32_t rmin, rmax;  // fewest / most rows (4 KiB) among them
     uint32_t nhalf;    // how many were at most 2 KiB
     uint32_t nwhole;   // how many were whole 4 KiB rows (> 0 bytes) at a 16-byte-aligned address
-    uint32_t pad[2];
+    uint32_t nmis;     // how many were 1-2 KiB and ended off the 16-byte grid
+    uint32_t n12k;     // how many were 1-2 KiB
 };
 constexpr int kShapeSlots = 8;  // shape records per (thread, device, stream): descriptor arrays remembered
 constexpr int64_t kLeftBytes = 256;
@@ -4562,7 +4563,7 @@ template <class Src>
 __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, BatchShape *rec, uint32_t seq) {
     const uint32_t l = threadIdx.x;
     const uint32_t m = (uint32_t)min<size_t>(n, 64);
-    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u, full = 0u;
+    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u, full = 0u, mis = 0u, k12 = 0u;
     if (l < m) {
         const FragInfo fi = src.get((size_t)l * n / m);
         const uint32_t R = (uint32_t)(((uint64_t)fi.len + kRowBytes - 1) / kRowBytes);
@@ -4570,12 +4571,16 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         rmax = R;
         half = fi.len <= (uint32_t)kRowBytes / 2u ? 1u : 0u;
         full = fi.len != 0u && fi.len % (uint32_t)kRowBytes == 0u && ((uintptr_t)fi.addr & 15u) == 0 ? 1u : 0u;
+        k12 = fi.len > 1024u && fi.len <= 2048u ? 1u : 0u;
+        mis = k12 && (((uintptr_t)fi.addr + fi.len) & 15u) != 0 ? 1u : 0u;
     }
     for (int o = 32; o >= 1; o >>= 1) {
         rmin = min(rmin, (uint32_t)__shfl_xor((int)rmin, o));
         rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o));
         half += (uint32_t)__shfl_xor((int)half, o);
         full += (uint32_t)__shfl_xor((int)full, o);
+        mis += (uint32_t)__shfl_xor((int)mis, o);
+        k12 += (uint32_t)__shfl_xor((int)k12, o);
     }
     if (l == 0) {
         volatile BatchShape *r = rec;
@@ -4584,6 +4589,8 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         r->rmax = rmax;
         r->nhalf = half;
         r->nwhole = full;
+        r->nmis = mis;
+        r->n12k = k12;
         __threadfence_system();
         r->seq = seq;
     }
@@ -4603,7 +4610,7 @@ template <class Src>
 static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int kind, uint32_t rows_hint,
                                   bool *pairs = nullptr, uint32_t **nhalf_dev = nullptr,
                                   uint32_t min_rows = kShapeRows, bool *one_row = nullptr,
-                                  bool *full_rows = nullptr) {
+                                  bool *full_rows = nullptr, bool pairs_misaligned_only = false) {
     if (pairs) *pairs = false;
     if (one_row) *one_row = false;
     if (full_rows) *full_rows = false;
@@ -4651,7 +4658,8 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     uint32_t W = rows_hint;
     const uint32_t q0 = v->seq;
     std::atomic_thread_fence(std::memory_order_acquire);  // the fields are read after the first seq ...
-    const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf, nwhole = v->nwhole;
+    const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf, nwhole = v->nwhole,
+                   nmis = v->nmis, n12k = v->n12k;
     std::atomic_thread_fence(std::memory_order_acquire);  // ... and before the second (a seqlock read)
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= min_rows && rmax <= 2 * rmin) W = rmax;
@@ -4659,7 +4667,9 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
         // every sampled fragment the same whole number of rows at a 16-byte-aligned address (*full_rows: the
         // rows, W the most rows as above)
         if (full_rows && nwhole == sampled && rmin == rmax) *full_rows = true;
-        if (pairs && nhalf == sampled && !slot.pair_broken) {  // every sampled fragment at most 2 KiB: two per wave
+        if (pairs && nhalf == sampled && !slot.pair_broken &&
+            (!pairs_misaligned_only || (n12k == sampled && 4 * nmis >= sampled))) {  // every sampled fragment at
+            // most 2 KiB: two per wave (read-only: 1-2 KiB each, a quarter or more ending off the 16-byte grid)
             void *dp = nullptr;
             if (nhalf_dev && hipHostGetDevicePointer(&dp, rec, 0) == hipSuccess) {
                 *pairs = true;
@@ -4894,9 +4904,17 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         const uint32_t W = small_batch_groups(n, s);
         if (W > 1) return launch_crc_light_frag_copy(SparseDescSource{{d}}, n, img, out, s, W);
     }
-    bool whole = false;
+    bool whole = false, pairs = false;
+    uint32_t *nhalf = nullptr;
     const uint32_t given = rows_hint;
-    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, 1u, nullptr, &whole);
+    // read-only: two fragments per wave only for 1-2 KiB fragments ending off the 16-byte grid (IB's 1,976 B), where
+    // the piece streams take their five-load variant (profiles/r05/crc_ro_pairs_ab.txt)
+    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &pairs, &nhalf, 1u, nullptr, &whole, true);
+    static const bool ro_pairs = [] {  // (A/B knob LAMPI_CRC_RO_PAIRS=0: read-only IB-sized batches on the piece streams)
+        const char *e = std::getenv("LAMPI_CRC_RO_PAIRS");
+        return !(e && e[0] == '0');
+    }();
+    if (pairs && ro_pairs) return launch_crc_light_pair_copy(DescSource{d}, n, img, out, s, nhalf);
     // batches of equal whole-row fragments of 1-7 rows on the regular kernel (profiles/r05/crc_desc_pairs_ab.txt:
     // 4 KiB 76.4-77.8 -> 80.3-80.4%, 8 KiB 74.3 -> 77.8%, 16 KiB 74.7 -> 79.2%, 28 KiB 70.4 -> 75.4%; from 8 rows
     // the table-light kernel stays ahead, 32 KiB 81 against 73%, 64 KiB 80 against 67%).  A/B knob
@@ -4977,6 +4995,12 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     // 10.5 -> 80.9% (the regular kernel's chains are fragments: 256 of them starve the grid), and of
     // non-whole-row 65,552-131,056 B on the framed regular kernel (removed) 71-76.5 -> 76-82%.
     const size_t R = (frag_len + kRowBytes - 1) / kRowBytes;
+    static const bool ro_pairs = [] {  // (A/B knob LAMPI_CRC_RO_PAIRS=0, as launch_crc_desc)
+        const char *e = std::getenv("LAMPI_CRC_RO_PAIRS");
+        return !(e && e[0] == '0');
+    }();
+    if (ro_pairs && frag_len > 1024 && frag_len <= kRowBytes / 2 && (frag_len & 15u) != 0 && n >= kShapeMin)
+        return launch_crc_light_pair_copy(MsgSource{base, msg_len, frag_len, partial}, n, img, out, s, nullptr);
     if (crc_light_msg(frag_len, msg_len))
         return launch_crc_light_frag_copy(MsgSource{base, msg_len, frag_len, partial}, n, img, out, s,
                                           R <= kSegRows ? 1u : (uint32_t)((R + kLightRoRows - 1) / kLightRoRows));
