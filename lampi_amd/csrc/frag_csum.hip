@@ -5259,7 +5259,20 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         if (W > 1) return launch_sum_copy_groups(DescSource{d}, n, out, s, W);
     }
     bool one_row = false;
-    if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, nullptr, nullptr, 2u, &one_row);
+    bool half = false;  // (every sampled fragment at most 2 KiB)
+    uint32_t *nh = nullptr;
+    if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &half, &nh, 2u, &one_row);
+    // batches the census saw as all <= 2 KiB fragments: one fragment per wave, four to a workgroup
+    // (sum_copy_waves_kernel, IB's SUM copies' schedule; profiles/r05/sum_ro_waves_ab.txt: 1,976 B 45.5 -> 69.5%,
+    // 1 KiB 35.6 -> 64.3%, 2 KiB 58.5 -> 80.4%, 256 B 10.2 -> 20.8%).  A/B knob LAMPI_SUM_RO_WAVES=0: off.
+    static const bool ro_waves = [] {
+        const char *e = std::getenv("LAMPI_SUM_RO_WAVES");
+        return !(e && e[0] == '0');
+    }();
+    if (img && ro_waves && half && rows_hint <= 1) {
+        launch_sum_copy(DescSource{d}, n, out, s, true);
+        return hipGetLastError();
+    }
     if (img && rows_hint > 1) {
         const uint32_t W = sum_ro_groups(n, rows_hint);
         if (W <= 1) {
@@ -5327,6 +5340,15 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
             return hipGetLastError();
         }
         if (W < 0xFFFFFFFFu) return launch_sum_copy_groups(src, n, out, s, W);
+    }
+    // fragments of at most 2 KiB one per wave (as launch_sum_desc: 1,976 B 51.2 -> 74.9%, 2 KiB 68 -> 84.2%)
+    static const bool ro_waves = [] {
+        const char *e = std::getenv("LAMPI_SUM_RO_WAVES");
+        return !(e && e[0] == '0');
+    }();
+    if (ro_waves && frag_len <= kRowBytes / 2 && n >= 256) {
+        launch_sum_copy(MsgSource{base, msg_len, frag_len, 0u}, n, out, s, true);
+        return hipGetLastError();
     }
     if (msg_wg && frag_len <= msg_max && n >= 256 && R <= 1) {
         hipLaunchKernelGGL(sum_copy_wg_kernel<MsgSource>,

@@ -318,12 +318,13 @@ def test_learned_whole_row_descriptors(cuda, oracle, L):
             assert bad.size == 0, (i, k, bad[:8].tolist())
 
 
-def test_learned_ib_pairs_read_only(cuda, oracle):
-    """Read-only CRC batches of 1-2 KiB fragments ending off the 16-byte grid (IB's 1,976-byte payloads) run
-    two to a wave on the table-light pair kernel once the census has seen them (round 5).  The same
-    descriptor array then holds fragments the pairs cannot take (0 / 8 / 2,049 / 4,096 / 9,000 bytes) under the
-    stale shape: the pair kernel lists their waves and the leftover launch checksums them.  Every call vs
-    the oracle."""
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_learned_ib_pairs_read_only(cuda, oracle, mode):
+    """Read-only batches of 1-2 KiB fragments (IB's 1,976-byte payloads) once the census has seen them (round
+    5): CRC two to a wave on the table-light pair kernel (fragments ending off the 16-byte grid), SUM one per
+    wave (sum_copy_waves_kernel).  The same descriptor array then holds fragments of other sizes (0 / 8 /
+    2,049 / 4,096 / 9,000 bytes) under the stale shape: CRC lists their waves for the leftover launch, SUM's
+    wave walks any length.  Every call vs the oracle."""
     import torch
 
     dv = _dv()
@@ -340,13 +341,14 @@ def test_learned_ib_pairs_read_only(cuda, oracle):
     pick = rng.choice(n, size=n // 10, replace=False)
     odd[pick] = rng.choice(np.array([0, 8, 2049, 4096, 9000], np.uint64), size=pick.size)
     prepared = {k: (dv.make_descs(base, offs, ln, parts),
-                    oracle.desc_batch(host, offs, ln.astype(np.uint32), parts.astype(np.uint32), 0))
+                    oracle.desc_batch(host, offs, ln.astype(np.uint32), parts.astype(np.uint32) if mode == 0 else None,
+                                      mode))
                 for k, ln in (("ib", ib), ("odd", odd))}
     descs = prepared["ib"][0].clone()
     stream = torch.cuda.Stream(device=cuda)
     with torch.cuda.stream(stream):
         for i, k in enumerate(["ib"] * 20 + ["odd"] * 4 + ["ib"] * 3):
             descs.copy_(prepared[k][0])
-            got = dv.as_u32(dv.frag_csum_batch(descs, mode=0, stream=stream))
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, stream=stream))
             bad = np.nonzero(got != prepared[k][1])[0]
             assert bad.size == 0, (i, k, bad[:8].tolist())
