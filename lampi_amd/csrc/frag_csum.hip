@@ -4327,7 +4327,11 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
 // profiles/r02_bigfrag_ab.txt).
 constexpr uint32_t kCrcFpg = 96;
 static uint32_t frags_per_wg(size_t n, size_t frag_len = 0) {
-    uint32_t fpg = kCrcFpg;
+    static const uint32_t fpg_env = [] {  // (A/B knob LAMPI_STREAM_FPG: fragments per workgroup, <= 256)
+        const char *e = std::getenv("LAMPI_STREAM_FPG");
+        return e ? (uint32_t)std::min(256, std::max(1, std::atoi(e))) : 0u;
+    }();
+    uint32_t fpg = fpg_env ? fpg_env : kCrcFpg;
     while (fpg > 3 && n / fpg < 256) fpg >>= 1;
     return spread_fpw(fpg, n, 1, frag_len);
 }
@@ -4610,7 +4614,9 @@ template <class Src>
 static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int kind, uint32_t rows_hint,
                                   bool *pairs = nullptr, uint32_t **nhalf_dev = nullptr,
                                   uint32_t min_rows = kShapeRows, bool *one_row = nullptr,
-                                  bool *full_rows = nullptr, bool pairs_misaligned_only = false) {
+                                  bool *full_rows = nullptr, bool pairs_misaligned_only = false,
+                                  bool *all_half = nullptr) {
+    if (all_half) *all_half = false;
     if (pairs) *pairs = false;
     if (one_row) *one_row = false;
     if (full_rows) *full_rows = false;
@@ -4667,6 +4673,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
         // every sampled fragment the same whole number of rows at a 16-byte-aligned address (*full_rows: the
         // rows, W the most rows as above)
         if (full_rows && nwhole == sampled && rmin == rmax) *full_rows = true;
+        if (all_half && nhalf == sampled) *all_half = true;  // every sampled fragment at most 2 KiB
         if (pairs && nhalf == sampled && !slot.pair_broken &&
             (!pairs_misaligned_only || (n12k == sampled && 4 * nmis >= sampled))) {  // every sampled fragment at
             // most 2 KiB: two per wave (read-only: 1-2 KiB each, a quarter or more ending off the 16-byte grid)
@@ -4909,7 +4916,8 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     const uint32_t given = rows_hint;
     // read-only: two fragments per wave only for 1-2 KiB fragments ending off the 16-byte grid (IB's 1,976 B), where
     // the piece streams take their five-load variant (profiles/r05/crc_ro_pairs_ab.txt)
-    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &pairs, &nhalf, 1u, nullptr, &whole, true);
+    bool small = false;
+    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &pairs, &nhalf, 1u, nullptr, &whole, true, &small);
     static const bool ro_pairs = [] {  // (A/B knob LAMPI_CRC_RO_PAIRS=0: read-only IB-sized batches on the piece streams)
         const char *e = std::getenv("LAMPI_CRC_RO_PAIRS");
         return !(e && e[0] == '0');
@@ -4936,7 +4944,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         return e ? (uint32_t)std::atoi(e) : 0u;
     }();
     if (part_div && rows_hint <= 1 && n > kSplitMax) return launch_crc_desc_partition(d, n, out, img, s, part_div);
-    if (n >= kSplitMin && n <= kSplitMax) {  // both size classes, one launch each (SplitDescSource)
+    if (n >= kSplitMin && n <= kSplitMax && !small) {  // both size classes, one launch each (SplitDescSource)
         const uint32_t fpg = frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<SplitDescSource<false>, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
                            frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, SplitDescSource<false>{d}, n, fpg, img, out,
@@ -4945,7 +4953,9 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         if (e != hipSuccess) return e;
         return launch_crc_light_frag_copy(SplitDescSource<true>{d}, n, img, out, s, 1u);
     }
-    const uint32_t fpg = frags_per_wg(n);
+    // batches of fragments of at most 2 KiB: the most fragments per workgroup, 256 (the table staging over more
+    // fragments; profiles/r05/stream_fpg_ab.txt: 64 B 5.4 -> 13.0%, 256 B 17.9 -> 36.3%, 1 KiB 50.8 -> 64.1%)
+    const uint32_t fpg = small && kFragsPerWg >= 256 && n / 256 >= 256 ? 256u : frags_per_wg(n);
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
                        frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
     return hipGetLastError();
@@ -5004,7 +5014,8 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     if (crc_light_msg(frag_len, msg_len))
         return launch_crc_light_frag_copy(MsgSource{base, msg_len, frag_len, partial}, n, img, out, s,
                                           R <= kSegRows ? 1u : (uint32_t)((R + kLightRoRows - 1) / kLightRoRows));
-    const uint32_t fpg = frags_per_wg(n, frag_len);
+    // fragments of at most 2 KiB: 256 per workgroup (as launch_crc_desc)
+    const uint32_t fpg = frag_len <= kRowBytes / 2 && n / 256 >= 256 ? 256u : frags_per_wg(n, frag_len);
     hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>), frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s,
                        MsgSource{base, msg_len, frag_len, partial}, n, fpg, img, out, nullptr);
     return hipGetLastError();
