@@ -5357,6 +5357,19 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
         const char *e = std::getenv("LAMPI_SUM_RO_WAVES");
         return !(e && e[0] == '0');
     }();
+    // messages of fragments up to 1 KiB: the SUM piece streams with 256 fragments per workgroup (many fragments
+    // share a row; profiles/r05/sum_tiny_ab.txt: 64 B 6.5 -> 19.8%, 256 B 22.8 -> 48.6%, 512 B 44.7 -> 67.6%,
+    // 1 KiB 70.2 -> 72.4%).  A/B knob LAMPI_SUM_TINY = the longest fragment taken (0: off).
+    static const uint32_t tiny_max = [] {
+        const char *e = std::getenv("LAMPI_SUM_TINY");
+        return e ? (uint32_t)std::atoi(e) : 1024u;
+    }();
+    if (img && frag_len <= tiny_max && n / 256 >= 256) {
+        hipLaunchKernelGGL((crc_stream_kernel<MsgSource, kStreamD, kStreamK, true, kSumWv, kSumCap>),
+                           frags_grid(n, 256), dim3(64 * kSumWv), 0, s, MsgSource{base, msg_len, frag_len, 0u}, n, 256u,
+                           img, out, nullptr);
+        return hipGetLastError();
+    }
     if (ro_waves && frag_len <= kRowBytes / 2 && n >= 256) {
         launch_sum_copy(MsgSource{base, msg_len, frag_len, 0u}, n, out, s, true);
         return hipGetLastError();
