@@ -4385,6 +4385,8 @@ struct BatchShape {
     uint32_t nwhole;   // how many were whole 4 KiB rows (> 0 bytes) at a 16-byte-aligned address
     uint32_t nmis;     // how many were 1-2 KiB and ended off the 16-byte grid
     uint32_t n12k;     // how many were 1-2 KiB
+    uint32_t n1k;      // how many were at most 1 KiB
+    uint32_t pad[3];
 };
 constexpr int kShapeSlots = 8;  // shape records per (thread, device, stream): descriptor arrays remembered
 constexpr int64_t kLeftBytes = 256;
@@ -4567,7 +4569,7 @@ template <class Src>
 __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, BatchShape *rec, uint32_t seq) {
     const uint32_t l = threadIdx.x;
     const uint32_t m = (uint32_t)min<size_t>(n, 64);
-    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u, full = 0u, mis = 0u, k12 = 0u;
+    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u, full = 0u, mis = 0u, k12 = 0u, k1 = 0u;
     if (l < m) {
         const FragInfo fi = src.get((size_t)l * n / m);
         const uint32_t R = (uint32_t)(((uint64_t)fi.len + kRowBytes - 1) / kRowBytes);
@@ -4576,6 +4578,7 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         half = fi.len <= (uint32_t)kRowBytes / 2u ? 1u : 0u;
         full = fi.len != 0u && fi.len % (uint32_t)kRowBytes == 0u && ((uintptr_t)fi.addr & 15u) == 0 ? 1u : 0u;
         k12 = fi.len > 1024u && fi.len <= 2048u ? 1u : 0u;
+        k1 = fi.len <= 1024u ? 1u : 0u;
         mis = k12 && (((uintptr_t)fi.addr + fi.len) & 15u) != 0 ? 1u : 0u;
     }
     for (int o = 32; o >= 1; o >>= 1) {
@@ -4585,6 +4588,7 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         full += (uint32_t)__shfl_xor((int)full, o);
         mis += (uint32_t)__shfl_xor((int)mis, o);
         k12 += (uint32_t)__shfl_xor((int)k12, o);
+        k1 += (uint32_t)__shfl_xor((int)k1, o);
     }
     if (l == 0) {
         volatile BatchShape *r = rec;
@@ -4595,6 +4599,7 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         r->nwhole = full;
         r->nmis = mis;
         r->n12k = k12;
+        r->n1k = k1;
         __threadfence_system();
         r->seq = seq;
     }
@@ -4615,8 +4620,9 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
                                   bool *pairs = nullptr, uint32_t **nhalf_dev = nullptr,
                                   uint32_t min_rows = kShapeRows, bool *one_row = nullptr,
                                   bool *full_rows = nullptr, bool pairs_misaligned_only = false,
-                                  bool *all_half = nullptr) {
+                                  bool *all_half = nullptr, bool *all_1k = nullptr) {
     if (all_half) *all_half = false;
+    if (all_1k) *all_1k = false;
     if (pairs) *pairs = false;
     if (one_row) *one_row = false;
     if (full_rows) *full_rows = false;
@@ -4665,7 +4671,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     const uint32_t q0 = v->seq;
     std::atomic_thread_fence(std::memory_order_acquire);  // the fields are read after the first seq ...
     const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf, nwhole = v->nwhole,
-                   nmis = v->nmis, n12k = v->n12k;
+                   nmis = v->nmis, n12k = v->n12k, n1k = v->n1k;
     std::atomic_thread_fence(std::memory_order_acquire);  // ... and before the second (a seqlock read)
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= min_rows && rmax <= 2 * rmin) W = rmax;
@@ -4674,6 +4680,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
         // rows, W the most rows as above)
         if (full_rows && nwhole == sampled && rmin == rmax) *full_rows = true;
         if (all_half && nhalf == sampled) *all_half = true;  // every sampled fragment at most 2 KiB
+        if (all_1k && n1k == sampled) *all_1k = true;        // ... at most 1 KiB
         if (pairs && nhalf == sampled && !slot.pair_broken &&
             (!pairs_misaligned_only || (n12k == sampled && 4 * nmis >= sampled))) {  // every sampled fragment at
             // most 2 KiB: two per wave (read-only: 1-2 KiB each, a quarter or more ending off the 16-byte grid)
@@ -5272,7 +5279,19 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     bool one_row = false;
     bool half = false;  // (every sampled fragment at most 2 KiB)
     uint32_t *nh = nullptr;
-    if (img) rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &half, &nh, 2u, &one_row);
+    bool tiny = false;  // (every sampled fragment at most 1 KiB)
+    if (img)
+        rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &half, &nh, 2u, &one_row, nullptr, false,
+                                      nullptr, &tiny);
+    static const bool sum_tiny = [] {  // (A/B knob LAMPI_SUM_TINY=0, as launch_sum_msg)
+        const char *e = std::getenv("LAMPI_SUM_TINY");
+        return !(e && e[0] == '0');
+    }();
+    if (img && sum_tiny && tiny && rows_hint <= 1 && n / 256 >= 256) {  // (as launch_sum_msg: 256 per workgroup)
+        hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, true, kSumWv, kSumCap>),
+                           frags_grid(n, 256), dim3(64 * kSumWv), 0, s, DescSource{d}, n, 256u, img, out, nullptr);
+        return hipGetLastError();
+    }
     // batches the census saw as all <= 2 KiB fragments: one fragment per wave, four to a workgroup
     // (sum_copy_waves_kernel, IB's SUM copies' schedule; profiles/r05/sum_ro_waves_ab.txt: 1,976 B 45.5 -> 69.5%,
     // 1 KiB 35.6 -> 64.3%, 2 KiB 58.5 -> 80.4%, 256 B 10.2 -> 20.8%).  A/B knob LAMPI_SUM_RO_WAVES=0: off.
