@@ -44,11 +44,15 @@ enum lampi_csum_mode {
     LAMPI_CSUM_CRC32 = 0,   /* uicrc  */
     LAMPI_CSUM_SUM32 = 1,   /* uicsum */
     /* Checksumming off: a network whose doChecksum flag is false (mpirun -mf/-if/-qf nochecksum,
-     * src/run/Input.cc:1986-2067; gmState.doChecksum src/path/gm/state.h:140).  Accepted only by the
-     * delivery batches (lampi_copy_to_app_batch, lampi_chain_copy_to_app_batch and their host forms):
-     * the bytes are copied, the checksum output is 0 and every fragment is DataOK, as CopyFunction /
+     * src/run/Input.cc:1986-2067; gmState.doChecksum src/path/gm/state.h:140).  Accepted by the copying
+     * batches only.  Receive side (lampi_copy_to_app_batch, lampi_chain_copy_to_app_batch and their host
+     * forms): the bytes are copied, the checksum output is 0 and every fragment is DataOK, as CopyFunction /
      * nonContigCopyFunction and CheckData behave with checksumming off (src/path/gm/recvFrag.h:178-181,
-     * :198-199, :231-232). */
+     * :198-199, :231-232).  Send side (lampi_frag_bcopy_batch[_strided], lampi_msg_bcopy[_strided],
+     * lampi_chain_csum_batch[_strided], lampi_host_msg_bcopy): the bytes are copied (copylen of each
+     * descriptor) and the checksum output is NOT written -- it may be NULL --, as the sender's MEMCOPY_FUNC
+     * leaves dataChecksum unset (src/path/gm/sendFrag.cc:153-155, :185-187, :206-208);
+     * lampi_header_csum_batch_strided writes nothing either (no header checksum, :219-225). */
     LAMPI_CSUM_NONE = 2
 };
 
@@ -154,7 +158,8 @@ int lampi_host_msg_csum(const void *h_msg, size_t msg_len, size_t frag_len, size
  * h_out[i] = bcopy_uicrc / bcopy_uicsum of it (copylen = crclen = the fragment length), as the
  * send loop of gmPath::send does per fragment (src/path/gm/path.cc:98-176, sendFrag.cc:147-155).
  * The bytes written to the slots are exactly the bytes checksummed; no other byte of the ring
- * is touched.  h_ring must not overlap h_msg. */
+ * is touched.  h_ring must not overlap h_msg.  mode LAMPI_CSUM_NONE: the fragments are copied
+ * (through the same DMA pipeline, no kernel) and h_out is unused (may be NULL). */
 int lampi_host_msg_bcopy(const void *h_msg, size_t msg_len, size_t frag_len, size_t k_first, size_t k_count,
                          void *h_ring, size_t slot_stride, uint32_t partial, uint32_t *h_out, int mode);
 
@@ -329,12 +334,23 @@ typedef struct lampi_copy_desc {
 
 /* Fused copy + checksum per descriptor: d[i].dst gets the first copylen bytes of d[i].src
  * (no other destination byte is written) and out[i] the checksum bcopy_uicrc / bcopy_uicsum
- * would return.  One wavefront per fragment, every source byte read from HBM once.
+ * would return.  Every source byte is read from HBM once; the schedule follows the batch (one
+ * wavefront per fragment, row groups joined by a second launch for long fragments, two IB-sized
+ * fragments per wavefront; SUM one short-lived workgroup or one wavefront per fragment).
  * Replaces the per-fragment bcopy_uicrc/bcopy_uicsum of the send side
  * (src/path/gm/sendFrag.cc:147-155, ref src/util/MemFunctions.cc:1263-1321, 518-875) and
- * the receive-side CopyFunction (src/path/gm/recvFrag.h:165-205, copylen < crclen at :174). */
+ * the receive-side CopyFunction (src/path/gm/recvFrag.h:165-205, copylen < crclen at :174).
+ * mode LAMPI_CSUM_NONE: copies only (d_out unused, may be NULL). */
 int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d_out, int mode,
                            void *stream);
+
+/* As lampi_frag_bcopy_batch, with checksum i written to (char *)d_out + i*out_stride (d_out and out_stride
+ * 4-byte aligned, out_stride >= 4): the send step in place -- d_out = the first buffer's
+ * gmHeaderData.dataChecksum (@64 of the 72-byte header, src/path/gm/header.h:56-70), out_stride = the buffer
+ * size, as gmSendFragDesc::init stores it (src/path/gm/sendFrag.cc:149-151); other bytes of the records are
+ * not touched.  out_stride != 4 uses 4 * n bytes of stream-ordered scratch and a second, small launch. */
+int lampi_frag_bcopy_batch_strided(const lampi_copy_desc *d_descs, size_t n, void *d_out, size_t out_stride,
+                                   int mode, void *stream);
 
 /* Chained checksums over typemap pieces (non-contiguous datatypes).  Fragment f is the
  * concatenation of the checksummed ranges (max(copylen, csumlen) bytes at src) of pieces
@@ -351,6 +367,12 @@ int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d
 int lampi_chain_csum_batch(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first,
                            size_t nfrags, uint32_t *d_out, int mode, void *stream);
 
+/* As lampi_chain_csum_batch, with fragment f's checksum written to (char *)d_out + f*out_stride (as
+ * lampi_frag_bcopy_batch_strided: the typemap send's `headerp->dataChecksum = csum`,
+ * src/path/gm/sendFrag.cc:216).  mode LAMPI_CSUM_NONE: the pieces are copied, d_out is unused (may be NULL). */
+int lampi_chain_csum_batch_strided(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first,
+                                   size_t nfrags, void *d_out, size_t out_stride, int mode, void *stream);
+
 /* Fragments a contiguous device-resident message like lampi_msg_csum and copies fragment k
  * to d_dst + k*dst_stride (dst_stride >= frag_len; e.g. frag_len for a plain copy, or the
  * slot size of a staging ring) with its checksum fused: bcopy_uicrc / bcopy_uicsum of every
@@ -358,6 +380,13 @@ int lampi_chain_csum_batch(const lampi_copy_desc *d_pieces, size_t npieces, cons
  * Source and destination must not overlap. */
 int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_dst, size_t dst_stride,
                     uint32_t partial, uint32_t *d_out, int mode, void *stream);
+
+/* As lampi_msg_bcopy, with fragment k's checksum written to (char *)d_out + k*out_stride (as
+ * lampi_frag_bcopy_batch_strided): a GM send of one message into a ring of header + payload buffers is
+ * d_dst = first buffer + 72, dst_stride = out_stride = the buffer size, d_out = first buffer + 64.
+ * mode LAMPI_CSUM_NONE: copies only, d_out unused (may be NULL). */
+int lampi_msg_bcopy_strided(const void *d_msg, size_t msg_len, size_t frag_len, void *d_dst, size_t dst_stride,
+                            uint32_t partial, void *d_out, size_t out_stride, int mode, void *stream);
 
 /* Fragments a contiguous device-resident message the way the path layer does
  * (fragment k = bytes [k*frag_len, min((k+1)*frag_len, msg_len)),
@@ -379,6 +408,15 @@ int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t 
  * Senders: src/path/gm/sendFrag.cc:218-225, gm/recvFrag.cc:125-130, quadrics/sendFrag.h:876-879. */
 int lampi_header_csum_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen,
                             uint32_t word_count, uint32_t *d_out, int mode, void *stream);
+
+/* As lampi_header_csum_batch, with header i's value written to (char *)d_out + i*out_stride (4-byte aligned):
+ * the sender's `headerp->checksum = BasePath_t::headerChecksum(headerp, sizeof(gmHeader) - 4, GM_HDR_WORDS)`
+ * in place (src/path/gm/sendFrag.cc:218-225) is d_out = d_hdrs + 68, out_stride = stride, crclen 68 -- run
+ * after dataChecksum was stamped (lampi_frag_bcopy_batch_strided / lampi_msg_bcopy_strided on the same
+ * stream).  Each header's bytes are read before its own word is written; d_out + i*out_stride must not lie
+ * inside the checksummed bytes of another header.  mode LAMPI_CSUM_NONE: nothing is written. */
+int lampi_header_csum_batch_strided(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen,
+                                    uint32_t word_count, void *d_out, size_t out_stride, int mode, void *stream);
 
 /* Receiver header check (ref src/path/gm/path.cc:364-393): header i fails unless
  * CRC mode: uicrc(hdr_i, hdr_bytes) == 0 (the whole header including the stored checksum);

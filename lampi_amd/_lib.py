@@ -16,7 +16,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "lampi_csum.h")
 
 CRC32 = 0  # enum lampi_csum_mode (include/lampi_csum.h)
 SUM32 = 1
-NONE = 2  # checksumming off (doChecksum == false): the delivery batches only
+NONE = 2  # checksumming off (doChecksum == false): the copying batches only (send and receive)
 BY_BYTES = 0x100  # LAMPI_CSUM_BY_BYTES: byte-balanced descriptor batches (OR'ed into the mode)
 
 
@@ -108,6 +108,13 @@ PROTOTYPES = {
     "lampi_header_compare_batch": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, ctypes.c_uint32,
                                                   c_void_p, c_void_p, ctypes.c_int, c_void_p]),
     "lampi_frag_csum_batch_strided": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.c_int, c_void_p]),
+    "lampi_frag_bcopy_batch_strided": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.c_int, c_void_p]),
+    "lampi_msg_bcopy_strided": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, ctypes.c_uint32,
+                                               c_void_p, c_size_t, ctypes.c_int, c_void_p]),
+    "lampi_chain_csum_batch_strided": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_size_t,
+                                                      ctypes.c_int, c_void_p]),
+    "lampi_header_csum_batch_strided": (ctypes.c_int, [c_void_p, c_size_t, c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                                       c_void_p, c_size_t, ctypes.c_int, c_void_p]),
     "lampi_check_data_batch": (ctypes.c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_size_t, c_size_t, c_void_p,
                                               c_void_p, c_void_p]),
     "lampi_copy_to_app_batch": (ctypes.c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,

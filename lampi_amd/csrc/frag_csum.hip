@@ -140,6 +140,19 @@ struct CopySource {
     }
 };
 
+// A fused send copy with checksumming off (LAMPI_CSUM_NONE: doChecksum == false, ref
+// src/path/gm/sendFrag.cc:153-155, :185-187, :206-208 -- MEMCOPY_FUNC instead of bcopy_uicrc / bcopy_uicsum):
+// only the copylen bytes are read and copied; the SUM copy kernels run it and their sums go to scratch.
+struct CopyOnlySource {
+    static constexpr bool kCopy = true;
+    static constexpr bool kPhase = false;
+    const lampi_copy_desc *d;
+    __device__ FragInfo get(size_t f) const {
+        const lampi_copy_desc x = d[f];
+        return {(gbyte *)(uintptr_t)x.src, x.copylen, 0u, (uint8_t *)(uintptr_t)x.dst, x.copylen};
+    }
+};
+
 // host-path pieces of one chained 64-bit csum: partial = the piece's byte phase (0..7)
 struct PhaseDescSource {
     static constexpr bool kCopy = false;
@@ -3813,7 +3826,8 @@ __device__ __forceinline__ void stage_slices(uint32_t *S, const uint32_t *__rest
 // (so that CRC(header || stored) == 0), SUM mode the sum of word_count 32-bit words.
 __global__ void __launch_bounds__(256) header_csum_kernel(const uint8_t *__restrict__ hdrs, uint32_t n, size_t stride,
                                                           uint32_t crclen, uint32_t word_count, int mode,
-                                                          const uint32_t *__restrict__ img, uint32_t *__restrict__ out) {
+                                                          const uint32_t *__restrict__ img, uint8_t *out,
+                                                          size_t out_stride) {
     __shared__ uint32_t S[1024];
     if (mode == LAMPI_CSUM_CRC32) stage_slices(S, img);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3825,7 +3839,9 @@ __global__ void __launch_bounds__(256) header_csum_kernel(const uint8_t *__restr
     } else {
         for (uint32_t w = 0; w < word_count; ++w) v += *(guint *)(h + 4 * w);
     }
-    out[i] = v;
+    // (out_stride = stride, out = hdrs + 68: the sender's `headerp->checksum = headerChecksum(...)` in place,
+    // ref src/path/gm/sendFrag.cc:218-225 -- this thread read its header's bytes above, no other thread does)
+    *(uint32_t *)(out + (size_t)i * out_stride) = v;
 }
 
 // One bit per fragment, set when it FAILS (wave ballot -> two mask words), plus a count.
@@ -4475,12 +4491,16 @@ static hipError_t stream_scratch(hipStream_t s, size_t bytes, void **out, bool *
             if (e == hipSuccess) e = hipFree(slot.p);
             if (e != hipSuccess) return e;  // the old buffer stays in the slot, still valid
             g_scratch_bytes.fetch_sub((int64_t)slot.cap, std::memory_order_relaxed);
-            slot = {};
+            // only the buffer goes: the learned shapes, the pair counters and their state are not tied to its
+            // size (`slot = {}` here leaked the host-mapped shape records and the counters)
+            slot.p = nullptr;
+            slot.cap = 0;
         }
         const size_t want = std::max<size_t>(bytes + bytes / 4, 1u << 20);
         e = hipMalloc(&slot.p, want);
         if (e != hipSuccess) {
-            slot = {};
+            slot.p = nullptr;
+            slot.cap = 0;
             return e;
         }
         slot.cap = want;
@@ -4527,6 +4547,15 @@ static void reset_pair_counters(hipStream_t s) {
         (void)hipGetLastError();
         it->second.pair_broken = true;
     }
+}
+
+// Whether stream s may still take the pair counters (false once reset_pair_counters could not re-zero them):
+// schedules that list leftovers through them check this before they are chosen.
+static bool pair_counters_ok(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    auto it = t_scratch.slots.find({dev, s});
+    return it == t_scratch.slots.end() || !it->second.pair_broken;
 }
 
 void release_stream_scratch(hipStream_t s) {
@@ -4678,7 +4707,9 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
         if (one_row && rmin == 1u && rmax == 1u) *one_row = true;  // every sampled fragment one row (17 B-4 KiB)
         // every sampled fragment the same whole number of rows at a 16-byte-aligned address (*full_rows: the
         // rows, W the most rows as above)
-        if (full_rows && nwhole == sampled && rmin == rmax) *full_rows = true;
+        // (the whole-row path lists off-shape fragments through the pair counters: not on a stream whose counters
+        // could not be re-zeroed)
+        if (full_rows && nwhole == sampled && rmin == rmax && !slot.pair_broken) *full_rows = true;
         if (all_half && nhalf == sampled) *all_half = true;  // every sampled fragment at most 2 KiB
         if (all_1k && n1k == sampled) *all_1k = true;        // ... at most 1 KiB
         if (pairs && nhalf == sampled && !slot.pair_broken &&
@@ -5016,7 +5047,8 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
         const char *e = std::getenv("LAMPI_CRC_RO_PAIRS");
         return !(e && e[0] == '0');
     }();
-    if (ro_pairs && frag_len > 1024 && frag_len <= kRowBytes / 2 && (frag_len & 15u) != 0 && n >= kShapeMin)
+    if (ro_pairs && frag_len > 1024 && frag_len <= kRowBytes / 2 && (frag_len & 15u) != 0 && n >= kShapeMin &&
+        pair_counters_ok(s))
         return launch_crc_light_pair_copy(MsgSource{base, msg_len, frag_len, partial}, n, img, out, s, nullptr);
     if (crc_light_msg(frag_len, msg_len))
         return launch_crc_light_frag_copy(MsgSource{base, msg_len, frag_len, partial}, n, img, out, s,
@@ -5160,6 +5192,10 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
     if (!img) return hipErrorInvalidValue;  // the tables (CRC)
     bool pairs = false;
     uint32_t *nhalf = nullptr;
+    if (mode == LAMPI_CSUM_NONE) {  // copies only (out: the caller's scratch), the SUM copy schedules
+        rows_hint = learned_rows_hint(CopyOnlySource{d}, n, s, 3, rows_hint, &pairs, &nhalf, kShapeRowsSum);
+        return launch_sum_copy_groups(CopyOnlySource{d}, n, out, s, rows_hint, pairs);
+    }
     const bool crc = mode == LAMPI_CSUM_CRC32;
     rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, &pairs, &nhalf, crc ? kShapeRows : kShapeRowsSum);
     if (crc && pairs) return launch_crc_light_pair_copy(CopySource{d}, n, img, out, s, nhalf);
@@ -5506,10 +5542,10 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
 }
 
 hipError_t launch_header_csum(const uint8_t *hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
-                              int mode, const uint32_t *img, uint32_t *out, hipStream_t s) {
+                              int mode, const uint32_t *img, uint8_t *out, size_t out_stride, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(header_csum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, hdrs, (uint32_t)n, stride,
-                       crclen, word_count, mode, img, out);
+                       crclen, word_count, mode, img, out, out_stride);
     return hipGetLastError();
 }
 

@@ -44,7 +44,8 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
 // Regular batch: frag_len % 4096 == 0, base 16-byte aligned, n full fragments.
 hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
                               const uint32_t *img, int grid, hipStream_t s);
-// Fused copy + checksum (bcopy_uicrc / bcopy_uicsum per descriptor), mode = lampi_csum_mode.
+// Fused copy + checksum (bcopy_uicrc / bcopy_uicsum per descriptor), mode = lampi_csum_mode (NONE: copies only,
+// out = n words of scratch).
 // rows_hint (LAMPI_CSUM_ROWS_HINT): row groups per fragment, 1 = one wave (SUM: workgroup) walks every row
 hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, int mode, const uint32_t *img,
                              hipStream_t s, uint32_t rows_hint = 1);
@@ -60,7 +61,7 @@ hipError_t launch_copy_to_app(const lampi_recv_desc *d, size_t n, const uint8_t 
                               const uint32_t *img, hipStream_t s, uint32_t rows_hint = 1);
 // headerChecksum per header / receiver header check / CheckData (mask bit set = corrupt).
 hipError_t launch_header_csum(const uint8_t *hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
-                              int mode, const uint32_t *img, uint32_t *out, hipStream_t s);
+                              int mode, const uint32_t *img, uint8_t *out, size_t out_stride, hipStream_t s);
 hipError_t launch_header_check(const uint8_t *hdrs, size_t n, size_t stride, uint32_t hdr_bytes, uint32_t word_count,
                                uint32_t csum_offset, int mode, const uint32_t *img, uint32_t *mask, uint32_t *nbad,
                                hipStream_t s);

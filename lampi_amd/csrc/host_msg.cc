@@ -181,6 +181,9 @@ hipError_t host_msg(const uint8_t *h_msg, size_t msg_len, size_t frag_len, size_
     TRY(ensure_meta(p, k_count * sizeof(uint32_t)));
     uint32_t *dres = (uint32_t *)p.dmeta, *hres = (uint32_t *)p.hmeta;
     const bool copy = h_ring != nullptr;
+    // checksumming off (bcopy only): the bytes go up and come back into the slots, no kernel, no results
+    // (MEMCOPY_FUNC instead of bcopy_uicrc / bcopy_uicsum, ref src/path/gm/sendFrag.cc:153-155)
+    const bool none = mode == LAMPI_CSUM_NONE;
 
     PipeDrain drain(p);  // any early return below leaves nothing in flight
     const size_t nchunks = (k_count + fpc - 1) / fpc;
@@ -198,26 +201,28 @@ hipError_t host_msg(const uint8_t *h_msg, size_t msg_len, size_t frag_len, size_
         TRY(hipMemcpyAsync(d, h_msg + off, nb, hipMemcpyHostToDevice, p.s_in));
         TRY(hipEventRecord(p.in_done[b], p.s_in));
         TRY(hipStreamWaitEvent(p.s_k, p.in_done[b], 0));
-        TRY(launch_msg_csum(d, nb, frag_len, partial, dres + f0, mode, dev, img, p.s_k));
+        if (!none) TRY(launch_msg_csum(d, nb, frag_len, partial, dres + f0, mode, dev, img, p.s_k));
         TRY(hipEventRecord(p.k_done[b], p.s_k));
         if (!copy) continue;
         TRY(hipStreamWaitEvent(p.s_out, p.in_done[b], 0));
         TRY(copy_out(p, h_ring, stride, d, f0, nf, r));
         TRY(hipEventRecord(p.out_done[b], p.s_out));
     }
-    TRY(hipMemcpyAsync(hres, dres, k_count * sizeof(uint32_t), hipMemcpyDeviceToHost, p.s_k));
+    if (!none) TRY(hipMemcpyAsync(hres, dres, k_count * sizeof(uint32_t), hipMemcpyDeviceToHost, p.s_k));
     TRY(hipStreamSynchronize(p.s_k));
     if (copy) TRY(hipStreamSynchronize(p.s_out));
     drain.armed = false;
-    std::memcpy(h_out, hres, k_count * sizeof(uint32_t));
+    if (!none) std::memcpy(h_out, hres, k_count * sizeof(uint32_t));
     return hipSuccess;
 }
 
 // Argument checks shared by both entry points; fills the one empty fragment of an empty message.
+// none_ok: LAMPI_CSUM_NONE is accepted (the bcopy: copies only, h_out unused and may be NULL).
 int check_args(const void *h_msg, size_t msg_len, size_t frag_len, size_t k_first, size_t k_count,
-               uint32_t *h_out, int mode, bool *done, uint32_t partial) {
+               uint32_t *h_out, int mode, bool *done, uint32_t partial, bool none_ok = false) {
     *done = false;
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return (int)hipErrorInvalidValue;
+    const bool none = none_ok && mode == LAMPI_CSUM_NONE;
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32 && !none) return (int)hipErrorInvalidValue;
     if (frag_len == 0 || frag_len > kHostMaxFrag) return (int)hipErrorInvalidValue;
     const size_t nfr = msg_len ? (msg_len - 1) / frag_len + 1 : 1;
     if (k_first > nfr || k_count > nfr - k_first) return (int)hipErrorInvalidValue;
@@ -225,9 +230,9 @@ int check_args(const void *h_msg, size_t msg_len, size_t frag_len, size_t k_firs
         *done = true;
         return 0;
     }
-    if (!h_out || (msg_len && !h_msg)) return (int)hipErrorInvalidValue;
-    if (msg_len == 0) {  // one empty fragment: the register unchanged / an empty sum
-        h_out[0] = mode == LAMPI_CSUM_CRC32 ? partial : 0u;
+    if ((!h_out && !none) || (msg_len && !h_msg)) return (int)hipErrorInvalidValue;
+    if (msg_len == 0) {  // one empty fragment: the register unchanged / an empty sum (nothing with checksumming off)
+        if (!none) h_out[0] = mode == LAMPI_CSUM_CRC32 ? partial : 0u;
         *done = true;
     }
     return 0;
@@ -255,7 +260,7 @@ int lampi_host_msg_csum(const void *h_msg, size_t msg_len, size_t frag_len, size
 int lampi_host_msg_bcopy(const void *h_msg, size_t msg_len, size_t frag_len, size_t k_first, size_t k_count,
                          void *h_ring, size_t slot_stride, uint32_t partial, uint32_t *h_out, int mode) {
     bool done = false;
-    const int rc = check_args(h_msg, msg_len, frag_len, k_first, k_count, h_out, mode, &done, partial);
+    const int rc = check_args(h_msg, msg_len, frag_len, k_first, k_count, h_out, mode, &done, partial, true);
     if (rc || done) return rc;
     if (!h_ring || slot_stride < frag_len) return (int)hipErrorInvalidValue;
     return (int)host_msg((const uint8_t *)h_msg, msg_len, frag_len, k_first, k_count, (uint8_t *)h_ring, slot_stride,

@@ -590,37 +590,67 @@ int lampi_diag_frag_csum_batch_per_wave(const lampi_frag_desc *d_descs, size_t n
     return to_int(launch_desc_per_wave(d_descs, n, d_out, mode, img, (hipStream_t)stream));
 }
 
+}  // extern "C"
+
+namespace {
+// A strided output (d_out 4-byte aligned, out_stride a multiple of 4 and >= 4) is valid for n words.
+bool strided_ok(const void *d_out, size_t out_stride, size_t n) {
+    return d_out && !((uintptr_t)d_out & 3u) && !(out_stride & 3u) && out_stride >= 4 && n <= 0xFFFFFFFFull;
+}
+
+// Runs batch(vals) -- a launch writing n checksum words to vals -- and puts word i at d_out + i*out_stride:
+// straight into d_out when out_stride is 4, otherwise into stream-ordered scratch and then one 4-byte scatter
+// (the send side's dataChecksum @64 of each 72-byte gmHeaderData record: d_out = hdrs + 64, out_stride = the
+// buffer size).  d_out == nullptr: the words are discarded (the copies with checksumming off).
+template <class F>
+int with_out(size_t n, void *d_out, size_t out_stride, hipStream_t s, F &&batch) {
+    if (d_out && out_stride == 4) return batch((uint32_t *)d_out);
+    uint32_t *vals = nullptr;
+    hipError_t e = hipMallocAsync((void **)&vals, std::max<size_t>(n, 1) * sizeof(uint32_t), s);
+    if (e != hipSuccess) return to_int(e);
+    int r = batch(vals);
+    if (r == 0 && d_out) r = to_int(launch_scatter_u32(vals, n, (uint8_t *)d_out, out_stride, s));
+    const hipError_t f = hipFreeAsync(vals, s);
+    return r != 0 ? r : to_int(f);
+}
+}  // namespace
+
+extern "C" {
+
 int lampi_frag_csum_batch_strided(const lampi_frag_desc *d_descs, size_t n, void *d_out, size_t out_stride, int mode,
                                   void *stream) {
     const int base_mode = mode & ~(LAMPI_CSUM_BY_BYTES | LAMPI_CSUM_ROWS_HINT_MASK);
     if (base_mode != LAMPI_CSUM_CRC32 && base_mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
     if (n == 0) return 0;
-    if (!d_descs || !d_out || ((uintptr_t)d_out & 3u) || (out_stride & 3u) || out_stride < 4 || n > 0xFFFFFFFFull)
-        return to_int(hipErrorInvalidValue);
-    if (out_stride == 4) return lampi_frag_csum_batch(d_descs, n, (uint32_t *)d_out, mode, stream);
-    hipStream_t s = (hipStream_t)stream;
-    uint32_t *vals = nullptr;
-    hipError_t e = hipMallocAsync((void **)&vals, n * sizeof(uint32_t), s);
-    if (e != hipSuccess) return to_int(e);
-    int r = lampi_frag_csum_batch(d_descs, n, vals, mode, stream);
-    if (r == 0) r = to_int(launch_scatter_u32(vals, n, (uint8_t *)d_out, out_stride, s));
-    const hipError_t f = hipFreeAsync(vals, s);
-    return r != 0 ? r : to_int(f);
+    if (!d_descs || !strided_ok(d_out, out_stride, n)) return to_int(hipErrorInvalidValue);
+    return with_out(n, d_out, out_stride, (hipStream_t)stream,
+                    [&](uint32_t *vals) { return lampi_frag_csum_batch(d_descs, n, vals, mode, stream); });
 }
 
-int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
+int lampi_frag_bcopy_batch_strided(const lampi_copy_desc *d_descs, size_t n, void *d_out, size_t out_stride, int mode,
+                                   void *stream) {
     const uint32_t rows_hint = std::max(1u, LAMPI_CSUM_ROWS_HINT_OF(mode));
-    mode &= ~LAMPI_CSUM_ROWS_HINT_MASK;
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    const int base_mode = mode & ~LAMPI_CSUM_ROWS_HINT_MASK;
+    if (base_mode != LAMPI_CSUM_CRC32 && base_mode != LAMPI_CSUM_SUM32 && base_mode != LAMPI_CSUM_NONE)
+        return to_int(hipErrorInvalidValue);
+    const bool none = base_mode == LAMPI_CSUM_NONE;  // (d_out unused: may be NULL)
     if (n == 0) return 0;
-    if (!d_descs || !d_out) return to_int(hipErrorInvalidValue);
+    if (!d_descs || (!none && !strided_ok(d_out, out_stride, n)) || n > 0xFFFFFFFFull)
+        return to_int(hipErrorInvalidValue);
     int dev = 0;
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
     const uint32_t *img = nullptr;  // CRC: the tables
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
-    return to_int(launch_bcopy_desc(d_descs, n, d_out, mode, img, (hipStream_t)stream, rows_hint));
+    hipStream_t s = (hipStream_t)stream;
+    return with_out(n, none ? nullptr : d_out, out_stride, s, [&](uint32_t *vals) {
+        return to_int(launch_bcopy_desc(d_descs, n, vals, base_mode, img, s, rows_hint));
+    });
+}
+
+int lampi_frag_bcopy_batch(const lampi_copy_desc *d_descs, size_t n, uint32_t *d_out, int mode, void *stream) {
+    return lampi_frag_bcopy_batch_strided(d_descs, n, d_out, sizeof(uint32_t), mode, stream);
 }
 
 int lampi_copy_to_app_batch(const lampi_recv_desc *d_descs, size_t n, const void *d_expected, size_t expected_stride,
@@ -660,27 +690,44 @@ int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t 
                                   (hipStream_t)stream));
 }
 
-int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_dst, size_t dst_stride,
-                    uint32_t partial, uint32_t *d_out, int mode, void *stream) {
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
-    if (frag_len == 0 || frag_len > 0xFFFFFFFFull || dst_stride < frag_len || !d_out || (msg_len && (!d_msg || !d_dst)))
+int lampi_msg_bcopy_strided(const void *d_msg, size_t msg_len, size_t frag_len, void *d_dst, size_t dst_stride,
+                            uint32_t partial, void *d_out, size_t out_stride, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32 && mode != LAMPI_CSUM_NONE)
         return to_int(hipErrorInvalidValue);
-    const size_t n = msg_len ? (msg_len + frag_len - 1) / frag_len : 1;
+    const bool none = mode == LAMPI_CSUM_NONE;  // (d_out unused: may be NULL)
+    const size_t n = frag_len && msg_len ? (msg_len + frag_len - 1) / frag_len : 1;
+    if (frag_len == 0 || frag_len > 0xFFFFFFFFull || dst_stride < frag_len || (!none && !strided_ok(d_out, out_stride, n)) ||
+        (msg_len && (!d_msg || !d_dst)))
+        return to_int(hipErrorInvalidValue);
+    if (none && msg_len == 0) return 0;  // (nothing to copy, no checksum)
     int dev = 0;
     hipError_t e = current_device(&dev);
     if (e != hipSuccess) return to_int(e);
     const uint32_t *img = nullptr;  // CRC: the tables
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
-    return to_int(launch_msg_bcopy((const uint8_t *)d_msg, msg_len, frag_len, partial, (uint8_t *)d_dst, dst_stride, n,
-                                   d_out, mode, img, (hipStream_t)stream));
+    hipStream_t s = (hipStream_t)stream;
+    // checksumming off: the SUM copy schedules (every byte copied is read once; the sums are discarded)
+    return with_out(n, none ? nullptr : d_out, out_stride, s, [&](uint32_t *vals) {
+        return to_int(launch_msg_bcopy((const uint8_t *)d_msg, msg_len, frag_len, partial, (uint8_t *)d_dst, dst_stride,
+                                       n, vals, none ? LAMPI_CSUM_SUM32 : mode, img, s));
+    });
 }
 
-int lampi_chain_csum_batch(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first, size_t nfrags,
-                           uint32_t *d_out, int mode, void *stream) {
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+int lampi_msg_bcopy(const void *d_msg, size_t msg_len, size_t frag_len, void *d_dst, size_t dst_stride,
+                    uint32_t partial, uint32_t *d_out, int mode, void *stream) {
+    return lampi_msg_bcopy_strided(d_msg, msg_len, frag_len, d_dst, dst_stride, partial, d_out, sizeof(uint32_t), mode,
+                                   stream);
+}
+
+int lampi_chain_csum_batch_strided(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first,
+                                   size_t nfrags, void *d_out, size_t out_stride, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32 && mode != LAMPI_CSUM_NONE)
+        return to_int(hipErrorInvalidValue);
+    const bool none = mode == LAMPI_CSUM_NONE;  // (d_out unused: may be NULL)
     if (nfrags == 0) return 0;
-    if (!d_first || !d_out || (npieces && !d_pieces) || npieces > 0xFFFFFFFFull || nfrags > 0xFFFFFFFFull)
+    if (!d_first || (!none && !strided_ok(d_out, out_stride, nfrags)) || (npieces && !d_pieces) ||
+        npieces > 0xFFFFFFFFull || nfrags > 0xFFFFFFFFull)
         return to_int(hipErrorInvalidValue);
     int dev = 0;
     hipError_t e = current_device(&dev);
@@ -694,13 +741,21 @@ int lampi_chain_csum_batch(const lampi_copy_desc *d_pieces, size_t npieces, cons
         e = hipMallocAsync((void **)&scratch, 2 * npieces * sizeof(uint32_t), s);
         if (e != hipSuccess) return to_int(e);
     }
-    e = launch_chain(d_pieces, npieces, d_first, nfrags, d_out, mode, img, scratch, scratch ? scratch + npieces : nullptr,
-                     s);
+    // (checksumming off: launch_chain copies and writes zeros, here into discarded scratch)
+    int r = with_out(nfrags, none ? nullptr : d_out, out_stride, s, [&](uint32_t *vals) {
+        return to_int(launch_chain(d_pieces, npieces, d_first, nfrags, vals, mode, img, scratch,
+                                   scratch ? scratch + npieces : nullptr, s));
+    });
     if (scratch) {
-        const hipError_t f = hipFreeAsync(scratch, s);
-        if (e == hipSuccess) e = f;
+        const int f = to_int(hipFreeAsync(scratch, s));
+        if (r == 0) r = f;
     }
-    return to_int(e);
+    return r;
+}
+
+int lampi_chain_csum_batch(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first, size_t nfrags,
+                           uint32_t *d_out, int mode, void *stream) {
+    return lampi_chain_csum_batch_strided(d_pieces, npieces, d_first, nfrags, d_out, sizeof(uint32_t), mode, stream);
 }
 
 int lampi_chain_copy_to_app_batch(const lampi_copy_desc *d_pieces, size_t npieces, const uint32_t *d_first,
@@ -742,11 +797,13 @@ int lampi_chain_copy_to_app_batch(const lampi_copy_desc *d_pieces, size_t npiece
     return to_int(e);
 }
 
-int lampi_header_csum_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
-                            uint32_t *d_out, int mode, void *stream) {
-    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+int lampi_header_csum_batch_strided(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
+                                    void *d_out, size_t out_stride, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32 && mode != LAMPI_CSUM_NONE)
+        return to_int(hipErrorInvalidValue);
+    if (mode == LAMPI_CSUM_NONE) return 0;  // no header checksum with checksumming off (gm/sendFrag.cc:219-225)
     if (n == 0) return 0;
-    if (!d_hdrs || !d_out || ((uintptr_t)d_hdrs & 3u) || (stride & 3u) || n > 0xFFFFFFFFull)
+    if (!d_hdrs || !strided_ok(d_out, out_stride, n) || ((uintptr_t)d_hdrs & 3u) || (stride & 3u))
         return to_int(hipErrorInvalidValue);
     int dev = 0;
     hipError_t e = current_device(&dev);
@@ -754,8 +811,15 @@ int lampi_header_csum_batch(const void *d_hdrs, size_t n, size_t stride, uint32_
     const uint32_t *img = nullptr;
     e = device_tables(dev, &img);
     if (e != hipSuccess) return to_int(e);
-    return to_int(launch_header_csum((const uint8_t *)d_hdrs, n, stride, crclen, word_count, mode, img, d_out,
-                                     (hipStream_t)stream));
+    return to_int(launch_header_csum((const uint8_t *)d_hdrs, n, stride, crclen, word_count, mode, img,
+                                     (uint8_t *)d_out, out_stride, (hipStream_t)stream));
+}
+
+int lampi_header_csum_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t crclen, uint32_t word_count,
+                            uint32_t *d_out, int mode, void *stream) {
+    if (mode != LAMPI_CSUM_CRC32 && mode != LAMPI_CSUM_SUM32) return to_int(hipErrorInvalidValue);
+    return lampi_header_csum_batch_strided(d_hdrs, n, stride, crclen, word_count, d_out, sizeof(uint32_t), mode,
+                                           stream);
 }
 
 int lampi_header_check_batch(const void *d_hdrs, size_t n, size_t stride, uint32_t hdr_bytes, uint32_t word_count,

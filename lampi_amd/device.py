@@ -11,7 +11,8 @@ import torch
 
 from ._lib import BY_BYTES, CRC32, CRC_INITIAL_REGISTER, NONE, SUM32, check, lib, rows_hint_bits
 
-__all__ = ["CRC32", "SUM32", "NONE", "chain_copy_to_app_batch", "frag_csum_batch", "diag_frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
+__all__ = ["CRC32", "SUM32", "NONE", "chain_copy_to_app_batch", "frag_bcopy_batch_strided", "msg_bcopy_strided",
+           "chain_csum_batch_strided", "header_csum_batch_strided", "frag_csum_batch", "diag_frag_csum_batch_per_wave", "frag_csum64_batch", "frag_bcopy_batch", "msg_bcopy", "msg_csum", "fill_stream", "fill_stream_frags",
            "make_descs", "make_copy_descs", "as_u32", "chain_csum_batch", "header_csum_batch", "header_check_batch", "check_data_batch",
            "mask_bits", "make_recv_descs", "copy_to_app_batch"]
 
@@ -88,6 +89,10 @@ def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC3
     rows_hint: LAMPI_CSUM_ROWS_HINT -- fragments span about that many 4 KiB rows (row groups)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
+    if mode == NONE:  # checksumming off: copies only, no output (returns None)
+        check(lib().lampi_frag_bcopy_batch(descs.data_ptr(), count, None, mode | rows_hint_bits(rows_hint),
+                                           _stream_handle(stream)), "lampi_frag_bcopy_batch")
+        return None
     if out is None:
         out = torch.empty(count, dtype=torch.int32, device=descs.device)
     _require_cuda(out, "out")
@@ -97,6 +102,29 @@ def frag_bcopy_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC3
                                        _stream_handle(stream)),
           "lampi_frag_bcopy_batch")
     return out
+
+
+def _strided_dst(dst: torch.Tensor | None, count: int, stride: int, offset: int, mode: int) -> int | None:
+    """Device address of record 0's output word (None with mode NONE: nothing is written)."""
+    if mode == NONE:
+        return None
+    if dst is None:
+        raise ValueError("dst is required unless mode is NONE")
+    _records(dst.view(torch.uint8)[offset:], count, stride, "dst")
+    return dst.data_ptr() + offset
+
+
+def frag_bcopy_batch_strided(descs: torch.Tensor, dst: torch.Tensor | None, stride: int, offset: int = 0,
+                             n: int | None = None, mode: int = CRC32, stream: torch.cuda.Stream | None = None,
+                             rows_hint: int = 0) -> torch.Tensor | None:
+    """frag_bcopy_batch with checksum i written at byte offset + i*stride of ``dst`` (e.g. dataChecksum @64
+    of each buffer of a GM send ring, src/path/gm/sendFrag.cc:149-151); returns ``dst``."""
+    _require_cuda(descs, "descs")
+    count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
+    ptr = _strided_dst(dst, count, stride, offset, mode)
+    check(lib().lampi_frag_bcopy_batch_strided(descs.data_ptr(), count, ptr, stride, mode | rows_hint_bits(rows_hint),
+                                               _stream_handle(stream)), "lampi_frag_bcopy_batch_strided")
+    return dst
 
 
 def frag_csum_batch(descs: torch.Tensor, n: int | None = None, mode: int = CRC32, out: torch.Tensor | None = None,
@@ -201,6 +229,10 @@ def msg_bcopy(msg: torch.Tensor, frag_len: int, dst: torch.Tensor, dst_stride: i
     n = (nbytes + frag_len - 1) // frag_len if nbytes else 1
     if nbytes and (n - 1) * stride + (nbytes - (n - 1) * frag_len) > dst.numel() * dst.element_size():
         raise ValueError("dst is too small")
+    if mode == NONE:  # checksumming off: copies only (returns None)
+        check(lib().lampi_msg_bcopy(msg.data_ptr(), nbytes, frag_len, dst.data_ptr(), stride, partial & 0xFFFFFFFF,
+                                    None, mode, _stream_handle(stream)), "lampi_msg_bcopy")
+        return None
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=msg.device)
     _require_cuda(out, "out")
@@ -209,6 +241,25 @@ def msg_bcopy(msg: torch.Tensor, frag_len: int, dst: torch.Tensor, dst_stride: i
     check(lib().lampi_msg_bcopy(msg.data_ptr(), nbytes, frag_len, dst.data_ptr(), stride, partial & 0xFFFFFFFF,
                                 out.data_ptr(), mode, _stream_handle(stream)), "lampi_msg_bcopy")
     return out
+
+
+def msg_bcopy_strided(msg: torch.Tensor, frag_len: int, dst: torch.Tensor, dst_stride: int, out: torch.Tensor | None,
+                      out_stride: int, out_offset: int = 0, partial: int = CRC_INITIAL_REGISTER, mode: int = CRC32,
+                      msg_len: int | None = None, stream: torch.cuda.Stream | None = None) -> None:
+    """msg_bcopy with fragment k's checksum written at byte out_offset + k*out_stride of ``out``: a GM send into
+    a ring of header + payload buffers (dst = ring[72:], out = ring, out_offset 64, both strides the buffer size)."""
+    _require_cuda(msg, "msg")
+    _require_cuda(dst, "dst")
+    nbytes = msg.numel() * msg.element_size() if msg_len is None else int(msg_len)
+    if nbytes > msg.numel() * msg.element_size():
+        raise ValueError("msg_len exceeds the tensor")
+    n = (nbytes + frag_len - 1) // frag_len if nbytes else 1
+    if nbytes and (n - 1) * dst_stride + (nbytes - (n - 1) * frag_len) > dst.numel() * dst.element_size():
+        raise ValueError("dst is too small")
+    ptr = _strided_dst(out, n, out_stride, out_offset, mode)
+    check(lib().lampi_msg_bcopy_strided(msg.data_ptr(), nbytes, frag_len, dst.data_ptr(), dst_stride,
+                                        partial & 0xFFFFFFFF, ptr, out_stride, mode, _stream_handle(stream)),
+          "lampi_msg_bcopy_strided")
 
 
 def chain_csum_batch(pieces: torch.Tensor, first, mode: int = CRC32, out: torch.Tensor | None = None,
@@ -226,11 +277,29 @@ def chain_csum_batch(pieces: torch.Tensor, first, mode: int = CRC32, out: torch.
         _require_cuda(first, "first")
         first_t = first
     nfrags = first_t.numel() - 1
+    if mode == NONE:  # checksumming off: the pieces are copied, no output (returns None)
+        check(lib().lampi_chain_csum_batch(pieces.data_ptr(), npieces, first_t.data_ptr(), nfrags, None, mode,
+                                           _stream_handle(stream)), "lampi_chain_csum_batch")
+        return None
     if out is None:
         out = torch.empty(max(nfrags, 0), dtype=torch.int32, device=pieces.device)
     check(lib().lampi_chain_csum_batch(pieces.data_ptr(), npieces, first_t.data_ptr(), nfrags, out.data_ptr(), mode,
                                        _stream_handle(stream)), "lampi_chain_csum_batch")
     return out
+
+
+def chain_csum_batch_strided(pieces: torch.Tensor, first: torch.Tensor, dst: torch.Tensor | None, stride: int,
+                             offset: int = 0, mode: int = CRC32, stream: torch.cuda.Stream | None = None):
+    """chain_csum_batch with fragment f's checksum written at byte offset + f*stride of ``dst`` (the typemap
+    send's dataChecksum, src/path/gm/sendFrag.cc:216); ``first`` a device int32 tensor of nfrags + 1 offsets."""
+    _require_cuda(pieces, "pieces")
+    _require_cuda(first, "first")
+    npieces = pieces.numel() * pieces.element_size() // 32
+    nfrags = first.numel() - 1
+    ptr = _strided_dst(dst, nfrags, stride, offset, mode)
+    check(lib().lampi_chain_csum_batch_strided(pieces.data_ptr(), npieces, first.data_ptr(), nfrags, ptr, stride,
+                                               mode, _stream_handle(stream)), "lampi_chain_csum_batch_strided")
+    return dst
 
 
 def chain_copy_to_app_batch(pieces: torch.Tensor, first, expected: torch.Tensor | None, expected_stride: int = 4,
@@ -277,6 +346,18 @@ def header_csum_batch(hdrs: torch.Tensor, n: int, stride: int, crclen: int, word
     check(lib().lampi_header_csum_batch(hdrs.data_ptr(), n, stride, crclen, word_count, out.data_ptr(), mode,
                                         _stream_handle(stream)), "lampi_header_csum_batch")
     return out
+
+
+def header_csum_batch_strided(hdrs: torch.Tensor, n: int, stride: int, crclen: int, word_count: int,
+                              dst: torch.Tensor, out_stride: int, offset: int = 0, mode: int = CRC32,
+                              stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """headerChecksum of n headers written at byte offset + i*out_stride of ``dst``: in place into the headers
+    with dst = hdrs, offset 68, out_stride = stride (src/path/gm/sendFrag.cc:218-225); mode NONE writes nothing."""
+    _records(hdrs, n, stride, "hdrs")
+    ptr = _strided_dst(dst, n, out_stride, offset, mode)
+    check(lib().lampi_header_csum_batch_strided(hdrs.data_ptr(), n, stride, crclen, word_count, ptr, out_stride, mode,
+                                                _stream_handle(stream)), "lampi_header_csum_batch_strided")
+    return dst
 
 
 def _mask_out(n: int, device) -> tuple[torch.Tensor, torch.Tensor]:
@@ -364,19 +445,21 @@ def copy_to_app_batch(descs: torch.Tensor, expected: torch.Tensor, expected_stri
     rows_hint: as for frag_bcopy_batch (GM's 65,456-byte payloads: 16)."""
     _require_cuda(descs, "descs")
     count = descs.numel() * descs.element_size() // 32 if n is None else int(n)
-    if expected is None:  # (mode NONE: nothing compared)
-        expected = torch.zeros(1, dtype=torch.int32, device=descs.device)
-        expected_stride = expected_offset = 0
+    if expected is None:  # (mode NONE: nothing compared; the C call refuses a null pointer in the other modes)
+        if (mode & 0xFF) != NONE:
+            raise ValueError("expected is required unless mode is NONE (checksumming off)")
+        exp_ptr, expected_stride = 0, 0
     else:
         _records(expected.view(torch.uint8)[expected_offset:] if count else expected, count, expected_stride,
                  "expected")
+        exp_ptr = expected.data_ptr() + expected_offset
     copied = torch.empty(max(count, 1), dtype=torch.int64, device=descs.device)
     csum = torch.empty(max(count, 1), dtype=torch.int32, device=descs.device)
     # (the call zeroes the mask words and the count itself: no fill kernels here, except for an empty batch)
     mask, nbad = (_mask_out(count, descs.device) if count == 0 else
                   (torch.empty((count + 31) // 32, dtype=torch.int32, device=descs.device),
                    torch.empty(1, dtype=torch.int32, device=descs.device)))
-    check(lib().lampi_copy_to_app_batch(descs.data_ptr(), count, expected.data_ptr() + expected_offset, expected_stride,
+    check(lib().lampi_copy_to_app_batch(descs.data_ptr(), count, exp_ptr or None, expected_stride,
                                         copied.data_ptr(), csum.data_ptr(), mask.data_ptr(), nbad.data_ptr(),
                                         mode | rows_hint_bits(rows_hint), _stream_handle(stream)),
           "lampi_copy_to_app_batch")

@@ -164,3 +164,18 @@ def test_native_host_typemap_chains_match_reference(cuda, tmp_path):
     assert len(lines) == 3 * (4 + 6 * 2 * 2 * 2 + 6 * 2 + 4 * 3) + 3
     assert any(ln.startswith("deliver ") and " bad 0 " not in ln for ln in lines)
     assert "pinned_after_release 0 scratch_after_release 0" in out
+
+
+def test_native_send_ring_in_place_matches_oracle(cuda):
+    """The device-resident send step in place from a native C++ caller (tests/native/send_ring_caller.cc): a GM
+    ring of 64 KiB buffers packed by lampi_msg_bcopy_strided (a message of 65,456-byte fragments),
+    lampi_chain_csum_batch_strided (typemap fragments) and lampi_frag_bcopy_batch_strided (ragged descriptors),
+    each stamping dataChecksum @64, then lampi_header_csum_batch_strided stamping the header checksum @68
+    (ref src/path/gm/sendFrag.cc:143-226) -- CRC, SUM and checksumming off; every byte of the ring against the
+    oracle's send loop and the receiver's header test inside the program."""
+    r = subprocess.run([_bin("send_ring_caller")], capture_output=True, text=True, timeout=300)
+    out = r.stdout
+    assert r.returncode == 0, out[-4000:] + r.stderr[-2000:]
+    assert out.strip().endswith("bad 0 done"), out[-2000:]
+    lines = [ln for ln in out.splitlines() if ln.startswith("send_ring ")]
+    assert len(lines) == 3 and all(ln.endswith(" ok") for ln in lines), out

@@ -352,3 +352,61 @@ def test_learned_ib_pairs_read_only(cuda, oracle, mode):
             got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, stream=stream))
             bad = np.nonzero(got != prepared[k][1])[0]
             assert bad.size == 0, (i, k, bad[:8].tolist())
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_learned_small_fragments_stale_shape(cuda, oracle, mode):
+    """large batches the census saw as all-small (every sampled fragment <= 1 KiB / <= 2 KiB) run the
+    piece streams with 256 fragments per workgroup (CRC, SUM) -- a schedule picked from a learned shape that can
+    be stale.  70,000 descriptors of 64 B .. 1 KiB on one array for 20 calls, then the same array holding 0 B,
+    17 B, 9,000 B and 1 MiB fragments at odd addresses among them; every call vs the oracle."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(707 + mode)
+    n = 70_000
+    size = 96 << 20
+    base = torch.empty(size, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=708)
+    host = base.cpu().numpy()
+    small = rng.integers(64, 1025, size=n).astype(np.uint64)
+    offs = rng.integers(0, size - (1 << 20) - 1, size=n).astype(np.uint64)
+    parts = rng.integers(0, 2**32, size=n, dtype=np.uint64)
+    odd = small.copy()
+    pick = rng.choice(n, size=n // 50, replace=False)
+    odd[pick] = rng.choice(np.array([0, 17, 9000, 1 << 20], np.uint64), size=pick.size)
+    odd_offs = offs.copy()
+    odd_offs[pick] |= np.uint64(1)
+    prepared = {k: (dv.make_descs(base, o, ln, parts),
+                    oracle.desc_batch(host, o, ln.astype(np.uint32), parts.astype(np.uint32) if mode == 0 else None,
+                                      mode))
+                for k, (o, ln) in (("small", (offs, small)), ("odd", (odd_offs, odd)))}
+    descs = prepared["small"][0].clone()
+    stream = torch.cuda.Stream(device=cuda)
+    with torch.cuda.stream(stream):
+        for i, k in enumerate(["small"] * 20 + ["odd"] * 3 + ["small"] * 2):
+            descs.copy_(prepared[k][0])
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, stream=stream))
+            bad = np.nonzero(got != prepared[k][1])[0]
+            assert bad.size == 0, (i, k, bad[:8].tolist())
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("frag_len", [64, 100, 1000, 1024])
+def test_small_fragment_messages_ragged(cuda, oracle, mode, frag_len):
+    """Messages of >= 65,536 fragments of at most 1 KiB (the SUM piece streams at 256 fragments per workgroup,
+    CRC's small-fragment schedules) with an odd start address and a ragged last fragment, vs the oracle."""
+    import torch
+
+    dv = _dv()
+    n = 70_001
+    msg_len = (n - 1) * frag_len + frag_len // 3 + 1
+    buf = torch.empty(msg_len + 5, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=709)
+    msg = buf[5:]
+    got = dv.as_u32(dv.msg_csum(msg, frag_len, partial=0x1234567 if mode == 0 else 0xFFFFFFFF, mode=mode))
+    host = buf.cpu().numpy()
+    offs = 5 + np.arange(n, dtype=np.uint64) * frag_len
+    lens = np.minimum(frag_len, msg_len + 5 - offs).astype(np.uint32)
+    want = oracle.desc_batch(host, offs, lens, np.full(n, 0x1234567, np.uint32) if mode == 0 else None, mode)
+    assert np.array_equal(got, want)
