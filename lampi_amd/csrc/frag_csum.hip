@@ -51,6 +51,17 @@
 #include "crc_tables.h"
 #include "frag_csum_kernels.h"
 
+// A/B knobs (tools/ab/*.sh): the schedule switches measured against each other are read from the environment
+// only in the A/B build of the library (make AB=1: liblampi_csum_ab.so, -DLAMPI_AB_KNOBS=1, loaded by the A/B
+// scripts through LAMPI_CSUM_LIB).  The default library compiles each to its measured default and reads only
+// the documented switches (LAMPI_CSUM_NO_SHAPES here, LAMPI_HOST_CHUNK_BYTES in host_msg.cc); the knob names
+// do not appear in it (tests/test_abi.py).
+#if LAMPI_AB_KNOBS
+#define LAMPI_AB_ENV(name) std::getenv(name)
+#else
+#define LAMPI_AB_ENV(name) (static_cast<const char *>(nullptr))
+#endif
+
 namespace lampi {
 
 // per-stream device scratch (defined with the launchers)
@@ -366,26 +377,6 @@ struct IsSparse : std::false_type {};
 template <>
 struct IsSparse<SparseDescSource> : std::true_type {};
 
-// A size class of a read-only CRC descriptor batch (config C's partition): entry i of
-// the class is descriptor idx[i]; entries at or past *count (the partition kernel's, on the device) read
-// as not this class's (aux = 1, nothing stored).  emit stores out[idx[i]].
-struct ListSource {
-    static constexpr bool kCopy = false;
-    static constexpr bool kPhase = false;
-    const lampi_frag_desc *d;
-    const uint32_t *idx;
-    const uint32_t *count;
-    __device__ FragInfo get(size_t i) const {
-        if (i >= *count) return {nullptr, 0u, 0u, nullptr, 0u, 1u};
-        const lampi_frag_desc x = d[idx[i]];
-        return {(gbyte *)(uintptr_t)x.addr, x.length, x.partial, nullptr, 0u};
-    }
-};
-template <class S>
-struct IsList : std::false_type {};
-template <>
-struct IsList<ListSource> : std::true_type {};
-
 template <class S>
 struct IsRecv : std::false_type {};
 template <>
@@ -499,10 +490,6 @@ __device__ __forceinline__ void emit(const Src &src, Acc *out, size_t f, Acc v, 
     }
     if constexpr (IsSplit<Src>::value)
         if (fi.aux) return;  // the other launch's fragment
-    if constexpr (IsList<Src>::value) {  // a size class: entry f is descriptor idx[f]
-        if (!fi.aux) out[src.idx[f]] = v;
-        return;
-    }
     if constexpr (std::is_same<Src, RecvCopyOnlySource>::value) v = 0;  // no checksum with checksumming off
     out[f] = v;
     if constexpr (IsRecv<Src>::value) src.verdict(f, v, fi);
@@ -1022,6 +1009,21 @@ __device__ __forceinline__ uint32_t wave_add(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
            __builtin_amdgcn_readlane(v, 48);
+}
+
+// XOR / sum of v over each group of kSub consecutive lanes (kSub = 1 .. 32, a power of two): the DPP
+// butterflies of row16_xor cut after log2(kSub) levels -- every lane of a group of <= 16 gets the group's
+// value -- and for 32, row_bcast:15 into rows 1 and 3 (their lanes, 31 and 63 among them, get it).
+template <int kSub, bool kAdd>
+__device__ __forceinline__ uint32_t group_reduce(uint32_t v) {
+    static_assert(kSub >= 1 && kSub <= 32 && (kSub & (kSub - 1)) == 0, "groups of 1..32 lanes");
+    auto op = [](uint32_t a, uint32_t b) { return kAdd ? a + b : a ^ b; };
+    if constexpr (kSub >= 2) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+    if constexpr (kSub >= 4) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    if constexpr (kSub >= 8) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+    if constexpr (kSub >= 16) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false));
+    if constexpr (kSub >= 32) v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+    return v;
 }
 
 // Fragments of a workgroup: wave w of workgroup b takes fragments b*4*fpw + w + 4i, i < fpw.
@@ -1920,11 +1922,6 @@ crc_stream_kernel(Src src, size_t n, uint32_t fpg, const uint32_t *__restrict__ 
         }
     }
     size_t base = (size_t)blockIdx.x * fpg;
-    if constexpr (IsList<Src>::value) {  // a size class: the launch is sized for the whole batch
-        const size_t c = min(n, (size_t)*src.count);
-        if (base >= c) return;
-        n = c;
-    }
     uint32_t nwg = (uint32_t)min((size_t)fpg, n - base);
     if constexpr (IsSeg<Src>::value) {  // the plan's workgroups: plan[0] of them, segments [plan[1+i], plan[2+i])
         const uint32_t g = plan[0];
@@ -2722,7 +2719,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_light_frag_copy_kernel(const Src
     FragInfo fi{nullptr, 0u, 0u, nullptr, 0u};
     if (f < n) fi = src.get(f);
     LightFrag F;
-    F.init(fi, f < n && !((IsSplit<Src>::value || IsList<Src>::value) && fi.aux), W, g);
+    F.init(fi, f < n && !(IsSplit<Src>::value && fi.aux), W, g);
     if constexpr (IsRecv<Src>::value)  // row groups: the join kernel gives every verdict, this launch zeroes them
         if (W > 1u && lane == 0u && f < n && g == 0u) zero_verdict_words(src, f);
     u32x4 d[4];
@@ -2730,7 +2727,7 @@ __global__ void __launch_bounds__(64 * kWv) crc_light_frag_copy_kernel(const Src
     // the first row's loads before the table staging (after it: 4 KiB copies 73 -> 66%, profiles/r04/late_loads_ab.txt)
     F.load_row(lane, F.r0, F.live, d, o, F.half);  // (an empty or dead wave's descriptor reads nothing but zeros)
     const u32x4 head = F.load_head();
-    if constexpr (IsSplit<Src>::value || IsSparse<Src>::value || IsList<Src>::value)  // the size split's light launch: most workgroups
+    if constexpr (IsSplit<Src>::value || IsSparse<Src>::value)  // the size split's light launch: most workgroups
         if (!__syncthreads_or(F.live)) return;  // hold no fragment of its class and leave before staging the tables
     build_slices_light<64 * kWv>(reinterpret_cast<char *>(lds), bs);
     reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(lds) + kLtNib)[min(t, kNibPieces - 1)] = nib;
@@ -2982,7 +2979,7 @@ static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uin
                                              hipStream_t s, uint32_t *shape_nhalf) {
     uint32_t *left = nullptr, *next_left = nullptr, *list = nullptr;
     static const int kWv = [] {
-        const char *e = std::getenv("LAMPI_PAIR_WAVES");
+        const char *e = LAMPI_AB_ENV("LAMPI_PAIR_WAVES");
         return e && e[0] == '1' ? 16 : e && e[0] == '4' ? 4 : 8;
     }();
     const size_t nwg = (n + 2 * kWv - 1) / (2 * kWv);
@@ -3021,7 +3018,7 @@ static hipError_t launch_crc_light_pair_copy(const Src &src, size_t n, const uin
 static int light_waves(bool recv = false) {
     (void)recv;
     static const int w = [] {
-        const char *e = std::getenv("LAMPI_LIGHT_WAVES");
+        const char *e = LAMPI_AB_ENV("LAMPI_LIGHT_WAVES");
         return e && e[0] == '1' ? 16 : e && e[0] == '8' ? 8 : 4;
     }();
     return w;
@@ -3231,8 +3228,14 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // ring's load counts stay fixed), not emitted, and listed (atomicAdd on *left) for
 // crc_light_pair_leftover_kernel, which checksums fragments 2e and 2e + 1 of entry e on the table-light
 // kernel (kV = 1 lists f / 2: its neighbour is checksummed again, to the same value).
+// kSub < 64 (packed rows, round 6; messages of 64 * kSub-byte fragments, kSub = 1 .. 32): every 4 KiB row holds
+// 64 / kSub whole fragments, lane l the 64-byte piece l % kSub of fragment l / kSub of the row.  The row's
+// bytes and lookups are config B's; only the ends change: the register enters at every group's first lane,
+// lane l shifts by 64 (kSub - 1 - l % kSub) bytes through the combine column of lane 64 - kSub + l % kSub
+// (none for kSub = 1), the group's values meet by DPP (group_reduce) and the group's last lane stores
+// out[row * 64 / kSub + l / kSub].  Launched with kV = 2 (every row a fragment end); read-only.
 template <int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
-          bool kSum = false, int kWv = kWaves, int kCap = 0, bool kDesc = false>
+          bool kSum = false, int kWv = kWaves, int kCap = 0, bool kDesc = false, int kSub = 64>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kCap > 0 ? kCap : 1)))
 crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, size_t frag_len, uint32_t partial,
                    const uint32_t *__restrict__ img, uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
@@ -3240,6 +3243,7 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     constexpr int K = kChains;
     static_assert(kWv >= kWaves, "the table builders need 256 threads");
     static_assert(!kDesc || (kV <= 2 && !kCopy && !kSum), "descriptor batches: read-only CRC, kV = 1 or 2");
+    static_assert(kSub == 64 || (kV == 2 && !kCopy && !kCoal && !kDesc), "packed rows: read-only, kV = 2");
     constexpr int kS = kCoal ? kRowBytes / 4 : 16;  // chunk stride of a lane
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
@@ -3342,6 +3346,9 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
         return;
     }
     const CrcLane k = make_lane(lane);
+    // packed rows: the combine column of lane 64 - kSub + l % kSub (a shift by 64 (kSub - 1 - l % kSub) bytes)
+    CrcLane ksub = k;
+    if constexpr (kSub < 64) ksub.comb_base = make_lane(64 - kSub + (lane & (kSub - 1))).comb_base;
     uint32_t C[K];
 #pragma unroll
     for (int c = 0; c < K; ++c) C[c] = 0;
@@ -3361,6 +3368,17 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 #pragma unroll
                 for (int w = 0; w < 16; ++w) y += row_word(b.x[c], w);
                 C[c] = y;
+            }
+            if constexpr (kSub < 64) {  // packed rows: every group of kSub lanes is a fragment
+                uint32_t x[K];
+#pragma unroll
+                for (int c = 0; c < K; ++c) x[c] = group_reduce<kSub, true>(C[c]);
+                if ((lane & (kSub - 1)) == kSub - 1) {
+#pragma unroll
+                    for (int c = 0; c < K; ++c)
+                        if (K * t.i + c < nfr) out[(frag(t.i, c) * kV + t.r) * (64u / kSub) + lane / kSub] = x[c];
+                }
+                return;
             }
             if (kV > 1 || t.r + 1 == R) {
                 uint32_t x[K];
@@ -3386,12 +3404,26 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
                 }
             } else if (kV > 1 || t.r == 0) {
 #pragma unroll
-                for (int c = 0; c < K; ++c) C[c] = (lane == 0) ? vinit : 0u;
+                for (int c = 0; c < K; ++c) C[c] = (lane & (kSub - 1)) == 0 ? vinit : 0u;
             } else {
 #pragma unroll
                 for (int c = 0; c < K; ++c) C[c] = horner_shift(lds, C[c]);
             }
             crc_pieces<K>(lds, k, C, b);
+        }
+        if constexpr (kSub < 64) {  // packed rows: lane l to its fragment's end, the group's XOR, its last lane stores
+            uint32_t x[K];
+#pragma unroll
+            for (int c = 0; c < K; ++c) x[c] = kSub > 1 ? lane_combine(lds, ksub, C[c]) : C[c];
+#pragma unroll
+            for (int c = 0; c < K; ++c) x[c] = group_reduce<kSub, false>(x[c]);
+            if ((lane & (kSub - 1)) == kSub - 1) {
+#pragma unroll
+                for (int c = 0; c < K; ++c)
+                    if (K * t.i + c < nfr)
+                        out[(frag(t.i, c) * kV + t.r) * (64u / kSub) + lane / kSub] = __builtin_bswap32(x[c]);
+            }
+            return;
         }
         if (kV > 1 || t.r + 1 == R) {
             uint32_t x[K];
@@ -4344,7 +4376,7 @@ static void launch_crc_rows_copy(const Src &src, size_t n, uint32_t R, const uin
 constexpr uint32_t kCrcFpg = 96;
 static uint32_t frags_per_wg(size_t n, size_t frag_len = 0) {
     static const uint32_t fpg_env = [] {  // (A/B knob LAMPI_STREAM_FPG: fragments per workgroup, <= 256)
-        const char *e = std::getenv("LAMPI_STREAM_FPG");
+        const char *e = LAMPI_AB_ENV("LAMPI_STREAM_FPG");
         return e ? (uint32_t)std::min(256, std::max(1, std::atoi(e))) : 0u;
     }();
     uint32_t fpg = fpg_env ? fpg_env : kCrcFpg;
@@ -4663,7 +4695,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     ScratchTable::Slot &slot = t_scratch.slots[{dev, s}];
     // this batch's record: the one of its descriptor array, else the least recently used one, reset
     static const bool keyed = [] {  // (A/B knob LAMPI_SHAPES_UNKEYED=1: one record per kind, as in round 4)
-        const char *e = std::getenv("LAMPI_SHAPES_UNKEYED");
+        const char *e = LAMPI_AB_ENV("LAMPI_SHAPES_UNKEYED");
         return !(e && e[0] == '1');
     }();
     const void *key = keyed ? (const void *)src.d : nullptr;
@@ -4808,63 +4840,6 @@ static hipError_t launch_row_segments(const lampi_frag_desc *d, size_t n, uint32
 // launches concurrently on a forked stream measured worse (GM 67-68%).
 constexpr size_t kSplitMin = 1024, kSplitMax = 65536;
 
-// Size-class partition of a large mixed read-only CRC batch (VERDICT r4 item 1, A/B knob LAMPI_CRC_PARTITION =
-// d: at most n / d entries in the large class): partition_kernel compacts the descriptor indices of the
-// 8-16-row fragments (split_large) into list A -- up to its capacity -- and the rest into list B (a wave's
-// ballot, one atomicAdd per list per wave); the table-light kernel then walks list A one wave per
-// fragment (its grid is list A's capacity; workgroups past the count leave before staging tables) and the
-// piece streams take list B (grid for the whole batch; workgroups past the count leave at once).
-__global__ void __launch_bounds__(256) partition_kernel(const lampi_frag_desc *__restrict__ d, size_t n,
-                                                       uint32_t capA, uint32_t *__restrict__ idxA,
-                                                       uint32_t *__restrict__ idxB, uint32_t *cnt) {
-    const size_t f = (size_t)blockIdx.x * 256 + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63u;
-    const bool valid = f < n;
-    const bool large = valid && split_large(d[f].length);
-    const uint64_t below = (1ull << lane) - 1ull;
-    const uint64_t mA = __ballot(large);
-    uint32_t a0 = 0u;
-    if (lane == 0 && mA) a0 = atomicAdd(&cnt[0], (uint32_t)__popcll(mA));
-    a0 = (uint32_t)__shfl((int)a0, 0);
-    const uint32_t ra = a0 + (uint32_t)__popcll(mA & below);
-    const bool toA = large && ra < capA;
-    const bool toB = valid && !toA;
-    const uint64_t mB = __ballot(toB);
-    uint32_t b0 = 0u;
-    if (lane == 0 && mB) b0 = atomicAdd(&cnt[1], (uint32_t)__popcll(mB));
-    b0 = (uint32_t)__shfl((int)b0, 0);
-    if (toA) idxA[ra] = (uint32_t)f;
-    if (toB) idxB[b0 + (uint32_t)__popcll(mB & below)] = (uint32_t)f;
-}
-
-static hipError_t launch_crc_desc_partition(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
-                                            hipStream_t s, uint32_t div) {
-    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t capA = (uint32_t)std::min<size_t>(n, std::max<size_t>(1024, n / div));
-    uint32_t *scratch = nullptr;
-    bool pooled = false;
-    hipError_t e = stream_scratch(s, ((size_t)capA + n + 2) * sizeof(uint32_t), (void **)&scratch, &pooled);
-    if (e != hipSuccess) return e;
-    uint32_t *cnt = scratch, *idxA = scratch + 2, *idxB = idxA + capA;
-    e = hipMemsetAsync(cnt, 0, 2 * sizeof(uint32_t), s);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(partition_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, capA, idxA, idxB,
-                           cnt);
-        e = hipGetLastError();
-    }
-    // (the list-A launch on a forked stream, concurrent with list B's, took the same 713 us per call:
-    // profiles/r05/configC_partition_ab.txt)
-    if (e == hipSuccess) e = launch_crc_light_frag_copy(ListSource{d, idxA, cnt}, capA, img, out, s, 1u);
-    if (e == hipSuccess) {
-        const uint32_t fpg = frags_per_wg(n);
-        hipLaunchKernelGGL((crc_stream_kernel<ListSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
-                           frags_grid(n, fpg), dim3(64 * kStreamWv), 0, s, ListSource{d, idxB, cnt + 1}, n, fpg, img, out,
-                           nullptr);
-        e = hipGetLastError();
-    }
-    return scratch_done(s, scratch, pooled, e);
-}
-
 // Read-only CRC descriptor batches the census saw as equal whole-row fragments (R rows) at 16-byte-aligned
 // addresses: crc_regular_kernel<kDesc> on config B's schedule -- 4 KiB fragments in pairs (two chains per
 // wave, each reading a pair in turn; an odd last fragment on the table-light kernel), longer ones one per
@@ -4878,7 +4853,7 @@ static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint
     const size_t span = R == 1 ? 2 * kRowBytes : (size_t)R * kRowBytes;
     if (items > 0xFFFFFFFFull) return hipErrorInvalidValue;
     static const uint32_t fpw_env = [] {  // (A/B knob LAMPI_DESC_FPW: items per wave)
-        const char *e = std::getenv("LAMPI_DESC_FPW");
+        const char *e = LAMPI_AB_ENV("LAMPI_DESC_FPW");
         return e ? (uint32_t)std::atoi(e) : 0u;
     }();
     uint32_t fpw = pick_regular_fpw(items, span);
@@ -4928,7 +4903,7 @@ static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint
 // target (0: the count split).
 static uint32_t small_batch_groups(size_t n, hipStream_t s) {
     static const size_t target = [] {
-        const char *e = std::getenv("LAMPI_SMALL_BATCH");
+        const char *e = LAMPI_AB_ENV("LAMPI_SMALL_BATCH");
         return e ? (size_t)std::atoll(e) : (size_t)4096;
     }();
     // graph captures keep the count split: the groups' scratch would be a pooled allocation inside the graph
@@ -4957,7 +4932,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     bool small = false;
     rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &pairs, &nhalf, 1u, nullptr, &whole, true, &small);
     static const bool ro_pairs = [] {  // (A/B knob LAMPI_CRC_RO_PAIRS=0: read-only IB-sized batches on the piece streams)
-        const char *e = std::getenv("LAMPI_CRC_RO_PAIRS");
+        const char *e = LAMPI_AB_ENV("LAMPI_CRC_RO_PAIRS");
         return !(e && e[0] == '0');
     }();
     if (pairs && ro_pairs) return launch_crc_light_pair_copy(DescSource{d}, n, img, out, s, nhalf);
@@ -4966,7 +4941,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     // the table-light kernel stays ahead, 32 KiB 81 against 73%, 64 KiB 80 against 67%).  A/B knob
     // LAMPI_CRC_DESC_REGULAR = the most rows taken (0: never).
     static const uint32_t reg_desc = [] {
-        const char *e = std::getenv("LAMPI_CRC_DESC_REGULAR");
+        const char *e = LAMPI_AB_ENV("LAMPI_CRC_DESC_REGULAR");
         return e ? (uint32_t)std::atoi(e) : 7u;
     }();
     if (whole && rows_hint >= 1u && rows_hint <= reg_desc && n >= 2 * kRegDescMinPairs)
@@ -4977,11 +4952,6 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
                                           rows_hint <= kSegRows ? 1u : (rows_hint + kLightRoRows - 1) / kLightRoRows);
     if (rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<false, kStreamWv, kStreamCap>(d, n, out, img, s, rows_hint);
-    static const uint32_t part_div = [] {  // (A/B knob LAMPI_CRC_PARTITION, above)
-        const char *e = std::getenv("LAMPI_CRC_PARTITION");
-        return e ? (uint32_t)std::atoi(e) : 0u;
-    }();
-    if (part_div && rows_hint <= 1 && n > kSplitMax) return launch_crc_desc_partition(d, n, out, img, s, part_div);
     if (n >= kSplitMin && n <= kSplitMax && !small) {  // both size classes, one launch each (SplitDescSource)
         const uint32_t fpg = frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<SplitDescSource<false>, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),
@@ -5031,6 +5001,10 @@ hipError_t launch_desc_per_wave(const lampi_frag_desc *d, size_t n, uint32_t *ou
     return hipGetLastError();
 }
 
+template <bool kSum>
+static hipError_t launch_packed(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, uint32_t *out,
+                                const uint32_t *img, hipStream_t s, size_t *done);
+
 hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, size_t n,
                           uint32_t *out, const uint32_t *img, int grid, hipStream_t s) {
     (void)grid;
@@ -5042,9 +5016,26 @@ hipError_t launch_crc_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     // 128 KiB-2 MiB fragments on the regular kernel 73-74 -> 80.7-83.4%, 4 MiB 40.9 -> 80.7%, 16 MiB
     // 10.5 -> 80.9% (the regular kernel's chains are fragments: 256 of them starve the grid), and of
     // non-whole-row 65,552-131,056 B on the framed regular kernel (removed) 71-76.5 -> 76-82%.
+    // fragments of 64 B .. 2 KiB (powers of two) in packed rows of config B's kernel; the rest of the message
+    // (its last fragments) through the schedules below
+    static const bool packed = [] {  // (A/B knob LAMPI_PACKED=0: off)
+        const char *e = LAMPI_AB_ENV("LAMPI_PACKED");
+        return !(e && e[0] == '0');
+    }();
+    if (packed) {
+        size_t done = 0;
+        const hipError_t e = launch_packed<false>(base, msg_len, frag_len, partial, out, img, s, &done);
+        if (e != hipSuccess || done == 0) {
+            if (e != hipSuccess) return e;
+        } else {
+            if (done >= n) return hipSuccess;
+            return launch_crc_msg(base + done * frag_len, msg_len - done * frag_len, frag_len, partial, n - done,
+                                  out + done, img, grid, s);
+        }
+    }
     const size_t R = (frag_len + kRowBytes - 1) / kRowBytes;
     static const bool ro_pairs = [] {  // (A/B knob LAMPI_CRC_RO_PAIRS=0, as launch_crc_desc)
-        const char *e = std::getenv("LAMPI_CRC_RO_PAIRS");
+        const char *e = LAMPI_AB_ENV("LAMPI_CRC_RO_PAIRS");
         return !(e && e[0] == '0');
     }();
     if (ro_pairs && frag_len > 1024 && frag_len <= kRowBytes / 2 && (frag_len & 15u) != 0 && n >= kShapeMin &&
@@ -5096,6 +5087,48 @@ static hipError_t launch_regular(const uint8_t *base, size_t n, size_t frag_len,
                        dim3(kBlock), 0, s, base + done * frag_len, (uint32_t)m, fpw, frag_len, partial, img, out + done,
                        nullptr, (size_t)0);
     return hipGetLastError();
+}
+
+// Packed rows (crc_regular_kernel<kSub < 64>): a message of 64 * kSub-byte fragments (kSub = 1 .. 32: 64 B ..
+// 2 KiB) at a 16-byte-aligned base on config B's schedule, 64 / kSub fragments per 4 KiB row, two rows per
+// chain item (kV = 2).  Takes the first *done fragments -- whole pairs of rows -- and leaves the rest (fewer
+// than 128 / kSub plus the message's last, possibly short, fragment) to the caller.
+constexpr size_t kPackedMinRows = 256;  // smaller messages keep the other schedules (one launch)
+template <bool kSum, int kSub>
+static hipError_t launch_packed_k(const uint8_t *base, size_t nv, uint32_t partial, uint32_t *out, const uint32_t *img,
+                                  hipStream_t s) {
+    static const uint32_t fpw_env = [] {  // (A/B knob LAMPI_PACKED_FPW: items per wave)
+        const char *e = LAMPI_AB_ENV("LAMPI_PACKED_FPW");
+        return e ? (uint32_t)std::atoi(e) : 0u;
+    }();
+    // (config B's choice, 12 items per wave; 1 GiB of 1 KiB fragments: 16 items 71.4%, 8 70.6%, 6 70.5-70.9%, 4 66%;
+    // a balanced grid of whole rounds of resident workgroups 68.6-71.1%: profiles/r06/packed_fpw.txt)
+    const uint32_t fpw = fpw_env ? fpw_env : pick_regular_fpw(nv, 2 * kRowBytes);
+    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 2, kSum, kWaves, 0, false, kSub>),
+                       grid_for(nv, fpw),
+                       dim3(kBlock), 0, s, base, (uint32_t)nv, fpw, 2 * kRowBytes, partial, img, out, nullptr, (size_t)0);
+    return hipGetLastError();
+}
+template <bool kSum>
+static hipError_t launch_packed(const uint8_t *base, size_t msg_len, size_t frag_len, uint32_t partial, uint32_t *out,
+                                const uint32_t *img, hipStream_t s, size_t *done) {
+    *done = 0;
+    if (((uintptr_t)base & 15u) != 0 || frag_len < 64 || frag_len > kRowBytes / 2 || (frag_len & (frag_len - 1)) != 0)
+        return hipSuccess;
+    const size_t rows = msg_len / kRowBytes, nv = rows / 2;  // whole 8 KiB items: every fragment in them is full
+    if (rows < kPackedMinRows || nv > 0xFFFFFFFFull) return hipSuccess;
+    hipError_t e = hipErrorInvalidValue;
+    switch (frag_len) {
+        case 64: e = launch_packed_k<kSum, 1>(base, nv, partial, out, img, s); break;
+        case 128: e = launch_packed_k<kSum, 2>(base, nv, partial, out, img, s); break;
+        case 256: e = launch_packed_k<kSum, 4>(base, nv, partial, out, img, s); break;
+        case 512: e = launch_packed_k<kSum, 8>(base, nv, partial, out, img, s); break;
+        case 1024: e = launch_packed_k<kSum, 16>(base, nv, partial, out, img, s); break;
+        case 2048: e = launch_packed_k<kSum, 32>(base, nv, partial, out, img, s); break;
+        default: return hipSuccess;
+    }
+    if (e == hipSuccess) *done = nv * 2 * (kRowBytes / frag_len);
+    return e;
 }
 
 hipError_t launch_crc_regular(const uint8_t *base, size_t n, size_t frag_len, uint32_t partial, uint32_t *out,
@@ -5174,11 +5207,11 @@ static hipError_t launch_sum_copy_groups(const Src &src, size_t n, uint32_t *out
 // (fewest rows for fragments that are not whole rows, 0 = never groups), LAMPI_SUM_CP_GRP_ROWS (rows per group).
 static uint32_t sum_copy_groups(uint32_t R, bool whole_rows) {
     static const uint32_t grp_min = [] {
-        const char *e = std::getenv("LAMPI_SUM_CP_GRP_MIN");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_CP_GRP_MIN");
         return e ? (uint32_t)std::atoi(e) : 64u;
     }();
     static const uint32_t grp_rows = [] {
-        const char *e = std::getenv("LAMPI_SUM_CP_GRP_ROWS");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_CP_GRP_ROWS");
         return e ? (uint32_t)std::max(1, std::atoi(e)) : 1u;
     }();
     if (!grp_min || R < 2 || (!whole_rows && R < grp_min)) return 1u;
@@ -5284,15 +5317,15 @@ hipError_t launch_sum64_finish(const uint64_t *vals, uint32_t nv, const uint8_t 
 // workgroup target, LAMPI_SUM_RO_GROUPS=0 = the round-4 schedules (groups of <= 8 up to 256 rows, segments above).
 static uint32_t sum_ro_groups(size_t n, uint32_t R) {
     static const size_t onewg = [] {
-        const char *e = std::getenv("LAMPI_SUM_RO_ONEWG");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_RO_ONEWG");
         return e ? (size_t)std::atoll(e) : (size_t)4096;
     }();
     static const size_t wgs = [] {
-        const char *e = std::getenv("LAMPI_SUM_RO_WGS");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_RO_WGS");
         return e ? (size_t)std::atoll(e) : (size_t)65536;
     }();
     static const bool r5 = [] {
-        const char *e = std::getenv("LAMPI_SUM_RO_GROUPS");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_RO_GROUPS");
         return !(e && e[0] == '0');
     }();
     if (!r5) return R <= 256u && sum_groups(n, min(R, 8u)) > 1 ? min(R, 8u) : 0xFFFFFFFFu;
@@ -5320,7 +5353,7 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &half, &nh, 2u, &one_row, nullptr, false,
                                       nullptr, &tiny);
     static const bool sum_tiny = [] {  // (A/B knob LAMPI_SUM_TINY=0, as launch_sum_msg)
-        const char *e = std::getenv("LAMPI_SUM_TINY");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_TINY");
         return !(e && e[0] == '0');
     }();
     if (img && sum_tiny && tiny && rows_hint <= 1 && n / 256 >= 256) {  // (as launch_sum_msg: 256 per workgroup)
@@ -5332,7 +5365,7 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     // (sum_copy_waves_kernel, IB's SUM copies' schedule; profiles/r05/sum_ro_waves_ab.txt: 1,976 B 45.5 -> 69.5%,
     // 1 KiB 35.6 -> 64.3%, 2 KiB 58.5 -> 80.4%, 256 B 10.2 -> 20.8%).  A/B knob LAMPI_SUM_RO_WAVES=0: off.
     static const bool ro_waves = [] {
-        const char *e = std::getenv("LAMPI_SUM_RO_WAVES");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_RO_WAVES");
         return !(e && e[0] == '0');
     }();
     if (img && ro_waves && half && rows_hint <= 1) {
@@ -5354,7 +5387,7 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     // workgroup 83.2%, four 82.7%; config C's mixed sizes lost 0.5 on it and keep the piece streams).  A/B knob
     // LAMPI_SUM_RO_WG = fragments per workgroup (0: off).
     static const uint32_t ro_wg = [] {
-        const char *e = std::getenv("LAMPI_SUM_RO_WG");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_RO_WG");
         return e ? (uint32_t)std::atoi(e) : 2u;
     }();
     if (img && ro_wg && one_row && rows_hint <= 1) {
@@ -5386,13 +5419,28 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     // 84.6%; 1 MiB 77.2 -> 88.4%.  A/B knobs LAMPI_SUM_MSG_WG = fragments per workgroup (0: off),
     // LAMPI_SUM_MSG_MAX = the longest fragment taken (bytes).
     static const uint32_t msg_wg = [] {
-        const char *e = std::getenv("LAMPI_SUM_MSG_WG");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_MSG_WG");
         return e ? (uint32_t)std::atoi(e) : 1u;
     }();
     static const size_t msg_max = [] {
-        const char *e = std::getenv("LAMPI_SUM_MSG_MAX");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_MSG_MAX");
         return e ? (size_t)std::atoll(e) : ~(size_t)0;
     }();
+    // fragments of 64 B .. 1 KiB (powers of two) in packed rows of config B's kernel (2 KiB: one per wave reads
+    // faster, below); the message's last fragments through the schedules below
+    static const size_t packed_max = [] {  // (A/B knob LAMPI_PACKED_SUM = the longest fragment taken, 0: off)
+        const char *e = LAMPI_AB_ENV("LAMPI_PACKED_SUM");
+        return e ? (size_t)std::atoll(e) : (size_t)1024;
+    }();
+    if (frag_len <= packed_max) {
+        size_t done = 0;
+        const hipError_t e = launch_packed<true>(base, msg_len, frag_len, 0u, out, nullptr, s, &done);
+        if (e != hipSuccess) return e;
+        if (done >= n && done) return hipSuccess;
+        if (done)
+            return launch_sum_msg(base + done * frag_len, msg_len - done * frag_len, frag_len, n - done, out + done, img,
+                                  grid, s);
+    }
     const uint32_t R = (uint32_t)std::min<size_t>((frag_len + kRowBytes - 1) / kRowBytes, 0xFFFFFFFFu);
     if (msg_wg && frag_len <= msg_max && (n >= 256 || R > 8) && R > 1 && img) {  // (few large fragments too:
         // 16 x 16 MiB on the regular kernel, one fragment per chain, read 1.9%)
@@ -5409,14 +5457,14 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
     }
     // fragments of at most 2 KiB one per wave (as launch_sum_desc: 1,976 B 51.2 -> 74.9%, 2 KiB 68 -> 84.2%)
     static const bool ro_waves = [] {
-        const char *e = std::getenv("LAMPI_SUM_RO_WAVES");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_RO_WAVES");
         return !(e && e[0] == '0');
     }();
     // messages of fragments up to 1 KiB: the SUM piece streams with 256 fragments per workgroup (many fragments
     // share a row; profiles/r05/sum_tiny_ab.txt: 64 B 6.5 -> 19.8%, 256 B 22.8 -> 48.6%, 512 B 44.7 -> 67.6%,
     // 1 KiB 70.2 -> 72.4%).  A/B knob LAMPI_SUM_TINY = the longest fragment taken (0: off).
     static const uint32_t tiny_max = [] {
-        const char *e = std::getenv("LAMPI_SUM_TINY");
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_TINY");
         return e ? (uint32_t)std::atoi(e) : 1024u;
     }();
     if (img && frag_len <= tiny_max && n / 256 >= 256) {

@@ -41,6 +41,13 @@ CASES = [
     (2, 16384, 65456, 1, (1,)),
     (2, 1024, 1048576, 1, (1,)),           # --desc --mode sum, 1 MiB / 4 MiB
     (2, 256, 4194304, 1, (1,)),
+    (1, 1048576, 1024, 1, (1,)),           # config A shape in SUM mode (round 6: packed rows)
+    (2, 16777216, 64, 0, (1,)),            # --frags 16777216 --frag-bytes 64: 1 GiB of 64-byte fragments
+    (2, 16777216, 64, 1, (1,)),
+    (2, 4194304, 256, 0, (1,)),            # 1 GiB of 256-byte fragments
+    (2, 4194304, 256, 1, (1,)),
+    (2, 2097152, 512, 0, (1,)),            # 1 GiB of 512-byte fragments
+    (2, 2097152, 512, 1, (1,)),
 ]
 # config D per-GPU shards: (seed, n_total, L, mode, nshard)
 SHARD_CASES = [(3, 33554432, 16384, 0, 8), (3, 33554432, 16384, 1, 8)]

@@ -259,3 +259,27 @@ def test_mode_flag_macros_match_the_binding(tmp_path):
     assert mask & (BY_BYTES | CRC32 | SUM32) == 0 and of_all == 4095
     with pytest.raises(ValueError):
         rows_hint_bits(4096)
+
+
+def test_default_library_reads_no_ab_knobs():
+    """the schedule knobs measured in A/B runs are compiled only into the A/B build
+    (make AB=1 -> liblampi_csum_ab.so, LAMPI_AB_KNOBS); the default library's dispatch depends on no
+    environment variable but the documented switches (LAMPI_CSUM_NO_SHAPES, LAMPI_HOST_CHUNK_BYTES) -- none of
+    the knob names is in its binary, and every getenv in the sources goes through LAMPI_AB_ENV or is documented."""
+    csrc = os.path.join(ROOT, "lampi_amd", "csrc")
+    knobs, documented = set(), {"LAMPI_CSUM_NO_SHAPES", "LAMPI_HOST_CHUNK_BYTES"}
+    for name in os.listdir(csrc):
+        if not name.endswith((".hip", ".cc", ".h")):
+            continue
+        src = open(os.path.join(csrc, name)).read()
+        knobs |= set(re.findall(r'LAMPI_AB_ENV\("([A-Z0-9_]+)"\)', src))
+        direct = set(re.findall(r'getenv\("([A-Z0-9_]+)"\)', src))
+        assert direct <= documented, (name, direct - documented)
+    assert len(knobs) >= 20, knobs
+    import lampi_amd
+
+    blob = open(lampi_amd._lib.LIB_PATH, "rb").read()
+    present = sorted(k for k in knobs if k.encode() in blob)
+    assert not present, present
+    for k in documented:
+        assert k.encode() in blob, k

@@ -72,6 +72,57 @@ def test_regular_batches_every_schedule(cuda, oracle, L, mode):
         assert np.array_equal(got, want), (L, n, mode)
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("L", [64, 128, 256, 512, 1024, 2048])
+def test_packed_row_messages(cuda, oracle, L, mode):
+    """Messages of 64 B .. 2 KiB fragments on config B's kernel in packed rows (round 6: 64 / kSub fragments per
+    4 KiB row, crc_regular_kernel<kSub>): whole 8 KiB items through the packed launch, the rest -- a tail of up to
+    two rows' fragments and a short last fragment -- through the other schedules; random registers (CRC), an
+    unaligned base (no packed launch), sizes just at and above the packed minimum (256 rows)."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(L + 7 * mode)
+    cases = [(256 * 4096, 0), (256 * 4096 + 3 * L + 17, 0), (257 * 4096 + L, 0), (600 * 4096 + 1, 0),
+             (300 * 4096 + 5 * L, 4), (300 * 4096, 3), (255 * 4096 + 4 * L + 1, 0)]
+    for msg_len, off in cases:
+        part = int(rng.integers(0, 2**32))
+        buf = torch.empty(msg_len + off, dtype=torch.uint8, device=cuda)
+        dv.fill_stream(buf, seed=msg_len + L)
+        got = dv.as_u32(dv.msg_csum(buf[off:], L, partial=part, mode=mode))
+        host = buf.cpu().numpy()
+        n = (msg_len + L - 1) // L
+        offs = off + np.arange(n, dtype=np.uint64) * L
+        lens = np.minimum(L, msg_len + off - offs).astype(np.uint32)
+        want = oracle.desc_batch(host, offs, lens, np.full(n, part, np.uint32) if mode == 0 else None, mode)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (L, msg_len, off, bad[:8].tolist())
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+def test_config_a_shape_full_digest(cuda, mode):
+    """Config A's workload on the GPU (1M x 1 KiB, stream seed 1: BASELINE.md's digest feb61101 / 41fadf13 in CRC,
+    tests/golden/bench_digests.json in SUM) through the message entry point (packed rows)."""
+    import json
+
+    import torch
+
+    from oracle.oracle import digest
+
+    dv = _dv()
+    n, L = 1048576, 1024
+    buf = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=1)
+    v = dv.as_u32(dv.msg_csum(buf, L, mode=mode))
+    if mode == 0:
+        assert digest(v) == (0xFEB61101, 0x41FADF13)
+    else:
+        with open(os.path.join(os.path.dirname(__file__), "golden", "bench_digests.json")) as f:
+            e = [x for x in json.load(f)["entries"] if (x["seed"], x["n_total"], x["frag_bytes"], x["mode"]) ==
+                 (1, n, L, "sum") and "nshard" not in x][0]
+        assert digest(v) == (e["xor"], e["wsum"])
+
+
 @pytest.mark.parametrize("L", [1, 3, 15, 16, 17, 63, 64, 1976, 4095, 4096, 4097, 16384, 65456, (1 << 20) + 48])
 def test_sum_messages_short_lived_workgroups(cuda, oracle, L):
     """lampi_msg_csum SUM of messages of >= 256 fragments (one fragment per short-lived 128-thread workgroup,

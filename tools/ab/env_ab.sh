@@ -3,6 +3,7 @@
 # Each run: bench.py with VAR=VALUE ("-" = unset); prints value, roofline frac, kernel ms and parity.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export LAMPI_CSUM_LIB="$PWD/lampi_amd/liblampi_csum_ab.so"  # the A/B build: knobs read from the environment
 mkdir -p gpurun_out
 var=$1; rounds=$2; args=$3; shift 3
 for r in $(seq 1 "$rounds"); do
