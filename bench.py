@@ -373,6 +373,54 @@ def shard_plan(args, world: int, rank: int):
     return n, L, seed, k0, kstep, n_global
 
 
+def _read_schedule(crc: bool, desc: bool, n: int, L: int, rows_hint: int) -> str:
+    """The read-only kernel the library's dispatch picks for a uniform batch of n x L-byte fragments (16-byte-aligned
+    buffer; lampi_msg_csum, or lampi_frag_csum_batch with --desc once the census has seen the batch), as
+    launch_crc_msg / launch_sum_msg / launch_crc_desc / launch_sum_desc choose it."""
+    R = (L + 4095) // 4096
+    pow2 = L & (L - 1) == 0
+    if desc:
+        if rows_hint > 1:
+            return ("crc_light_frag_copy_kernel<DescSource> (read-only, row groups + crc_light_group_join_kernel)"
+                    if crc and rows_hint >= 8 else "crc_stream_kernel<RowSegSource%s> (16-row segments)"
+                    % ("" if crc else ", kSum"))
+        if crc:
+            if L % 4096 == 0 and R <= 7 and n >= 4096:
+                return ("crc_regular_kernel<kDesc> (learned: equal whole-row fragments, config B's schedule with "
+                        "per-fragment addresses; crc_light_pair_leftover_kernel for off-shape ones)")
+            if R >= 8:
+                return "crc_light_frag_copy_kernel<DescSource> (learned: one wave per fragment, read-only)"
+            if 1024 < L <= 2048 and L % 16:
+                return "crc_light_pair_copy_kernel<DescSource> (learned: two fragments per wave)"
+            return "crc_stream_kernel<DescSource> (piece streams)"
+        if 2 <= R <= 8 and n >= 4096:
+            return "sum_copy_wg_kernel<DescSource> (learned: one fragment per short-lived workgroup)"
+        if R > 1:
+            return "sum_copy_wg_kernel<GroupSource<DescSource>> + sum_group_join_kernel (learned row groups)"
+        if L <= 1024:
+            return "crc_stream_kernel<DescSource, kSum> (piece streams, 256 fragments per workgroup)"
+        if L <= 2048:
+            return "sum_copy_waves_kernel<DescSource> (learned: one fragment per wave)"
+        return "sum_copy_wg_kernel<DescSource> (learned: two one-row fragments per workgroup)"
+    if pow2 and 64 <= L <= (2048 if crc else 1024) and n * L >= 256 * 4096:
+        return f"crc_regular_kernel<{'kSum, ' if not crc else ''}kSub = {L // 64}> (packed rows: {4096 // L} fragments per 4 KiB row)"
+    if crc:
+        if L % 4096 == 0 and R < 8 and L != 65536:
+            return "crc_regular_kernel"
+        if R >= 8:
+            return "crc_light_frag_copy_kernel<MsgSource> (read-only, one wave per fragment; > 16 rows: 8-row groups)"
+        if 1024 < L <= 2048 and L % 16 and n >= 256:
+            return "crc_light_pair_copy_kernel<MsgSource> (two fragments per wave)"
+        return "crc_stream_kernel<MsgSource> (piece streams)"
+    if R > 1 and (n >= 256 or R > 8):
+        return "sum_copy_wg_kernel<MsgSource> (one fragment per short-lived workgroup, or row groups)"
+    if L <= 2048 and n >= 256:
+        return "sum_copy_waves_kernel<MsgSource> (one fragment per wave)"
+    if n >= 256:
+        return "sum_copy_wg_kernel<MsgSource> (one fragment per short-lived workgroup)"
+    return "crc_regular_kernel (kSum)" if L % 4096 == 0 else "crc_stream_kernel<MsgSource, kSum>"
+
+
 def _copy_schedule(crc: bool, src: str, L: int, rows_hint: int) -> str:
     """The kernels a uniform batch of L-byte descriptor copies / receives runs once the stream's census
     has landed (frag_csum.hip learned_rows_hint: kShapeRows 8 CRC / kShapeRowsSum 4 SUM, pairs at <= 2 KiB)."""
@@ -558,18 +606,7 @@ def run_device(args):
         # PMC traffic is recorded per kernel: the descriptor runs have no entry of their own
         cfg_key = f"{'crc' if crc else 'sum'}_{'desc_' if args.desc else ''}{n}x{L}"
         traffic = None if args.dry_run else read_traffic(cfg_key)
-        kernel = ("none (dry run)" if args.dry_run else
-                  "crc_light_frag_copy_kernel<DescSource> (read-only, row groups + crc_light_group_join_kernel)"
-                  if args.desc and crc and args.rows_hint >= 8 else
-                  "crc_stream_kernel<RowSegSource> (descriptors, 16-row segments)"
-                  if args.desc and crc and args.rows_hint > 1 else
-                  "crc_stream_kernel<RowSegSource, kSum> (descriptors, 16-row segments)"
-                  if args.desc and args.rows_hint > 1 else
-                  "learned schedule (DESIGN.md 4.2 census): crc_stream_kernel (descriptors) until a shape is "
-                  "learned, then the row-group schedule the census picks" if args.desc and crc else
-                  "learned schedule (DESIGN.md 4.2 census): crc_stream_kernel<kSum> (descriptors) until a shape "
-                  "is learned, then the row-segment schedule the census picks" if args.desc else
-                  "crc_regular_kernel" if crc else "crc_regular_kernel (kSum: uicsum on the same schedule)")
+        kernel = "none (dry run)" if args.dry_run else _read_schedule(crc, args.desc, n, L, args.rows_hint)
         workload = (f"config D shard {args.shard} of 8: {n} x {L} B fragments k = {args.shard} (mod 8), seed 3"
                     if args.shard is not None else
                     f"{n} x {L} B fragments per GPU, device-resident, "

@@ -5102,11 +5102,12 @@ static hipError_t launch_packed_k(const uint8_t *base, size_t nv, uint32_t parti
         return e ? (uint32_t)std::atoi(e) : 0u;
     }();
     // (config B's choice, 12 items per wave; 1 GiB of 1 KiB fragments: 16 items 71.4%, 8 70.6%, 6 70.5-70.9%, 4 66%;
-    // a balanced grid of whole rounds of resident workgroups 68.6-71.1%: profiles/r06/packed_fpw.txt)
+    // a balanced grid of whole rounds of resident workgroups 68.6-71.1%, profiles/r06/packed_fpw.txt; a tapered grid
+    // ending on 512-2,048 workgroups of 2-6 items 68-72%, profiles/r06/packed_taper.txt)
     const uint32_t fpw = fpw_env ? fpw_env : pick_regular_fpw(nv, 2 * kRowBytes);
     hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 2, kSum, kWaves, 0, false, kSub>),
-                       grid_for(nv, fpw),
-                       dim3(kBlock), 0, s, base, (uint32_t)nv, fpw, 2 * kRowBytes, partial, img, out, nullptr, (size_t)0);
+                       grid_for(nv, fpw), dim3(kBlock), 0, s, base, (uint32_t)nv, fpw, 2 * kRowBytes, partial, img, out,
+                       nullptr, (size_t)0);
     return hipGetLastError();
 }
 template <bool kSum>
