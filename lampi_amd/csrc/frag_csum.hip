@@ -3253,7 +3253,55 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     const uint32_t nfr = f0 < n ? min(fpw, (n - f0 + kWv - 1) / kWv) : 0u;
     const uint32_t ngrp = (nfr + K - 1) / K;
     const uint32_t lane_off = (uint32_t)lane * (kCoal ? kChunkBytes : kLaneBytes);
-    const uint32_t vinit = __builtin_bswap32(partial);
+    uint32_t vinit = __builtin_bswap32(partial);
+    // packed rows over a descriptor batch (read-only CRC; dst = the lampi_frag_desc array, base unused): a batch the
+    // census saw as one contiguous run of equal fragments (fragment i = d[0].addr + i * L, L = 64 kSub, d[0]'s
+    // register) runs as that message.  Each wave first checks the descriptors of its items (F = 128 / kSub
+    // fragments each, one 16-byte load per lane and item, clamped so every load is issued): an item holding any
+    // other fragment is read at a dummy address (the table image), not emitted, and its F / 2 fragment pairs are
+    // listed for crc_light_pair_leftover_kernel -- no address outside the batch's own fragments is read.
+    uint64_t pbad = 0u;
+    const uint8_t *pbase = base;
+    if constexpr (kSub < 64 && !kSum) {
+        if (dst != nullptr) {
+            const lampi_frag_desc *pd = reinterpret_cast<const lampi_frag_desc *>(dst);
+            const uint64_t a0 = uniform64(pd[0].addr);
+            const uint32_t p0 = uniform(pd[0].partial);
+            constexpr uint32_t L = 64u * kSub, F = 128u / kSub, kPer = F > 64 ? 2 : 1;
+            pbase = reinterpret_cast<const uint8_t *>(a0);
+            vinit = __builtin_bswap32(p0);
+            constexpr uint32_t kBatch = kPer == 2 ? 6u : 12u;  // items checked per round (12 x 4 VGPRs in flight)
+            for (uint32_t j0 = 0; j0 < nfr; j0 += kBatch) {
+                lampi_frag_desc x[kBatch][kPer];
+#pragma unroll
+                for (uint32_t jj = 0; jj < kBatch; ++jj)
+#pragma unroll
+                    for (uint32_t h = 0; h < kPer; ++h) {
+                        const uint32_t j = min(j0 + jj, nfr - 1u), k = min(lane + 64u * h, F - 1u);
+                        x[jj][h] = pd[(size_t)(f0 + kWv * j) * F + k];
+                    }
+#pragma unroll
+                for (uint32_t jj = 0; jj < kBatch; ++jj) {
+                    const uint32_t j = j0 + jj;
+                    bool bad = false;
+#pragma unroll
+                    for (uint32_t h = 0; h < kPer; ++h) {
+                        const uint64_t fi = (uint64_t)(f0 + kWv * min(j, nfr - 1u)) * F + min(lane + 64u * h, F - 1u);
+                        bad |= x[jj][h].addr != a0 + fi * L || x[jj][h].length != L || x[jj][h].partial != p0;
+                    }
+                    if (j < nfr && __ballot(bad)) pbad |= 1ull << j;
+                }
+            }
+            pbad = uniform64(pbad);
+            for (uint64_t m = pbad; m; m &= m - 1) {  // list the item's fragment pairs
+                const uint32_t item = f0 + kWv * (uint32_t)__builtin_ctzll(m);
+                uint32_t e0 = 0u;
+                if (lane == 0) e0 = atomicAdd(left, F / 2u);
+                e0 = uniform(e0);
+                if (lane < F / 2u) list[e0 + lane] = item * (F / 2u) + lane;
+            }
+        }
+    }
     // kDesc: lane kV j + r holds fragment kV (f0 + kWv j) + r's descriptor; bad bit j: item j is listed
     uint32_t da_lo = 0u, da_hi = 0u, dpart = 0u;
     uint64_t bad = 0u;
@@ -3308,7 +3356,10 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
             const uint64_t ro = kV == 2 || !(nfr && !((bad >> j) & 1u)) ? 0u : (uint64_t)r * kRowBytes;
             return (gbyte *)(a + ro + lane_off);
         }
-        return (gbyte *)(base + ((uint64_t)(nfr ? f : 0u) * frag_len + (uint64_t)r * kRowBytes + lane_off));
+        if constexpr (kSub < 64 && !kSum) {
+            if (pbad >> ((f - f0) / kWv) & 1u) return (gbyte *)((const uint8_t *)img + lane_off);
+        }
+        return (gbyte *)(pbase + ((uint64_t)(nfr ? f : 0u) * frag_len + (uint64_t)r * kRowBytes + lane_off));
     };
     auto issue = [&](const GroupTask &t, RowsK<K> &b) {
 #pragma unroll
@@ -3420,7 +3471,7 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
             if ((lane & (kSub - 1)) == kSub - 1) {
 #pragma unroll
                 for (int c = 0; c < K; ++c)
-                    if (K * t.i + c < nfr)
+                    if (K * t.i + c < nfr && !((pbad >> (K * t.i + c)) & 1u))
                         out[(frag(t.i, c) * kV + t.r) * (64u / kSub) + lane / kSub] = __builtin_bswap32(x[c]);
             }
             return;
@@ -4434,7 +4485,10 @@ struct BatchShape {
     uint32_t nmis;     // how many were 1-2 KiB and ended off the 16-byte grid
     uint32_t n12k;     // how many were 1-2 KiB
     uint32_t n1k;      // how many were at most 1 KiB
-    uint32_t pad[3];
+    uint32_t ncontig;  // how many lay where a contiguous run of equal fragments from fragment 0 puts them (fragment i
+                       // at d[0].addr + i * d[0].length, the same length and register; d[0].addr 16-byte aligned)
+    uint32_t len0;     // fragment 0's length
+    uint32_t pad;
 };
 constexpr int kShapeSlots = 8;  // shape records per (thread, device, stream): descriptor arrays remembered
 constexpr int64_t kLeftBytes = 256;
@@ -4630,9 +4684,14 @@ template <class Src>
 __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, BatchShape *rec, uint32_t seq) {
     const uint32_t l = threadIdx.x;
     const uint32_t m = (uint32_t)min<size_t>(n, 64);
-    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u, full = 0u, mis = 0u, k12 = 0u, k1 = 0u;
+    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u, full = 0u, mis = 0u, k12 = 0u, k1 = 0u, contig = 0u;
+    const FragInfo f0i = src.get(0);  // (sample 0 is fragment 0: the run's start)
     if (l < m) {
-        const FragInfo fi = src.get((size_t)l * n / m);
+        const size_t idx = (size_t)l * n / m;
+        const FragInfo fi = src.get(idx);
+        contig = fi.len == f0i.len && fi.partial == f0i.partial && ((uintptr_t)f0i.addr & 15u) == 0 &&
+                         (uint64_t)(uintptr_t)fi.addr == (uint64_t)(uintptr_t)f0i.addr + (uint64_t)idx * f0i.len
+                     ? 1u : 0u;
         const uint32_t R = (uint32_t)(((uint64_t)fi.len + kRowBytes - 1) / kRowBytes);
         rmin = R;
         rmax = R;
@@ -4650,6 +4709,7 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         mis += (uint32_t)__shfl_xor((int)mis, o);
         k12 += (uint32_t)__shfl_xor((int)k12, o);
         k1 += (uint32_t)__shfl_xor((int)k1, o);
+        contig += (uint32_t)__shfl_xor((int)contig, o);
     }
     if (l == 0) {
         volatile BatchShape *r = rec;
@@ -4661,6 +4721,8 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         r->nmis = mis;
         r->n12k = k12;
         r->n1k = k1;
+        r->ncontig = contig;
+        r->len0 = f0i.len;
         __threadfence_system();
         r->seq = seq;
     }
@@ -4681,7 +4743,8 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
                                   bool *pairs = nullptr, uint32_t **nhalf_dev = nullptr,
                                   uint32_t min_rows = kShapeRows, bool *one_row = nullptr,
                                   bool *full_rows = nullptr, bool pairs_misaligned_only = false,
-                                  bool *all_half = nullptr, bool *all_1k = nullptr) {
+                                  bool *all_half = nullptr, bool *all_1k = nullptr, uint32_t *contig_len = nullptr) {
+    if (contig_len) *contig_len = 0u;
     if (all_half) *all_half = false;
     if (all_1k) *all_1k = false;
     if (pairs) *pairs = false;
@@ -4732,7 +4795,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     const uint32_t q0 = v->seq;
     std::atomic_thread_fence(std::memory_order_acquire);  // the fields are read after the first seq ...
     const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf, nwhole = v->nwhole,
-                   nmis = v->nmis, n12k = v->n12k, n1k = v->n1k;
+                   nmis = v->nmis, n12k = v->n12k, n1k = v->n1k, ncontig = v->ncontig, len0 = v->len0;
     std::atomic_thread_fence(std::memory_order_acquire);  // ... and before the second (a seqlock read)
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= min_rows && rmax <= 2 * rmin) W = rmax;
@@ -4744,6 +4807,9 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
         if (full_rows && nwhole == sampled && rmin == rmax && !slot.pair_broken) *full_rows = true;
         if (all_half && nhalf == sampled) *all_half = true;  // every sampled fragment at most 2 KiB
         if (all_1k && n1k == sampled) *all_1k = true;        // ... at most 1 KiB
+        // every sampled fragment where one contiguous run of equal fragments puts it (packed rows; the pair counters
+        // list the items that are not, so not on a stream whose counters are broken)
+        if (contig_len && ncontig == sampled && !slot.pair_broken) *contig_len = len0;
         if (pairs && nhalf == sampled && !slot.pair_broken &&
             (!pairs_misaligned_only || (n12k == sampled && 4 * nmis >= sampled))) {  // every sampled fragment at
             // most 2 KiB: two per wave (read-only: 1-2 KiB each, a quarter or more ending off the 16-byte grid)
@@ -4846,6 +4912,7 @@ constexpr size_t kSplitMin = 1024, kSplitMax = 65536;
 // chain row by row -- the items holding any other fragment listed by the kernel and checksummed by
 // crc_light_pair_leftover_kernel (the pair kernel's counters and leftover launch).
 constexpr size_t kRegDescMinPairs = 2048;
+constexpr size_t kPackedMinRows = 256;  // packed rows: smaller batches keep the other schedules (one launch)
 static uint32_t pick_regular_fpw(size_t n, size_t span);
 static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
                                         hipStream_t s, uint32_t R) {
@@ -4890,6 +4957,51 @@ static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint
     return e;
 }
 
+// Read-only CRC descriptor batches the census saw as one contiguous run of equal L-byte fragments (L = 64 B .. 2 KiB,
+// a power of two; config A's shape as descriptors): the message's packed rows (crc_regular_kernel<kSub>) over the
+// whole 8 KiB items from d[0].addr, each wave checking its items' descriptors first; items holding anything else are
+// listed by fragment pairs for crc_light_pair_leftover_kernel; the last fragments (past the whole items) on the
+// count split.
+template <int kSub>
+static hipError_t launch_packed_desc_k(const lampi_frag_desc *d, size_t nv, uint32_t *out, const uint32_t *img,
+                                       hipStream_t s, uint32_t *list, uint32_t *left) {
+    const uint32_t fpw = pick_regular_fpw(nv, 2 * kRowBytes);
+    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 2, false, kWaves, 0, false, kSub>),
+                       grid_for(nv, fpw), dim3(kBlock), 0, s, (const uint8_t *)nullptr, (uint32_t)nv, fpw,
+                       2 * kRowBytes, 0u, img, out, (uint8_t *)const_cast<lampi_frag_desc *>(d), (size_t)0, list, left);
+    return hipGetLastError();
+}
+static hipError_t launch_crc_desc_packed(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
+                                         hipStream_t s, uint32_t L, size_t *done) {
+    *done = 0;
+    const size_t F = 2 * kRowBytes / L, nv = n / F;
+    if (nv * 2 < kPackedMinRows || nv > 0xFFFFFFFFull || nv * F / 2 > 0xFFFFFFFFull) return hipSuccess;
+    uint32_t *list = nullptr, *left = nullptr, *next_left = nullptr;
+    bool pooled = false;
+    hipError_t e = stream_scratch(s, (nv * F / 2 + 1) * sizeof(uint32_t), (void **)&list, &pooled);
+    if (e != hipSuccess) return e;
+    e = pair_counters(s, &left, &next_left);
+    if (e != hipSuccess) return scratch_done(s, list, pooled, e);
+    switch (L) {
+        case 64: e = launch_packed_desc_k<1>(d, nv, out, img, s, list, left); break;
+        case 128: e = launch_packed_desc_k<2>(d, nv, out, img, s, list, left); break;
+        case 256: e = launch_packed_desc_k<4>(d, nv, out, img, s, list, left); break;
+        case 512: e = launch_packed_desc_k<8>(d, nv, out, img, s, list, left); break;
+        case 1024: e = launch_packed_desc_k<16>(d, nv, out, img, s, list, left); break;
+        default: e = launch_packed_desc_k<32>(d, nv, out, img, s, list, left); break;
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(crc_light_pair_leftover_kernel<DescSource>, dim3(kLeftoverWgs), dim3(256), 0, s,
+                           DescSource{d}, nv * F, img, out, (const uint32_t *)left, next_left, (const uint32_t *)list,
+                           (uint32_t *)nullptr);
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) reset_pair_counters(s);
+    e = scratch_done(s, list, pooled, e);
+    if (e == hipSuccess) *done = nv * F;
+    return e;
+}
+
 // Read-only descriptor batches under the learned-shape minimum (kShapeMin fragments) without a rows hint.
 // The lengths are on the device only: the count split gave a whole fragment to one workgroup (16 x 16 MiB
 // 2.3 ms, 1.5% of the roofline; one 64 MiB fragment 3 ms).  Every fragment runs as W row groups instead
@@ -4930,7 +5042,20 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     // read-only: two fragments per wave only for 1-2 KiB fragments ending off the 16-byte grid (IB's 1,976 B), where
     // the piece streams take their five-load variant (profiles/r05/crc_ro_pairs_ab.txt)
     bool small = false;
-    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &pairs, &nhalf, 1u, nullptr, &whole, true, &small);
+    uint32_t contig = 0;
+    rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &pairs, &nhalf, 1u, nullptr, &whole, true, &small,
+                                  nullptr, &contig);
+    // one contiguous run of equal 64 B .. 2 KiB fragments (a message as descriptors): packed rows, the rest after it
+    static const bool packed_desc = [] {  // (A/B knob LAMPI_PACKED_DESC=0: off)
+        const char *e = LAMPI_AB_ENV("LAMPI_PACKED_DESC");
+        return !(e && e[0] == '0');
+    }();
+    if (packed_desc && contig >= 64 && contig <= kRowBytes / 2 && (contig & (contig - 1)) == 0) {
+        size_t done = 0;
+        const hipError_t e = launch_crc_desc_packed(d, n, out, img, s, contig, &done);
+        if (e != hipSuccess) return e;
+        if (done) return done >= n ? hipSuccess : launch_crc_desc(d + done, n - done, out + done, img, grid, s, false, 1u);
+    }
     static const bool ro_pairs = [] {  // (A/B knob LAMPI_CRC_RO_PAIRS=0: read-only IB-sized batches on the piece streams)
         const char *e = LAMPI_AB_ENV("LAMPI_CRC_RO_PAIRS");
         return !(e && e[0] == '0');
@@ -5093,7 +5218,6 @@ static hipError_t launch_regular(const uint8_t *base, size_t n, size_t frag_len,
 // 2 KiB) at a 16-byte-aligned base on config B's schedule, 64 / kSub fragments per 4 KiB row, two rows per
 // chain item (kV = 2).  Takes the first *done fragments -- whole pairs of rows -- and leaves the rest (fewer
 // than 128 / kSub plus the message's last, possibly short, fragment) to the caller.
-constexpr size_t kPackedMinRows = 256;  // smaller messages keep the other schedules (one launch)
 template <bool kSum, int kSub>
 static hipError_t launch_packed_k(const uint8_t *base, size_t nv, uint32_t partial, uint32_t *out, const uint32_t *img,
                                   hipStream_t s) {

@@ -410,3 +410,67 @@ def test_small_fragment_messages_ragged(cuda, oracle, mode, frag_len):
     lens = np.minimum(frag_len, msg_len + 5 - offs).astype(np.uint32)
     want = oracle.desc_batch(host, offs, lens, np.full(n, 0x1234567, np.uint32) if mode == 0 else None, mode)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("L", [64, 256, 1024, 2048])
+def test_learned_contiguous_descriptors_packed(cuda, oracle, L):
+    """Round 6: read-only CRC descriptor batches the census saw as one contiguous run of equal L-byte fragments run
+    as packed rows (crc_regular_kernel<kSub> from d[0].addr, each wave checking its items' descriptors).  The same
+    array then holds, under the stale shape: a few descriptors moved elsewhere (odd addresses), with another length
+    or another register; a batch that is not contiguous at all; a batch at another start; a shorter batch -- every
+    call vs the oracle (items holding any of those go to the leftover launch; nothing outside the fragments is read)."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(800 + L)
+    n = max(300 * 4096 // L, 600) + 37  # whole 8 KiB items plus a tail
+    size = n * L + (8 << 20)
+    base = torch.empty(size, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=801)
+    host = base.cpu().numpy()
+    part = np.full(n, 0xFFFFFFFF, np.uint64)
+    run = (np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, np.uint64), part)
+    moved = [a.copy() for a in run]
+    pick = rng.choice(n, size=n // 200 + 3, replace=False)
+    moved[0][pick[0::3]] = (rng.integers(0, size - 2 * L, size=pick[0::3].size) | 1).astype(np.uint64)
+    moved[1][pick[1::3]] = rng.choice(np.array([0, 1, L - 1, L + 1, 3000], np.uint64), size=pick[1::3].size)
+    moved[2][pick[2::3]] = rng.integers(0, 2**32, size=pick[2::3].size, dtype=np.uint64)
+    scattered = (rng.integers(0, (size - L) // 16, size=n).astype(np.uint64) * np.uint64(16),
+                 np.full(n, L, np.uint64), part)
+    shifted = (run[0] + np.uint64(4096), run[1], part)
+    cases = {"run": run, "moved": moved, "scattered": scattered, "shifted": shifted}
+    prepared = {}
+    for k, (o, ln, pt) in cases.items():
+        prepared[k] = (dv.make_descs(base, o, ln, pt),
+                       oracle.desc_batch(host, o, ln.astype(np.uint32), pt.astype(np.uint32), 0))
+    descs = prepared["run"][0].clone()
+    stream = torch.cuda.Stream(device=cuda)
+    seq = ["run"] * 20 + ["moved"] * 3 + ["run"] * 2 + ["scattered"] * 2 + ["shifted"] * 2 + ["run"]
+    with torch.cuda.stream(stream):
+        for i, k in enumerate(seq):
+            descs.copy_(prepared[k][0])
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=0, stream=stream))
+            bad = np.nonzero(got != prepared[k][1])[0]
+            assert bad.size == 0, (i, k, bad[:8].tolist())
+        # a shorter batch on the same array (its first two thirds) under the learned shape
+        m = n - n // 3
+        got = dv.as_u32(dv.frag_csum_batch(descs, n=m, mode=0, stream=stream))
+        assert np.array_equal(got[:m], prepared["run"][1][:m])
+
+
+def test_config_a_shape_descriptors_digest(cuda):
+    """Config A's workload (1M x 1 KiB, stream seed 1) as one descriptor per fragment, after the census has seen
+    it (packed rows): BASELINE.md's digest feb61101 / 41fadf13."""
+    import torch
+
+    from oracle.oracle import digest
+
+    dv = _dv()
+    n, L = 1048576, 1024
+    buf = torch.empty(n * L, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(buf, seed=1)
+    descs = dv.make_descs(buf, np.arange(n, dtype=np.uint64) * np.uint64(L), np.full(n, L, np.uint64))
+    out = torch.empty(n, dtype=torch.int32, device=cuda)
+    for _ in range(3):
+        dv.frag_csum_batch(descs, out=out)
+        assert digest(dv.as_u32(out)) == (0xFEB61101, 0x41FADF13)
