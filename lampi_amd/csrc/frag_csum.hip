@@ -3262,8 +3262,8 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     // listed for crc_light_pair_leftover_kernel -- no address outside the batch's own fragments is read.
     uint64_t pbad = 0u;
     const uint8_t *pbase = base;
-    if constexpr (kSub < 64 && !kSum) {
-        if (dst != nullptr) {
+    if constexpr (kSub < 64) {
+        if (dst != nullptr) {  // (SUM: the register is ignored; the pairs go to sum_pair_leftover_kernel)
             const lampi_frag_desc *pd = reinterpret_cast<const lampi_frag_desc *>(dst);
             const uint64_t a0 = uniform64(pd[0].addr);
             const uint32_t p0 = uniform(pd[0].partial);
@@ -3287,7 +3287,7 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
 #pragma unroll
                     for (uint32_t h = 0; h < kPer; ++h) {
                         const uint64_t fi = (uint64_t)(f0 + kWv * min(j, nfr - 1u)) * F + min(lane + 64u * h, F - 1u);
-                        bad |= x[jj][h].addr != a0 + fi * L || x[jj][h].length != L || x[jj][h].partial != p0;
+                        bad |= x[jj][h].addr != a0 + fi * L || x[jj][h].length != L || (!kSum && x[jj][h].partial != p0);
                     }
                     if (j < nfr && __ballot(bad)) pbad |= 1ull << j;
                 }
@@ -3356,7 +3356,7 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
             const uint64_t ro = kV == 2 || !(nfr && !((bad >> j) & 1u)) ? 0u : (uint64_t)r * kRowBytes;
             return (gbyte *)(a + ro + lane_off);
         }
-        if constexpr (kSub < 64 && !kSum) {
+        if constexpr (kSub < 64) {
             if (pbad >> ((f - f0) / kWv) & 1u) return (gbyte *)((const uint8_t *)img + lane_off);
         }
         return (gbyte *)(pbase + ((uint64_t)(nfr ? f : 0u) * frag_len + (uint64_t)r * kRowBytes + lane_off));
@@ -3427,7 +3427,8 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
                 if ((lane & (kSub - 1)) == kSub - 1) {
 #pragma unroll
                     for (int c = 0; c < K; ++c)
-                        if (K * t.i + c < nfr) out[(frag(t.i, c) * kV + t.r) * (64u / kSub) + lane / kSub] = x[c];
+                        if (K * t.i + c < nfr && !((pbad >> (K * t.i + c)) & 1u))
+                            out[(frag(t.i, c) * kV + t.r) * (64u / kSub) + lane / kSub] = x[c];
                 }
                 return;
             }
@@ -3652,6 +3653,25 @@ __global__ void __launch_bounds__(256) sum_copy_waves_kernel(Src src, size_t n, 
         const uint32_t acc = wave_add(sum_copy_frag<64, Src>(fi, lane));
         if (lane == 0) emit(src, out, f, acc, fi);
     }
+}
+
+// The leftovers of SUM packed rows over descriptors (launch_sum_desc_packed): entry e of the list = fragments 2 list[e]
+// and 2 list[e] + 1, one wave per fragment through sum_copy_frag (any length, any alignment); the entry count is the
+// pair kernel's counter, the next call's zeroed here (as crc_light_pair_leftover_kernel).
+__global__ void __launch_bounds__(256) sum_pair_leftover_kernel(const lampi_frag_desc *__restrict__ d, size_t n,
+                                                                uint32_t *__restrict__ out, const uint32_t *left,
+                                                                uint32_t *next_left, const uint32_t *__restrict__ list) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (size_t e = (size_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); e < 2 * (size_t)c;
+         e += (size_t)gridDim.x * 4) {
+        const size_t f = 2 * (size_t)list[e >> 1] + (e & 1u);
+        if (f >= n) continue;
+        const FragInfo fi = DescSource{d}.get(f);
+        const uint32_t acc = wave_add(sum_copy_frag<64, DescSource>(fi, lane));
+        if (lane == 0) out[f] = acc;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *next_left = 0u;
 }
 
 // SUM row groups: out[f] = the sum of fragment f's W group sums, then emit (receive sources: the verdict).
@@ -4962,17 +4982,18 @@ static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint
 // whole 8 KiB items from d[0].addr, each wave checking its items' descriptors first; items holding anything else are
 // listed by fragment pairs for crc_light_pair_leftover_kernel; the last fragments (past the whole items) on the
 // count split.
-template <int kSub>
+template <bool kSum, int kSub>
 static hipError_t launch_packed_desc_k(const lampi_frag_desc *d, size_t nv, uint32_t *out, const uint32_t *img,
                                        hipStream_t s, uint32_t *list, uint32_t *left) {
     const uint32_t fpw = pick_regular_fpw(nv, 2 * kRowBytes);
-    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 2, false, kWaves, 0, false, kSub>),
+    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 2, kSum, kWaves, 0, false, kSub>),
                        grid_for(nv, fpw), dim3(kBlock), 0, s, (const uint8_t *)nullptr, (uint32_t)nv, fpw,
                        2 * kRowBytes, 0u, img, out, (uint8_t *)const_cast<lampi_frag_desc *>(d), (size_t)0, list, left);
     return hipGetLastError();
 }
-static hipError_t launch_crc_desc_packed(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
-                                         hipStream_t s, uint32_t L, size_t *done) {
+template <bool kSum>
+static hipError_t launch_desc_packed(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
+                                     hipStream_t s, uint32_t L, size_t *done) {
     *done = 0;
     const size_t F = 2 * kRowBytes / L, nv = n / F;
     if (nv * 2 < kPackedMinRows || nv > 0xFFFFFFFFull || nv * F / 2 > 0xFFFFFFFFull) return hipSuccess;
@@ -4983,17 +5004,21 @@ static hipError_t launch_crc_desc_packed(const lampi_frag_desc *d, size_t n, uin
     e = pair_counters(s, &left, &next_left);
     if (e != hipSuccess) return scratch_done(s, list, pooled, e);
     switch (L) {
-        case 64: e = launch_packed_desc_k<1>(d, nv, out, img, s, list, left); break;
-        case 128: e = launch_packed_desc_k<2>(d, nv, out, img, s, list, left); break;
-        case 256: e = launch_packed_desc_k<4>(d, nv, out, img, s, list, left); break;
-        case 512: e = launch_packed_desc_k<8>(d, nv, out, img, s, list, left); break;
-        case 1024: e = launch_packed_desc_k<16>(d, nv, out, img, s, list, left); break;
-        default: e = launch_packed_desc_k<32>(d, nv, out, img, s, list, left); break;
+        case 64: e = launch_packed_desc_k<kSum, 1>(d, nv, out, img, s, list, left); break;
+        case 128: e = launch_packed_desc_k<kSum, 2>(d, nv, out, img, s, list, left); break;
+        case 256: e = launch_packed_desc_k<kSum, 4>(d, nv, out, img, s, list, left); break;
+        case 512: e = launch_packed_desc_k<kSum, 8>(d, nv, out, img, s, list, left); break;
+        case 1024: e = launch_packed_desc_k<kSum, 16>(d, nv, out, img, s, list, left); break;
+        default: e = launch_packed_desc_k<kSum, 32>(d, nv, out, img, s, list, left); break;
     }
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(crc_light_pair_leftover_kernel<DescSource>, dim3(kLeftoverWgs), dim3(256), 0, s,
-                           DescSource{d}, nv * F, img, out, (const uint32_t *)left, next_left, (const uint32_t *)list,
-                           (uint32_t *)nullptr);
+        if constexpr (kSum)
+            hipLaunchKernelGGL(sum_pair_leftover_kernel, dim3(kLeftoverWgs), dim3(256), 0, s, d, nv * F, out,
+                               (const uint32_t *)left, next_left, (const uint32_t *)list);
+        else
+            hipLaunchKernelGGL(crc_light_pair_leftover_kernel<DescSource>, dim3(kLeftoverWgs), dim3(256), 0, s,
+                               DescSource{d}, nv * F, img, out, (const uint32_t *)left, next_left,
+                               (const uint32_t *)list, (uint32_t *)nullptr);
         e = hipGetLastError();
     }
     if (e != hipSuccess) reset_pair_counters(s);
@@ -5052,7 +5077,7 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     }();
     if (packed_desc && contig >= 64 && contig <= kRowBytes / 2 && (contig & (contig - 1)) == 0) {
         size_t done = 0;
-        const hipError_t e = launch_crc_desc_packed(d, n, out, img, s, contig, &done);
+        const hipError_t e = launch_desc_packed<false>(d, n, out, img, s, contig, &done);
         if (e != hipSuccess) return e;
         if (done) return done >= n ? hipSuccess : launch_crc_desc(d + done, n - done, out + done, img, grid, s, false, 1u);
     }
@@ -5474,9 +5499,22 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     bool half = false;  // (every sampled fragment at most 2 KiB)
     uint32_t *nh = nullptr;
     bool tiny = false;  // (every sampled fragment at most 1 KiB)
+    uint32_t contig = 0;  // (one contiguous run of equal fragments: their length)
     if (img)
         rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &half, &nh, 2u, &one_row, nullptr, false,
-                                      nullptr, &tiny);
+                                      nullptr, &tiny, &contig);
+    // one contiguous run of equal 64 B .. 1 KiB fragments: packed rows, as launch_crc_desc (2 KiB: one per wave reads
+    // faster, as for messages)
+    static const bool packed_desc = [] {  // (A/B knob LAMPI_PACKED_DESC=0: off, as launch_crc_desc)
+        const char *e = LAMPI_AB_ENV("LAMPI_PACKED_DESC");
+        return !(e && e[0] == '0');
+    }();
+    if (img && packed_desc && rows_hint <= 1 && contig >= 64 && contig <= 1024 && (contig & (contig - 1)) == 0) {
+        size_t done = 0;
+        const hipError_t e = launch_desc_packed<true>(d, n, out, img, s, contig, &done);
+        if (e != hipSuccess) return e;
+        if (done) return done >= n ? hipSuccess : launch_sum_desc(d + done, n - done, out + done, img, grid, s, false, 1u);
+    }
     static const bool sum_tiny = [] {  // (A/B knob LAMPI_SUM_TINY=0, as launch_sum_msg)
         const char *e = LAMPI_AB_ENV("LAMPI_SUM_TINY");
         return !(e && e[0] == '0');

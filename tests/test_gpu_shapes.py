@@ -412,10 +412,12 @@ def test_small_fragment_messages_ragged(cuda, oracle, mode, frag_len):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
 @pytest.mark.parametrize("L", [64, 256, 1024, 2048])
-def test_learned_contiguous_descriptors_packed(cuda, oracle, L):
-    """Round 6: read-only CRC descriptor batches the census saw as one contiguous run of equal L-byte fragments run
-    as packed rows (crc_regular_kernel<kSub> from d[0].addr, each wave checking its items' descriptors).  The same
+def test_learned_contiguous_descriptors_packed(cuda, oracle, L, mode):
+    """Round 6: read-only descriptor batches the census saw as one contiguous run of equal L-byte fragments run as
+    packed rows (crc_regular_kernel<kSub> from d[0].addr, each wave checking its items' descriptors; CRC up to 2 KiB,
+    SUM up to 1 KiB, the leftovers on crc_light_pair_leftover_kernel / sum_pair_leftover_kernel).  The same
     array then holds, under the stale shape: a few descriptors moved elsewhere (odd addresses), with another length
     or another register; a batch that is not contiguous at all; a batch at another start; a shorter batch -- every
     call vs the oracle (items holding any of those go to the leftover launch; nothing outside the fragments is read)."""
@@ -442,19 +444,20 @@ def test_learned_contiguous_descriptors_packed(cuda, oracle, L):
     prepared = {}
     for k, (o, ln, pt) in cases.items():
         prepared[k] = (dv.make_descs(base, o, ln, pt),
-                       oracle.desc_batch(host, o, ln.astype(np.uint32), pt.astype(np.uint32), 0))
+                       oracle.desc_batch(host, o, ln.astype(np.uint32), pt.astype(np.uint32) if mode == 0 else None,
+                                         mode))
     descs = prepared["run"][0].clone()
     stream = torch.cuda.Stream(device=cuda)
     seq = ["run"] * 20 + ["moved"] * 3 + ["run"] * 2 + ["scattered"] * 2 + ["shifted"] * 2 + ["run"]
     with torch.cuda.stream(stream):
         for i, k in enumerate(seq):
             descs.copy_(prepared[k][0])
-            got = dv.as_u32(dv.frag_csum_batch(descs, mode=0, stream=stream))
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=mode, stream=stream))
             bad = np.nonzero(got != prepared[k][1])[0]
             assert bad.size == 0, (i, k, bad[:8].tolist())
         # a shorter batch on the same array (its first two thirds) under the learned shape
         m = n - n // 3
-        got = dv.as_u32(dv.frag_csum_batch(descs, n=m, mode=0, stream=stream))
+        got = dv.as_u32(dv.frag_csum_batch(descs, n=m, mode=mode, stream=stream))
         assert np.array_equal(got[:m], prepared["run"][1][:m])
 
 
