@@ -293,7 +293,9 @@ typedef struct lampi_frag_desc {
 } lampi_frag_desc;
 
 /* out[i] = checksum of fragment d[i] (CRC register or SUM value, as uicrc/uicsum
- * would return for the same bytes).  The schedule follows the batch: by
+ * would return for the same bytes).  The schedule follows the batch: a batch the
+ * library has seen to be one contiguous run of equal 64 B .. 2 KiB fragments (a message handed over as
+ * descriptors) runs as that message's packed rows, every descriptor still checked; otherwise, by
  * default the piece streams -- each workgroup's fragments cut into 64-byte pieces packed into full
  * 4 KiB rows, so mixed sizes keep every lane busy; with LAMPI_CSUM_ROWS_HINT (or the shape the
  * stream's earlier batches showed) long fragments one wavefront each on the table-light kernel (CRC)
@@ -391,7 +393,9 @@ int lampi_msg_bcopy_strided(const void *d_msg, size_t msg_len, size_t frag_len, 
 /* Fragments a contiguous device-resident message the way the path layer does
  * (fragment k = bytes [k*frag_len, min((k+1)*frag_len, msg_len)),
  * src/path/gm/path.cc:98-121) and writes ceil(msg_len/frag_len) checksums to d_out.
- * Every fragment starts from `partial` (CRC mode) or a fresh state (SUM mode). */
+ * Every fragment starts from `partial` (CRC mode) or a fresh state (SUM mode).  Fragments of 64 B .. 2 KiB
+ * (powers of two) in messages of at least 1 MiB from a 16-byte-aligned base are checksummed 64 / (frag_len / 64)
+ * to a 4 KiB row of the uniform-batch kernel. */
 int lampi_msg_csum(const void *d_msg, size_t msg_len, size_t frag_len, uint32_t partial,
                    uint32_t *d_out, int mode, void *stream);
 
