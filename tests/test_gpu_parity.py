@@ -664,6 +664,45 @@ def test_descriptor_batch_small_fragments(cuda, oracle, n):
             assert bad.size == 0, [(mode, by_bytes, int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["crc", "sum"])
+@pytest.mark.parametrize("L", [64, 128, 256, 512, 1024, 1976])
+def test_small_fragment_sizes_mixed_with_large(cuda, oracle, L, mode):
+    """fragments of exactly L bytes (64 .. 1,024, IB's 1,976) as messages, as contiguous descriptor
+    runs (after the census has seen them) and mixed 9:1 with large fragments (4 KiB .. 300 KB) at aligned and odd
+    addresses in one descriptor batch, every fragment against the oracle; random registers."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(L * 3 + mode)
+    n = 1 << 20 if L <= 256 else 300 * 4096 // L * 2
+    base = torch.empty(n * L + (48 << 20), dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=L + 31)
+    host = base.cpu().numpy()
+    part = int(rng.integers(0, 2**32))
+    # the message and its contiguous descriptor run
+    got = dv.as_u32(dv.msg_csum(base[:n * L], L, partial=part, mode=mode))
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    lens = np.full(n, L, np.uint32)
+    want = oracle.desc_batch(host, offs, lens, np.full(n, part, np.uint32) if mode == 0 else None, mode)
+    assert np.array_equal(got, want)
+    descs = dv.make_descs(base, offs, lens, np.full(n, part, np.uint64))
+    stream = torch.cuda.Stream(device=cuda)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            assert np.array_equal(dv.as_u32(dv.frag_csum_batch(descs, mode=mode, stream=stream)), want)
+    # mixed with large fragments, aligned and odd addresses
+    m = 60000
+    big = rng.random(m) < 0.1
+    mlens = np.where(big, rng.integers(4096, 300000, size=m), L).astype(np.uint64)
+    moffs = rng.integers(0, base.numel() - 300001, size=m).astype(np.uint64)
+    moffs[~big & (rng.random(m) < 0.7)] &= ~np.uint64(15)
+    parts = rng.integers(0, 2**32, size=m, dtype=np.uint64)
+    mdescs = dv.make_descs(base, moffs, mlens, parts)
+    mwant = oracle.desc_batch(host, moffs, mlens.astype(np.uint32), parts.astype(np.uint32) if mode == 0 else None,
+                              mode)
+    assert np.array_equal(dv.as_u32(dv.frag_csum_batch(mdescs, mode=mode)), mwant)
+
+
 def test_kat_check_values(cuda):
     import torch
 
