@@ -664,12 +664,14 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // Issues the combine basis, lets `pre` issue kPre more asm loads (the first rows of the
 // workgroup), builds the constant tables, waits for the basis only (vmcnt(kPre)), builds the
 // combine tables and ends with an LDS-only barrier.
-template <int kPre, class Pre, int kParts = 7, bool kCoal = false, bool kSync = true>
+// kLatePre: `pre` runs after the slicing tables are built (the rows' addresses wait for loads issued before).
+template <int kPre, class Pre, int kParts = 7, bool kCoal = false, bool kSync = true, bool kLatePre = false>
 __device__ __forceinline__ void stage_tables(uint32_t *lds, const uint32_t *__restrict__ img, Pre pre) {
     CombineBasis cb = issue_combine_basis<kCoal>(img);
-    pre();
+    if (!kLatePre) pre();
     char *b = reinterpret_cast<char *>(lds);
     if (kParts & 1) build_slices(b);
+    if (kLatePre) pre();
     if (kParts & 4) build_horner<kCoal>(b);
     asm volatile("s_waitcnt vmcnt(%2) ; lampi-wait %0 %1" : "+v"(cb.a), "+v"(cb.b) : "n"(kPre) : "memory");
     if (kParts & 2) build_combine(b, cb);
@@ -3303,19 +3305,28 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
         }
     }
     // kDesc: lane kV j + r holds fragment kV (f0 + kWv j) + r's descriptor; bad bit j: item j is listed
+    // The descriptors are loaded here and checked (desc_check) after the slicing tables are built, so their
+    // latency hides behind that build instead of delaying the workgroup's first rows.
     uint32_t da_lo = 0u, da_hi = 0u, dpart = 0u;
     uint64_t bad = 0u;
+    lampi_frag_desc dx{};
     if constexpr (kDesc) {
-        const lampi_frag_desc *descs = reinterpret_cast<const lampi_frag_desc *>(base);
+        if (nfr) {  // every lane loads (clamped to the wave's last item)
+            const lampi_frag_desc *descs = reinterpret_cast<const lampi_frag_desc *>(base);
+            const uint32_t j = min((uint32_t)lane / kV, nfr - 1u);
+            dx = descs[(size_t)(f0 + kWv * j) * kV + (kV == 2 ? (lane & 1) : 0)];
+        }
+    }
+    auto desc_check = [&] {
+      if constexpr (kDesc) {
         const uint32_t j = (uint32_t)lane / kV;
         const bool mine = j < nfr;
         uint32_t len = 0u;
         if (mine) {
-            const lampi_frag_desc x = descs[(size_t)(f0 + kWv * j) * kV + (kV == 2 ? (lane & 1) : 0)];
-            da_lo = (uint32_t)x.addr;
-            da_hi = (uint32_t)(x.addr >> 32);
-            len = x.length;
-            dpart = x.partial;
+            da_lo = (uint32_t)dx.addr;
+            da_hi = (uint32_t)(dx.addr >> 32);
+            len = dx.length;
+            dpart = dx.partial;
         }
         const bool odd = mine && (len != (uint32_t)(frag_len / kV) || (da_lo & 15u) != 0u);
         const uint64_t lanes = __ballot(odd);
@@ -3331,7 +3342,8 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
                 list[atomicAdd(left, 1u)] = kV == 2 ? f : f >> 1;
             }
         }
-    }
+      }
+    };
 
     auto advance = [&](GroupTask t) -> GroupTask {
         if (t.r + 1 < R) return {t.i, t.r + 1};
@@ -3384,8 +3396,17 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
         asm volatile("" ::"v"(lds) : "memory");  // the LDS array escapes: it stays allocated
     } else if (kWv == kWaves) {
         // every ring slot is in flight while the workgroup builds its tables
-        stage_tables<4 * K * D, decltype(issue_all), 7, kCoal>(lds, img, issue_all);
+        if constexpr (kDesc) {
+            auto checked_issue = [&] {
+                desc_check();
+                issue_all();
+            };
+            stage_tables<4 * K * D, decltype(checked_issue), 7, kCoal, true, true>(lds, img, checked_issue);
+        } else {
+            stage_tables<4 * K * D, decltype(issue_all), 7, kCoal>(lds, img, issue_all);
+        }
     } else {
+        desc_check();
         if (threadIdx.x < 64 * kWaves)
             stage_tables<4 * K * D, decltype(issue_all), 7, kCoal, false>(lds, img, issue_all);
         else
