@@ -477,3 +477,75 @@ def test_config_a_shape_descriptors_digest(cuda):
     for _ in range(3):
         dv.frag_csum_batch(descs, out=out)
         assert digest(dv.as_u32(out)) == (0xFEB61101, 0x41FADF13)
+
+
+def _ragged_layout(rng, lens, align=64):
+    """Offsets of fragments laid one after another, each start rounded up to `align` (plus a random 0-2 blocks of gap)."""
+    offs = np.empty(lens.size, np.uint64)
+    o = 0
+    for i, ln in enumerate(lens.tolist()):
+        o = (o + align - 1) // align * align + align * int(rng.integers(0, 3))
+        offs[i] = o
+        o += ln
+    return offs, o
+
+
+@pytest.mark.parametrize("case", ["zipf", "bytes"])
+def test_learned_ragged_descriptors(cuda, oracle, case):
+    """Round 6: read-only CRC descriptor batches of mixed lengths up to 16 rows at 64-byte-aligned
+    addresses run on crc_ragged_kernel once the census has seen the shape -- per-fragment row counts, the last row
+    masked to its npc pieces and h bytes, the register shifted back by 64 - h bytes.  `zipf`: config C's lengths (64-byte
+    multiples); `bytes`: any length 1 .. 65,536 (the ragged 1-7-row lengths 4,097 .. 28,671 among them) with random
+    registers.  Then, on the same array under the learned shape: some descriptors moved off the 64-byte grid (odd and
+    16-byte-aligned addresses), emptied or lengthened past 16 rows (listed for the leftover launch); the same lengths at
+    odd addresses (1-byte alignment; another schedule); a shorter batch -- every call vs the oracle."""
+    import torch
+
+    from lampi_amd.workload import zipf_lengths
+
+    dv = _dv()
+    rng = np.random.default_rng(9100 + len(case))
+    if case == "zipf":
+        lens = zipf_lengths(48 << 20).astype(np.uint64)
+    else:
+        n0 = 9000
+        lens = np.concatenate([
+            rng.integers(4097, 28672, size=n0 // 3),           # 2-7 rows, any length
+            rng.integers(1, 4097, size=n0 // 3),                # one row
+            rng.integers(28672, 65537, size=n0 // 6),           # 8-16 rows
+            np.array([1, 2, 3, 4, 5, 63, 64, 65, 127, 128, 4095, 4096, 4097, 4159, 4160, 8191, 8192, 28671,
+                      65535, 65536] * 20)]).astype(np.uint64)
+        lens = lens[rng.permutation(lens.size)]
+    n = lens.size
+    offs, total = _ragged_layout(rng, lens)
+    size = total + (1 << 20)
+    base = torch.empty(size, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(base, seed=9101)
+    host = base.cpu().numpy()
+    part = (np.full(n, 0xFFFFFFFF, np.uint64) if case == "zipf"
+            else rng.integers(0, 2**32, size=n, dtype=np.uint64))
+    moved = [offs.copy(), lens.copy(), part]
+    pick = rng.choice(n, size=n // 100 + 4, replace=False)
+    moved[0][pick[0::4]] = (rng.integers(0, size - 70000, size=pick[0::4].size) | 1).astype(np.uint64)
+    moved[0][pick[1::4]] = (rng.integers(0, (size - 70000) // 64, size=pick[1::4].size) * 64 + 16).astype(np.uint64)
+    moved[1][pick[2::4]] = 0
+    moved[0][pick[3::4]] = 0
+    moved[1][pick[3::4]] = rng.integers(65537, 70001, size=pick[3::4].size).astype(np.uint64)
+    odd = (np.minimum(offs + np.uint64(1), np.uint64(size) - lens), lens, part)
+    cases = {"run": (offs, lens, part), "moved": tuple(moved), "odd": odd}
+    prepared = {}
+    for k, (o, ln, pt) in cases.items():
+        prepared[k] = (dv.make_descs(base, o, ln, pt),
+                       oracle.desc_batch(host, o, ln.astype(np.uint32), pt.astype(np.uint32), 0))
+    descs = prepared["run"][0].clone()
+    stream = torch.cuda.Stream(device=cuda)
+    seq = ["run"] * 20 + ["moved"] * 3 + ["run"] * 2 + ["odd"] * 2 + ["run"]
+    with torch.cuda.stream(stream):
+        for i, k in enumerate(seq):
+            descs.copy_(prepared[k][0])
+            got = dv.as_u32(dv.frag_csum_batch(descs, mode=dv.CRC32, stream=stream))
+            bad = np.nonzero(got != prepared[k][1])[0]
+            assert bad.size == 0, (case, i, k, bad[:8].tolist(), lens[bad[:8]].tolist())
+        m = n - n // 3
+        got = dv.as_u32(dv.frag_csum_batch(descs, n=m, mode=dv.CRC32, stream=stream))
+        assert np.array_equal(got[:m], prepared["run"][1][:m])
