@@ -3547,222 +3547,6 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped re-loads before exit
 }
 
-// ---- CRC: ragged whole-row descriptor batches (round 6) ---------------------------------------
-// Read-only CRC of descriptor batches of mixed lengths (config C's Zipf sizes) on config B's row
-// machinery.  A fragment of len bytes at a 64-byte-aligned address (1 .. kRaggedMaxRows rows) is R = ceil(len / 4096)
-// rows from its start; the last row holds e = len - 4096 (R - 1) bytes: npc = ceil(e / 64) pieces, the last of them
-// h = e - 64 (npc - 1) bytes.  Lane l reads the piece at 64 l of every row, as in config B, so the per-lane Horner step
-// (4032 bytes) and the per-lane state carry over unchanged; only the last row differs:
-//   - lanes l >= npc read a zero row and keep the state they had before it (their last piece is the row before);
-//   - lane npc - 1 reads its whole 64-byte block (the address is 64-byte aligned, so the block never leaves the page
-//     of its first byte) and zeroes bytes h .. 63;
-//   - lane l's state moves to the padded end (4096 (R - 1) + 64 npc) through the combine column (l + 64 - npc) mod 64,
-//     a shift of 64 ((npc - 1 - l) mod 64) bytes -- lanes >= npc pass their last piece's row end on the way;
-//   - the XOR of the lanes is the register after h - 64 extra zero bytes: h < 64 shifts it back by 64 - h bytes
-//     (x^-8z, z = 64 - h: lane b < 32 takes bit b's column x^(b - 8z) mod P from a 536-word LDS table, one XOR).
-// Each of a wave's K chains walks its own fragment row by row and takes the wave's next fragment when it is done (a
-// wave-uniform counter), so the chains stay within one fragment of each other; an idle chain reads the zero row (the
-// ring's load counts stay fixed).  A fragment of another shape (empty, longer, or off the 64-byte grid) is skipped and
-// listed (f / 2) for crc_light_pair_leftover_kernel, as in crc_regular_kernel<kDesc>.
-constexpr uint32_t kRaggedMaxRows = 16;
-constexpr uint32_t kUnshiftMax = 63;                     // bytes shifted back at most
-constexpr uint32_t kUnshiftWords = 8 * kUnshiftMax + 32;  // x^j mod P, j = -504 .. 31
-constexpr uint32_t kLdsUnshift = kLdsBytes;              // its place in the ragged kernel's LDS
-struct UnshiftTable {
-    uint32_t v[kUnshiftWords];
-};
-// v[j + 504] = x^j mod P (normal domain, register bit b <-> x^b); x^-1 = (P - 1) / x = 0x82608EDB
-constexpr UnshiftTable make_unshift() {
-    UnshiftTable t{};
-    for (uint32_t j = 0; j < 32; ++j) t.v[8 * kUnshiftMax + j] = 1u << j;
-    uint32_t x = 1u;
-    for (uint32_t m = 1; m <= 8 * kUnshiftMax; ++m) {
-        x = (x & 1u) ? (x >> 1) ^ 0x82608EDBu : (x >> 1);
-        t.v[8 * kUnshiftMax - m] = x;
-    }
-    return t;
-}
-__constant__ UnshiftTable g_unshift = make_unshift();
-__device__ __attribute__((aligned(256))) uint8_t g_zero_row[kRowBytes];  // (zero-initialised; never written)
-
-struct RagTask {
-    uint32_t j[2], r[2];  // chain c: the wave's fragment j (kRagIdle: none) and its row r
-};
-constexpr uint32_t kRagIdle = 0xFFFFFFFFu;
-
-template <int D = 3>
-__global__ void __launch_bounds__(kBlock) crc_ragged_kernel(const lampi_frag_desc *__restrict__ d, uint32_t n, uint32_t fpw,
-                                                            const uint32_t *__restrict__ img, uint32_t *__restrict__ out,
-                                                            uint32_t *__restrict__ list, uint32_t *left) {
-    constexpr int K = 2;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLdsBytes + 4 * kUnshiftWords) / 4];
-    const int lane = threadIdx.x & 63;
-    const uint32_t f0 = uniform(blockIdx.x * kWaves * fpw + (threadIdx.x >> 6));
-    const uint32_t nfr = f0 < n ? min(fpw, (n - f0 + kWaves - 1) / kWaves) : 0u;  // fragments f0 + kWaves j, j < nfr
-    const uint32_t lane_off = (uint32_t)lane * kLaneBytes;
-    // lane j: fragment f0 + kWaves j's descriptor; the unshift table's words t, t + 256, t + 512 -- both loaded now,
-    // used once the slicing tables are built
-    lampi_frag_desc dx{};
-    if (nfr) dx = d[f0 + (size_t)kWaves * min((uint32_t)lane, nfr - 1u)];
-    const uint32_t t = threadIdx.x;
-    const uint32_t u0 = g_unshift.v[t], u1 = g_unshift.v[t + 256u], u2 = g_unshift.v[min(t + 512u, kUnshiftWords - 1u)];
-    uint32_t da_lo = 0u, da_hi = 0u, dlen = 0u, dpart = 0u, nextj = 0u;
-    uint64_t bad = 0u;
-    auto desc_check = [&] {
-        uint32_t *ul = lds + kLdsUnshift / 4;
-        ul[t] = u0;
-        ul[t + 256u] = u1;
-        if (t + 512u < kUnshiftWords) ul[t + 512u] = u2;
-        const bool mine = (uint32_t)lane < nfr;
-        da_lo = (uint32_t)dx.addr;
-        da_hi = (uint32_t)(dx.addr >> 32);
-        dlen = dx.length;
-        dpart = dx.partial;
-        const bool ok = dlen != 0u && dlen <= kRaggedMaxRows * (uint32_t)kRowBytes && (da_lo & 63u) == 0u;
-        bad = uniform64(__ballot(mine && !ok));
-        if (bad && lane == 0) {
-            for (uint64_t m = bad; m; m &= m - 1) list[atomicAdd(left, 1u)] = (f0 + kWaves * (uint32_t)__builtin_ctzll(m)) >> 1;
-        }
-    };
-    auto len_of = [&](uint32_t j) -> uint32_t { return uniform((uint32_t)__builtin_amdgcn_readlane(dlen, j)); };
-    auto rows_of = [&](uint32_t j) -> uint32_t { return (len_of(j) + kRowBytes - 1u) / kRowBytes; };
-    auto next_frag = [&]() -> uint32_t {
-        uint32_t j = nextj;
-        while (j < nfr && ((bad >> j) & 1u)) ++j;
-        nextj = j < nfr ? j + 1u : nfr;
-        return j < nfr ? j : kRagIdle;
-    };
-    auto advance = [&](const RagTask &p) -> RagTask {
-        RagTask q;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            if (p.j[c] != kRagIdle && p.r[c] + 1u < rows_of(p.j[c])) {
-                q.j[c] = p.j[c];
-                q.r[c] = p.r[c] + 1u;
-            } else {
-                q.j[c] = next_frag();
-                q.r[c] = 0u;
-            }
-        }
-        return q;
-    };
-    auto all_idle = [](const RagTask &p) -> bool { return p.j[0] == kRagIdle && p.j[1] == kRagIdle; };
-    gbyte *const zero = (gbyte *)(g_zero_row + lane_off);
-    auto issue = [&](const RagTask &p, RowsK<K> &b) {
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            gbyte *q = zero;
-            if (p.j[c] != kRagIdle) {
-                const uint32_t j = p.j[c];
-                const uint64_t a = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(da_hi, j) << 32) |
-                                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane(da_lo, j);
-                const uint32_t len = len_of(j), R = (len + kRowBytes - 1u) / kRowBytes;
-                const uint32_t npc = p.r[c] + 1u == R ? (len - (R - 1u) * kRowBytes + kLaneBytes - 1u) / kLaneBytes : 64u;
-                if ((uint32_t)lane < npc) q = (gbyte *)(uniform64(a + (uint64_t)p.r[c] * kRowBytes) + lane_off);
-            }
-            issue_row<16>(q, b.x[c]);
-        }
-    };
-
-    RagTask tk[D];
-    RowsK<K> ring[D];
-    auto issue_all = [&] {
-        RagTask p;
-        p.j[0] = p.j[1] = kRagIdle;
-        p.r[0] = p.r[1] = 0u;
-#pragma unroll
-        for (int q = 0; q < D; ++q) {
-            tk[q] = advance(q == 0 ? p : tk[q - 1]);
-            issue(tk[q], ring[q]);
-        }
-    };
-    auto checked_issue = [&] {
-        desc_check();
-        issue_all();
-    };
-    stage_tables<4 * K * D, decltype(checked_issue), 7, false, true, true>(lds, img, checked_issue);
-    if (all_idle(tk[0])) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        return;
-    }
-    const CrcLane k = make_lane(lane);
-    uint32_t C[K] = {0u, 0u};
-    auto process = [&](RowsK<K> &b, const RagTask &p) {
-        uint32_t Cold[K], npc[K], h[K];
-        bool last[K];
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            npc[c] = 64u;
-            h[c] = 64u;
-            last[c] = false;
-            Cold[c] = C[c];
-            if (p.j[c] == kRagIdle) continue;
-            const uint32_t len = len_of(p.j[c]), R = (len + kRowBytes - 1u) / kRowBytes;
-            last[c] = p.r[c] + 1u == R;
-            if (last[c]) {
-                const uint32_t e = len - (R - 1u) * kRowBytes;
-                npc[c] = (e + kLaneBytes - 1u) / kLaneBytes;
-                h[c] = e - (npc[c] - 1u) * kLaneBytes;
-            }
-            if (p.r[c] == 0u) {  // the fragment's register enters at lane 0
-                const uint32_t v = __builtin_bswap32((uint32_t)__builtin_amdgcn_readlane(dpart, p.j[c]));
-                C[c] = lane == 0 ? v : 0u;
-                Cold[c] = C[c];
-            } else {
-                C[c] = horner_shift(lds, C[c]);
-            }
-            if (h[c] < 64u) {  // lane npc - 1: bytes h .. 63 of its block are past the end
-                const uint32_t lim = (uint32_t)lane == npc[c] - 1u ? h[c] : 64u;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    uint32_t w4[4] = {b.x[c].q[q].x, b.x[c].q[q].y, b.x[c].q[q].z, b.x[c].q[q].w};
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t o = 16u * q + 4u * i;
-                        const uint32_t keep = lim >= o + 4u ? 4u : (lim > o ? lim - o : 0u);
-                        w4[i] &= keep >= 4u ? 0xFFFFFFFFu : ((1u << (8u * keep)) - 1u);
-                    }
-                    b.x[c].q[q] = u32x4{w4[0], w4[1], w4[2], w4[3]};
-                }
-            }
-        }
-        crc_pieces<K>(lds, k, C, b);
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-            if (!last[c]) continue;
-            const uint32_t s = (uint32_t)lane < npc[c] ? C[c] : Cold[c];
-            CrcLane kr = k;
-            kr.comb_base = make_lane((int)(((uint32_t)lane + 64u - npc[c]) & 63u)).comb_base;
-            uint32_t v = __builtin_bswap32(wave_xor(lane_combine(lds, kr, s)));
-            if (h[c] < 64u) {  // shift back by z = 64 - h bytes: XOR over the set bits b of v of x^(b - 8z)
-                const uint32_t z = 64u - h[c], bl = (uint32_t)lane & 31u;
-                const uint32_t col = lds[kLdsUnshift / 4 + bl + 8u * (kUnshiftMax - z)];
-                v = wave_xor(lane < 32 && ((v >> bl) & 1u) ? col : 0u);
-            }
-            if (lane == 0) out[f0 + kWaves * p.j[c]] = v;
-        }
-    };
-    constexpr int kL = 4 * K;
-#define LAMPI_RAG_STEP(S)                                  \
-    if constexpr ((S) < D) {                               \
-        wait_rows<(D - 1) * kL, K>(ring[(S) % D]);         \
-        process(ring[(S) % D], tk[(S) % D]);               \
-        if (all_idle(tk[((S) + 1) % D])) break;            \
-        tk[(S) % D] = advance(tk[((S) + D - 1) % D]);      \
-        issue(tk[(S) % D], ring[(S) % D]);                 \
-    }
-    for (;;) {
-        LAMPI_RAG_STEP(0)
-        LAMPI_RAG_STEP(1)
-        LAMPI_RAG_STEP(2)
-        LAMPI_RAG_STEP(3)
-        LAMPI_RAG_STEP(4)
-        LAMPI_RAG_STEP(5)
-    }
-#undef LAMPI_RAG_STEP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-row loads issued past the last fragment
-}
-
 // ---- SUM -------------------------------------------------------------------------------
 // SUM fused copies (bcopy_uicsum descriptors, the receive step, ragged message fragments and the
 // rows of longer ones) in the textbook copy shape: one short-lived 128-thread workgroup per
@@ -4745,7 +4529,7 @@ struct BatchShape {
     uint32_t ncontig;  // how many lay where a contiguous run of equal fragments from fragment 0 puts them (fragment i
                        // at d[0].addr + i * d[0].length, the same length and register; d[0].addr 16-byte aligned)
     uint32_t len0;     // fragment 0's length
-    uint32_t nrag;     // how many were 1 .. kRaggedMaxRows rows at a 64-byte-aligned address (crc_ragged_kernel's shape)
+    uint32_t pad;
 };
 constexpr int kShapeSlots = 8;  // shape records per (thread, device, stream): descriptor arrays remembered
 constexpr int64_t kLeftBytes = 256;
@@ -4941,7 +4725,7 @@ template <class Src>
 __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, BatchShape *rec, uint32_t seq) {
     const uint32_t l = threadIdx.x;
     const uint32_t m = (uint32_t)min<size_t>(n, 64);
-    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u, full = 0u, mis = 0u, k12 = 0u, k1 = 0u, contig = 0u, rag = 0u;
+    uint32_t rmin = 0xFFFFFFFFu, rmax = 0u, half = 0u, full = 0u, mis = 0u, k12 = 0u, k1 = 0u, contig = 0u;
     const FragInfo f0i = src.get(0);  // (sample 0 is fragment 0: the run's start)
     if (l < m) {
         const size_t idx = (size_t)l * n / m;
@@ -4957,7 +4741,6 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         k12 = fi.len > 1024u && fi.len <= 2048u ? 1u : 0u;
         k1 = fi.len <= 1024u ? 1u : 0u;
         mis = k12 && (((uintptr_t)fi.addr + fi.len) & 15u) != 0 ? 1u : 0u;
-        rag = fi.len != 0u && R <= kRaggedMaxRows && ((uintptr_t)fi.addr & 63u) == 0 ? 1u : 0u;
     }
     for (int o = 32; o >= 1; o >>= 1) {
         rmin = min(rmin, (uint32_t)__shfl_xor((int)rmin, o));
@@ -4968,7 +4751,6 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         k12 += (uint32_t)__shfl_xor((int)k12, o);
         k1 += (uint32_t)__shfl_xor((int)k1, o);
         contig += (uint32_t)__shfl_xor((int)contig, o);
-        rag += (uint32_t)__shfl_xor((int)rag, o);
     }
     if (l == 0) {
         volatile BatchShape *r = rec;
@@ -4982,7 +4764,6 @@ __global__ void __launch_bounds__(64) census_kernel(const Src src, size_t n, Bat
         r->n1k = k1;
         r->ncontig = contig;
         r->len0 = f0i.len;
-        r->nrag = rag;
         __threadfence_system();
         r->seq = seq;
     }
@@ -5003,9 +4784,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
                                   bool *pairs = nullptr, uint32_t **nhalf_dev = nullptr,
                                   uint32_t min_rows = kShapeRows, bool *one_row = nullptr,
                                   bool *full_rows = nullptr, bool pairs_misaligned_only = false,
-                                  bool *all_half = nullptr, bool *all_1k = nullptr, uint32_t *contig_len = nullptr,
-                                  bool *ragged = nullptr) {
-    if (ragged) *ragged = false;
+                                  bool *all_half = nullptr, bool *all_1k = nullptr, uint32_t *contig_len = nullptr) {
     if (contig_len) *contig_len = 0u;
     if (all_half) *all_half = false;
     if (all_1k) *all_1k = false;
@@ -5057,8 +4836,7 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
     const uint32_t q0 = v->seq;
     std::atomic_thread_fence(std::memory_order_acquire);  // the fields are read after the first seq ...
     const uint32_t sampled = v->sampled, rmin = v->rmin, rmax = v->rmax, nhalf = v->nhalf, nwhole = v->nwhole,
-                   nmis = v->nmis, n12k = v->n12k, n1k = v->n1k, ncontig = v->ncontig, len0 = v->len0,
-                   nrag = v->nrag;
+                   nmis = v->nmis, n12k = v->n12k, n1k = v->n1k, ncontig = v->ncontig, len0 = v->len0;
     std::atomic_thread_fence(std::memory_order_acquire);  // ... and before the second (a seqlock read)
     if (q0 != 0 && v->seq == q0 && sampled > 0) {
         if (rmin >= min_rows && rmax <= 2 * rmin) W = rmax;
@@ -5073,9 +4851,6 @@ static uint32_t learned_rows_hint(const Src &src, size_t n, hipStream_t s, int k
         // every sampled fragment where one contiguous run of equal fragments puts it (packed rows; the pair counters
         // list the items that are not, so not on a stream whose counters are broken)
         if (contig_len && ncontig == sampled && !slot.pair_broken) *contig_len = len0;
-        // every sampled fragment in the ragged kernel's shape, some of more than one row (it lists the others through
-        // the pair counters)
-        if (ragged && nrag == sampled && rmax >= 2u && !slot.pair_broken) *ragged = true;
         if (pairs && nhalf == sampled && !slot.pair_broken &&
             (!pairs_misaligned_only || (n12k == sampled && 4 * nmis >= sampled))) {  // every sampled fragment at
             // most 2 KiB: two per wave (read-only: 1-2 KiB each, a quarter or more ending off the 16-byte grid)
@@ -5223,38 +4998,6 @@ static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint
     return e;
 }
 
-// Read-only CRC descriptor batches the census saw in the ragged kernel's shape (1 .. kRaggedMaxRows rows at 64-byte-aligned
-// addresses, some of more than one row; config C): crc_ragged_kernel, fpw fragments per wave; the fragments of any other
-// shape listed by the kernel and checksummed by crc_light_pair_leftover_kernel (the pair counters, as the whole-row path).
-constexpr uint32_t kRaggedFpw = 16;
-constexpr size_t kRaggedMin = 4096;  // fragments: smaller batches keep the other schedules
-static hipError_t launch_crc_desc_ragged(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
-                                         hipStream_t s) {
-    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    static const uint32_t fpw_env = [] {  // (A/B knob LAMPI_RAGGED_FPW: fragments per wave, 1 .. 64)
-        const char *e = LAMPI_AB_ENV("LAMPI_RAGGED_FPW");
-        return e ? (uint32_t)std::atoi(e) : 0u;
-    }();
-    const uint32_t fpw = fpw_env >= 1u && fpw_env <= 64u ? fpw_env : kRaggedFpw;
-    uint32_t *list = nullptr, *left = nullptr, *next_left = nullptr;
-    bool pooled = false;
-    hipError_t e = stream_scratch(s, (n + 1) * sizeof(uint32_t), (void **)&list, &pooled);
-    if (e != hipSuccess) return e;
-    e = pair_counters(s, &left, &next_left);
-    if (e != hipSuccess) return scratch_done(s, list, pooled, e);
-    hipLaunchKernelGGL(crc_ragged_kernel<3>, grid_for(n, fpw), dim3(kBlock), 0, s, d, (uint32_t)n, fpw, img, out, list,
-                       left);
-    e = hipGetLastError();
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(crc_light_pair_leftover_kernel<DescSource>, dim3(kLeftoverWgs), dim3(256), 0, s,
-                           DescSource{d}, n, img, out, (const uint32_t *)left, next_left, (const uint32_t *)list,
-                           (uint32_t *)nullptr);
-        e = hipGetLastError();
-    }
-    if (e != hipSuccess) reset_pair_counters(s);
-    return scratch_done(s, list, pooled, e);
-}
-
 // Read-only CRC descriptor batches the census saw as one contiguous run of equal L-byte fragments (L = 64 B .. 2 KiB,
 // a power of two; config A's shape as descriptors): the message's packed rows (crc_regular_kernel<kSub>) over the
 // whole 8 KiB items from d[0].addr, each wave checking its items' descriptors first; items holding anything else are
@@ -5344,10 +5087,10 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
     const uint32_t given = rows_hint;
     // read-only: two fragments per wave only for 1-2 KiB fragments ending off the 16-byte grid (IB's 1,976 B), where
     // the piece streams take their five-load variant (profiles/r05/crc_ro_pairs_ab.txt)
-    bool small = false, ragged = false;
+    bool small = false;
     uint32_t contig = 0;
     rows_hint = learned_rows_hint(DescSource{d}, n, s, 0, rows_hint, &pairs, &nhalf, 1u, nullptr, &whole, true, &small,
-                                  nullptr, &contig, &ragged);
+                                  nullptr, &contig);
     // one contiguous run of equal 64 B .. 2 KiB fragments (a message as descriptors): packed rows, the rest after it
     static const bool packed_desc = [] {  // (A/B knob LAMPI_PACKED_DESC=0: off)
         const char *e = LAMPI_AB_ENV("LAMPI_PACKED_DESC");
@@ -5380,12 +5123,6 @@ hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
                                           rows_hint <= kSegRows ? 1u : (rows_hint + kLightRoRows - 1) / kLightRoRows);
     if (rows_hint > 1 && n * ((rows_hint + kSegRows - 1) / kSegRows) <= 0xFFFFFFFFull)
         return launch_row_segments<false, kStreamWv, kStreamCap>(d, n, out, img, s, rows_hint);
-    // mixed lengths of up to kRaggedMaxRows rows at 64-byte-aligned addresses (config C): the ragged rows (round 6)
-    static const bool ragged_on = [] {  // (A/B knob LAMPI_RAGGED=0: off)
-        const char *e = LAMPI_AB_ENV("LAMPI_RAGGED");
-        return !(e && e[0] == '0');
-    }();
-    if (ragged && ragged_on && given <= 1 && n >= kRaggedMin) return launch_crc_desc_ragged(d, n, out, img, s);
     if (n >= kSplitMin && n <= kSplitMax && !small) {  // both size classes, one launch each (SplitDescSource)
         const uint32_t fpg = frags_per_wg(n);
         hipLaunchKernelGGL((crc_stream_kernel<SplitDescSource<false>, kStreamD, kStreamK, false, kStreamWv, kStreamCap>),

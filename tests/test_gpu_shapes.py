@@ -493,12 +493,12 @@ def _ragged_layout(rng, lens, align=64):
 @pytest.mark.parametrize("case", ["zipf", "bytes"])
 def test_learned_ragged_descriptors(cuda, oracle, case):
     """Round 6: read-only CRC descriptor batches of mixed lengths up to 16 rows at 64-byte-aligned
-    addresses run on crc_ragged_kernel once the census has seen the shape -- per-fragment row counts, the last row
-    masked to its npc pieces and h bytes, the register shifted back by 64 - h bytes.  `zipf`: config C's lengths (64-byte
+    addresses, under whatever schedule the learned shape selects (the piece streams; the ragged whole-row kernel of
+    commit dcda139 passed this test and was not adopted).  `zipf`: config C's lengths (64-byte
     multiples); `bytes`: any length 1 .. 65,536 (the ragged 1-7-row lengths 4,097 .. 28,671 among them) with random
     registers.  Then, on the same array under the learned shape: some descriptors moved off the 64-byte grid (odd and
-    16-byte-aligned addresses), emptied or lengthened past 16 rows (listed for the leftover launch); the same lengths at
-    odd addresses (1-byte alignment; another schedule); a shorter batch -- every call vs the oracle."""
+    16-byte-aligned addresses), emptied or lengthened past 16 rows; the same lengths at odd addresses (1-byte
+    alignment); a shorter batch -- every call vs the oracle."""
     import torch
 
     from lampi_amd.workload import zipf_lengths
