@@ -3424,6 +3424,18 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     uint32_t C[K];
 #pragma unroll
     for (int c = 0; c < K; ++c) C[c] = 0;
+    // a fragment's checksum waits in lane j kV + r of `res` (fragment kV (f0 + kWv j) + r) and the wave stores all of
+    // them once, after its last row: a store inside the ring is one more operation each later wait counts
+    // (CRC only: with kSum the compiler read a ring register before its wait -- tests/test_isa_guard.py)
+    const bool late = !kSum && nfr * (uint32_t)kV <= 64u;
+    uint32_t res = 0u;
+    auto emit = [&](uint32_t j, uint32_t r, uint32_t v) {  // item j (K i + c) of this wave, row r (kV > 1)
+        if (late) {
+            res = (uint32_t)lane == j * kV + (kV > 1 ? r : 0u) ? v : res;
+        } else if (lane == 0) {
+            out[kV > 1 ? (f0 + kWv * j) * kV + r : f0 + kWv * j] = v;
+        }
+    };
     auto process = [&](RowsK<K> &b, const GroupTask &t) {
         if constexpr (kCopy) {
 #pragma unroll
@@ -3457,11 +3469,9 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
                 uint32_t x[K];
 #pragma unroll
                 for (int c = 0; c < K; ++c) x[c] = wave_add(C[c]);
-                if (lane == 0) {
 #pragma unroll
-                    for (int c = 0; c < K; ++c)
-                        if (K * t.i + c < nfr) out[kV > 1 ? frag(t.i, c) * kV + t.r : frag(t.i, c)] = x[c];
-                }
+                for (int c = 0; c < K; ++c)
+                    if (K * t.i + c < nfr) emit(K * t.i + c, t.r, x[c]);
             }
             return;
         }
@@ -3504,12 +3514,10 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
             for (int c = 0; c < K; ++c) x[c] = lane_combine(lds, k, C[c]);
 #pragma unroll
             for (int c = 0; c < K; ++c) x[c] = wave_xor(x[c]);
-            if (lane == 0) {
 #pragma unroll
-                for (int c = 0; c < K; ++c)
-                    if (K * t.i + c < nfr && !(kDesc && ((bad >> (K * t.i + c)) & 1u)))
-                        out[kV > 1 ? frag(t.i, c) * kV + t.r : frag(t.i, c)] = __builtin_bswap32(x[c]);
-            }
+            for (int c = 0; c < K; ++c)
+                if (K * t.i + c < nfr && !(kDesc && ((bad >> (K * t.i + c)) & 1u)))
+                    emit(K * t.i + c, t.r, __builtin_bswap32(x[c]));
         }
     };
     // steady state: slot S is waited for, checksummed (and stored) and refilled with the task
@@ -3545,6 +3553,11 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     }
 #undef LAMPI_RING_STEP
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the clamped re-loads before exit
+    if constexpr (kSub == 64) {
+        const uint32_t j = (uint32_t)lane / kV;
+        if (late && j < nfr && !(kDesc && ((bad >> j) & 1u)))
+            out[kV > 1 ? (f0 + kWv * j) * kV + (uint32_t)lane % kV : f0 + kWv * j] = res;
+    }
 }
 
 // ---- SUM -------------------------------------------------------------------------------

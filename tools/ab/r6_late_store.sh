@@ -1,0 +1,31 @@
+#!/usr/bin/env bash
+# Round 6: crc_regular_kernel keeps each fragment's checksum in a lane and stores the wave's results once after its last
+# row (no store inside the asm ring) -- "new" (product library) against the library before (ab_libs/), interleaved:
+# the GPU parity/shape/send suites first, then config B (messages, descriptors), 16 KiB messages, the fused copy.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_gpu_send.py -m gpu -q \
+  --timeout 120 --timeout-method thread -x > gpurun_out/r6_late_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r6_late_tests.log; [ $rc -eq 0 ] || exit $rc
+line() {
+  local tag=$1; shift
+  local out
+  out=$(timeout -k 10 200 env "$@" 2>/dev/null | tail -1) || { echo "FAIL $tag"; exit 1; }
+  python - "$tag" "$out" <<'PY'
+import json, sys
+d = json.loads(sys.argv[2]); r = d.get("roofline", {})
+print(f"{sys.argv[1]:30s} frac {r.get('frac')} kernel_ms {r.get('kernel_avg_ms')} parity {d.get('parity', {}).get('ok')}", flush=True)
+PY
+}
+OLD="LAMPI_CSUM_LIB=$PWD/ab_libs/liblampi_csum_before.so"
+NEW="LAMPI_CSUM_LIB=$PWD/lampi_amd/liblampi_csum.so"
+for r in 1 2 3; do
+  for v in new old; do
+    if [ $v = new ]; then L=$NEW; else L=$OLD; fi
+    line "r$r B msg $v" $L python bench.py --no-cpu-baseline --steps 20
+    line "r$r B desc $v" $L python bench.py --desc --no-cpu-baseline --steps 10 --warmup 30
+    line "r$r 16K msg $v" $L python bench.py --frags 1048576 --frag-bytes 16384 --no-cpu-baseline --steps 10
+    line "r$r B bcopy $v" $L python bench.py --bcopy --no-cpu-baseline --steps 10
+  done
+done
