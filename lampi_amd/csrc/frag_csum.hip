@@ -3237,7 +3237,7 @@ __device__ __forceinline__ void crc_chunks(const uint32_t *lds, const CrcLane &k
 // (none for kSub = 1), the group's values meet by DPP (group_reduce) and the group's last lane stores
 // out[row * 64 / kSub + l / kSub].  Launched with kV = 2 (every row a fragment end); read-only.
 template <int kChains, bool kCopy = false, bool kCoal = kCopy, int kDepth = 3, int kV = 1,
-          bool kSum = false, int kWv = kWaves, int kCap = 0, bool kDesc = false, int kSub = 64>
+          bool kSum = false, int kWv = kWaves, int kCap = 0, bool kDesc = false, int kSub = 64, bool kDiag = false>
 __global__ void __launch_bounds__(64 * kWv) __attribute__((amdgpu_waves_per_eu(kCap > 0 ? kCap : 1)))
 crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, size_t frag_len, uint32_t partial,
                    const uint32_t *__restrict__ img, uint32_t *__restrict__ out, uint8_t *__restrict__ dst,
@@ -3249,6 +3249,13 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
     constexpr int kS = kCoal ? kRowBytes / 4 : 16;  // chunk stride of a lane
     __shared__ __attribute__((aligned(16))) uint32_t lds[kLdsBytes / 4];
     const int lane = threadIdx.x & 63;
+    if constexpr (kDiag) {  // timeline diagnostic (diag_regular_timeline): [0] entry, [8] HW_ID, [9] XCC_ID
+        if (threadIdx.x == 0) {
+            g_stream_diag[(size_t)blockIdx.x * 16] = __builtin_amdgcn_s_memrealtime();
+            g_stream_diag[(size_t)blockIdx.x * 16 + 8] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (31 << 11));
+            g_stream_diag[(size_t)blockIdx.x * 16 + 9] = (uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (31 << 11));
+        }
+    }
     const uint32_t R = (uint32_t)(frag_len / kRowBytes);
     const uint32_t f0 = uniform(blockIdx.x * kWv * fpw + (threadIdx.x >> 6));
     // fragments of this wave: f0 + kWv*j, j < nfr; processed in groups of K
@@ -3413,6 +3420,9 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
             issue_all();
         lds_barrier();
     }
+    if constexpr (kDiag) {  // [1] tables staged
+        if (threadIdx.x == 0) g_stream_diag[(size_t)blockIdx.x * 16 + 1] = __builtin_amdgcn_s_memrealtime();
+    }
     if (nfr == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         return;
@@ -3557,6 +3567,9 @@ crc_regular_kernel(const uint8_t *__restrict__ base, uint32_t n, uint32_t fpw, s
         const uint32_t j = (uint32_t)lane / kV;
         if (late && j < nfr && !(kDesc && ((bad >> j) & 1u)))
             out[kV > 1 ? (f0 + kWv * j) * kV + (uint32_t)lane % kV : f0 + kWv * j] = res;
+    }
+    if constexpr (kDiag) {  // [2 + w] wave w done
+        if (lane == 0) g_stream_diag[(size_t)blockIdx.x * 16 + 2 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -5166,6 +5179,25 @@ hipError_t diag_stream_timeline(const lampi_frag_desc *d, size_t n, uint32_t *ou
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((crc_stream_kernel<DescSource, kStreamD, kStreamK, false, kStreamWv, kStreamCap, true>), wgs,
                        dim3(64 * kStreamWv), 0, s, DescSource{d}, n, fpg, img, out, nullptr);
+    return hipGetLastError();
+}
+
+// Timeline diagnostic of config B's kernel (tools/microbench/regular_timeline.py): a read-only CRC message of 4 KiB
+// fragments on launch_regular's grid and schedule (pairs, pick_regular_fpw), the kDiag instantiation stamping 16
+// words per workgroup into `stamps`; returns the workgroup count in *nwg.  Not on any product path.
+hipError_t diag_regular_timeline(const uint8_t *base, size_t n, uint32_t *out, const uint32_t *img, uint64_t *stamps,
+                                 hipStream_t s, uint32_t *nwg) {
+    const size_t nv = n / 2;
+    if (nv == 0 || (n & 1u) || nv > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t fpw = pick_regular_fpw(nv, 2 * kRowBytes);
+    const dim3 g = grid_for(nv, fpw);
+    *nwg = g.x;
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_stream_diag), &stamps, sizeof(stamps), 0,
+                                          hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((crc_regular_kernel<kRegularChains, false, false, 3, 2, false, kWaves, 0, false, 64, true>), g,
+                       dim3(kBlock), 0, s, base, (uint32_t)nv, fpw, (size_t)2 * kRowBytes, 0xFFFFFFFFu, img, out,
+                       nullptr, (size_t)0);
     return hipGetLastError();
 }
 

@@ -34,6 +34,8 @@ int crc_grid(int device);
 // rows_hint (LAMPI_CSUM_ROWS_HINT): row segments per fragment (RowSegSource), 1 = none
 hipError_t diag_stream_timeline(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
                                 uint64_t *stamps, hipStream_t s, uint32_t *nwg);
+hipError_t diag_regular_timeline(const uint8_t *base, size_t n, uint32_t *out, const uint32_t *img, uint64_t *stamps,
+                                 hipStream_t s, uint32_t *nwg);
 hipError_t launch_crc_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img, int grid,
                            hipStream_t s, bool plan = false, uint32_t rows_hint = 1);
 // One wavefront per fragment (crc_rows_kernel / sum_rows_kernel), mode = lampi_csum_mode.

@@ -573,6 +573,22 @@ int lampi_diag_stream_timeline(const lampi_frag_desc *d_descs, size_t n, uint32_
     return e != hipSuccess ? -to_int(e) : (int)nwg;
 }
 
+// Internal diagnostic (not in include/lampi_csum.h): config B's kernel's timeline on a read-only CRC message of n 4 KiB
+// fragments at d_base (n even), 16 u64 per workgroup into d_stamps (tools/microbench/regular_timeline.py).  Returns
+// the workgroup count or a negative hipError_t.
+int lampi_diag_regular_timeline(const void *d_base, size_t n, uint32_t *d_out, uint64_t *d_stamps, void *stream) {
+    if (n == 0 || !d_base || !d_out || !d_stamps) return -to_int(hipErrorInvalidValue);
+    int dev = 0;
+    hipError_t e = current_device(&dev);
+    if (e != hipSuccess) return -to_int(e);
+    const uint32_t *img = nullptr;
+    e = device_tables(dev, &img);
+    if (e != hipSuccess) return -to_int(e);
+    uint32_t nwg = 0;
+    e = diag_regular_timeline((const uint8_t *)d_base, n, d_out, img, d_stamps, (hipStream_t)stream, &nwg);
+    return e != hipSuccess ? -to_int(e) : (int)nwg;
+}
+
 // Internal diagnostic (retired from include/lampi_csum.h in round 5): lampi_frag_csum_batch's
 // results on the north_star's baseline schedule, one wavefront walking each fragment's 4 KiB rows
 // (crc_rows_kernel / sum_rows_kernel) -- kept for bench.py's config C comparison and the parity tests only.
