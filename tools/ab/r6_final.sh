@@ -31,6 +31,9 @@ step bench_64_desc_sum 300 python bench.py --desc --frags 16777216 --frag-bytes 
 step bench_desc4k 300 python bench.py --desc --warmup 30 --no-cpu-baseline
 step bench_recv_gm 300 python bench.py --recv --frags 16384 --frag-bytes 65456
 step bench_recv_gm_sum 300 python bench.py --recv --frags 16384 --frag-bytes 65456 --mode sum
+step bench_recv_ib 300 python bench.py --recv --frags 262144 --frag-bytes 1976 --warmup 30
+step bench_recv_ib_sum 300 python bench.py --recv --frags 262144 --frag-bytes 1976 --mode sum --warmup 30
+step bench_B_1g 300 python bench.py --frags 262144 --no-cpu-baseline
 step bench_bcopy 300 python bench.py --bcopy --steps 10
 step bench_bcopy_sum 300 python bench.py --bcopy --mode sum --steps 10
 step bench_e2e 300 python bench.py --e2e
