@@ -112,8 +112,24 @@ def main():
                              {"sq_per_4KiB_row": {"SQ_INSTS_VALU": round(valu / rows, 1), "SQ_INSTS_LDS": round(lds / rows, 1),
                                                   "source": "profiles/r06/pmc/configC_SQ_INSTS_VALU.csv (round 6, own "
                                                             "pass: SQ_INSTS_VALU, SQ_INSTS_LDS, SQ_WAVES)"}})
+    # config B on the round-6 final library (tools/ab/r6_pmc_b.sh), when its passes are present
+    if os.path.exists(os.path.join(PMC, "B6_FETCH_SIZE.csv")):
+        f, _ = phase("B6", "FETCH_SIZE", "crc_regular_kernel", 1e6)
+        w, _ = phase("B6", "WRITE_SIZE", "crc_regular_kernel", 1)
+        rowsB = B / 4096
+        sq = {c: round(phase("B6", c, "crc_regular_kernel", 1, fname="SQ_INSTS_VALU")[0] / rowsB, 1)
+              for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU")}
+        sq["source"] = "profiles/r06/pmc/B6_SQ_INSTS_VALU.csv (round 6 final library, own pass)"
+        t["crc_4194304x4096"] = entry("crc_regular_kernel", f, w, B,
+                                      "profiles/r06/pmc/B6_{FETCH,WRITE}_SIZE.csv (round 6 final library, "
+                                      "tools/ab/r6_pmc_b.sh: bench.py; writes = the 4-byte results)",
+                                      {"sq_per_4KiB_row": sq})
+        f, _ = phase("desc6", "FETCH_SIZE", "crc_regular_kernel", 1e6)
+        t["crc_desc_4194304x4096"] = entry("crc_regular_kernel<kDesc>", f, None, B,
+                                           "profiles/r06/pmc/desc6_FETCH_SIZE.csv (round 6 final library: bench.py "
+                                           "--desc; reads include the 64 MiB of descriptors)")
     json.dump(t, open(path, "w"), indent=1)
-    for k in ["crc_bcopy_4194304x4096", "crc_bcopy_desc_4194304x4096", "crc_bcopy_desc_src8", "crc_bcopy_gm_slots",
+    for k in ["crc_4194304x4096", "crc_desc_4194304x4096", "crc_bcopy_4194304x4096", "crc_bcopy_desc_4194304x4096", "crc_bcopy_desc_src8", "crc_bcopy_gm_slots",
               "sum_bcopy_4194304x4096", "sum_bcopy_desc_4194304x4096", "sum_bcopy_gm_slots", "crc_1048576x1024",
               "crc_16777216x64", "crc_configC"]:
         print(k, t[k]["traffic_over_algorithmic"], t[k].get("sq_per_4KiB_row", ""))
