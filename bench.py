@@ -615,7 +615,7 @@ def run_device(args):
                     if args.shard is not None else
                     f"{n} x {L} B fragments per GPU, device-resident, "
                     f"{'CRC-32/MPEG-2 (uicrc)' if crc else 'uicsum'}, "
-                    f"{('one descriptor per fragment, LAMPI_CSUM_ROWS_HINT(%d)' % args.rows_hint) if args.desc and args.rows_hint > 1 else 'one descriptor per fragment (piece streams)' if args.desc else 'uniform fragments (regular kernel schedule)'}")
+                    f"{('one descriptor per fragment, LAMPI_CSUM_ROWS_HINT(%d)' % args.rows_hint) if args.desc and args.rows_hint > 1 else 'one descriptor per fragment (the schedule of the learned batch shape: roofline.kernel)' if args.desc else 'one contiguous message (roofline.kernel)'}")
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -647,6 +647,11 @@ def run_device(args):
                 "kernel_avg_ms": round(kern_avg_s * 1e3, 4),
                 "kernel_ms_min_median_max": [round(x, 4) for x in (min(kern_ms), sorted(kern_ms)[len(kern_ms) // 2], max(kern_ms))],
                 "algorithmic_bytes_per_launch": n * L,
+                # + the 16-byte descriptor read (--desc) and the 4-byte result write per fragment
+                "incl_metadata": {"bytes": n * (L + (16 if args.desc else 0) + 4),
+                                  "achieved": round(n * (L + (16 if args.desc else 0) + 4) / kern_avg_s / 1e9, 1),
+                                  "frac": round(n * (L + (16 if args.desc else 0) + 4) / kern_avg_s / 1e9
+                                                / HBM_PEAK_GBS, 4)},
                 "traffic_source": None if traffic is None else traffic.get("source"),
                 "sq_per_4KiB_row": None if traffic is None else traffic.get("sq_per_4KiB_row"),
                 "note": "rank 0's kernel; every rank's in per_gpu",
