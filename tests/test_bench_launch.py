@@ -52,6 +52,12 @@ def test_dry_run_launches_n_ranks(gpus, mode, oracle):
     assert (int(d["parity"]["xor"], 16), int(d["parity"]["wsum"], 16)) == want
     assert d["parity"]["ok"] is True and d["parity"]["all_ranks_ok"] is True
     assert d["aggregate"]["roofline_frac"] > 0
+    # the roofline object: payload bytes per launch, and beside them the 4-byte results (messages; + the 16-byte
+    # descriptors with --desc)
+    rf = d["roofline"]
+    n = d["config"]["fragments_per_gpu"]
+    assert rf["algorithmic_bytes_per_launch"] == n * 4096
+    assert rf["incl_metadata"]["bytes"] == n * (4096 + 4) and rf["incl_metadata"]["frac"] >= rf["frac"]
 
 
 @pytest.mark.parametrize("mode", ["crc", "sum"])
