@@ -3659,6 +3659,33 @@ __device__ __forceinline__ uint32_t sum_copy_frag(const FragInfo &fi, uint32_t t
     return acc;
 }
 
+// SUM messages of fragments of L = 64 .. 1024 bytes (a power of two; round 6): one short-lived 128-thread workgroup
+// per 4 KiB of the message, thread t the 16-byte chunks at 16 t and 2048 + 16 t, non-temporal -- config B SUM's shape
+// (sum_copy_wg_kernel) over 4096 / L fragments at once.  A fragment's chunks sit in kG = L / 16 consecutive lanes of
+// one wave: summed by DPP (group_reduce; a whole wave for 1 KiB), the group's last lane stores.  Whole words only:
+// every chunk is on its fragment's word grid (L is a multiple of 16).
+template <int kG>
+__global__ void __launch_bounds__(128) sum_row4k_kernel(const uint8_t *__restrict__ base, uint32_t *__restrict__ out) {
+    constexpr uint32_t L = 16u * kG, F = (uint32_t)kRowBytes / L;  // fragment bytes, fragments per 4 KiB
+    static_assert(kG >= 4 && kG <= 64 && (kG & (kG - 1)) == 0, "64 B .. 1 KiB fragments");
+    const uint32_t t = threadIdx.x;
+    gbyte *p = (gbyte *)(base + (size_t)blockIdx.x * kRowBytes + 16u * t);
+    const u32x4 a = ld16u((gu32x4_a1 *)p), b = ld16u((gu32x4_a1 *)(p + kRowBytes / 2));
+    uint32_t s0 = a.x + a.y + a.z + a.w, s1 = b.x + b.y + b.z + b.w;
+    if constexpr (kG == 64) {
+        s0 = wave_add(s0);
+        s1 = wave_add(s1);
+    } else {
+        s0 = group_reduce<kG, true>(s0);
+        s1 = group_reduce<kG, true>(s1);
+    }
+    if ((t & (kG - 1u)) == kG - 1u) {
+        const size_t f = (size_t)blockIdx.x * F + (16u * t) / L;
+        out[f] = s0;
+        out[f + F / 2] = s1;
+    }
+}
+
 template <class Src, int kT = kSumWgThreads>
 __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
     static_assert(!Src::kPhase, "word-grid sources only (read-only ones: row groups of read-only SUM batches)");
@@ -4979,7 +5006,8 @@ constexpr size_t kSplitMin = 1024, kSplitMax = 65536;
 // chain row by row -- the items holding any other fragment listed by the kernel and checksummed by
 // crc_light_pair_leftover_kernel (the pair kernel's counters and leftover launch).
 constexpr size_t kRegDescMinPairs = 2048;
-constexpr size_t kPackedMinRows = 256;  // packed rows: smaller batches keep the other schedules (one launch)
+constexpr size_t kPackedMinRows = 256;
+constexpr size_t kSumRow4kMinRows = 256;  // sum_row4k_kernel: smaller messages keep the other schedules  // packed rows: smaller batches keep the other schedules (one launch)
 static uint32_t pick_regular_fpw(size_t n, size_t span);
 static hipError_t launch_crc_desc_whole(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
                                         hipStream_t s, uint32_t R) {
@@ -5661,6 +5689,29 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
         const char *e = LAMPI_AB_ENV("LAMPI_PACKED_SUM");
         return e ? (size_t)std::atoll(e) : (size_t)1024;
     }();
+    // fragments of 64 B .. 1 KiB (powers of two): one short-lived workgroup per 4 KiB of the message (sum_row4k_kernel),
+    // the message's last fragments (past its last whole 4 KiB) through the schedules below.  A/B knob LAMPI_SUM_ROW4K=1:
+    // on (not yet measured on the GPU: off in the product library)
+    static const bool row4k = [] {
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_ROW4K");
+        return e && e[0] == '1';
+    }();
+    if (row4k && frag_len >= 64 && frag_len <= 1024 && (frag_len & (frag_len - 1)) == 0 &&
+        msg_len / kRowBytes >= kSumRow4kMinRows && msg_len / kRowBytes <= 0xFFFFFFFFull) {
+        const size_t nrow = msg_len / kRowBytes, done = nrow * (kRowBytes / frag_len);
+        const dim3 g((unsigned)nrow);
+        switch (frag_len) {
+            case 64: hipLaunchKernelGGL(sum_row4k_kernel<4>, g, dim3(128), 0, s, base, out); break;
+            case 128: hipLaunchKernelGGL(sum_row4k_kernel<8>, g, dim3(128), 0, s, base, out); break;
+            case 256: hipLaunchKernelGGL(sum_row4k_kernel<16>, g, dim3(128), 0, s, base, out); break;
+            case 512: hipLaunchKernelGGL(sum_row4k_kernel<32>, g, dim3(128), 0, s, base, out); break;
+            default: hipLaunchKernelGGL(sum_row4k_kernel<64>, g, dim3(128), 0, s, base, out); break;
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess || done >= n) return e;
+        return launch_sum_msg(base + done * frag_len, msg_len - done * frag_len, frag_len, n - done, out + done, img,
+                              grid, s);
+    }
     if (frag_len <= packed_max) {
         size_t done = 0;
         const hipError_t e = launch_packed<true>(base, msg_len, frag_len, 0u, out, nullptr, s, &done);
