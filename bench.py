@@ -406,6 +406,9 @@ def _read_schedule(crc: bool, desc: bool, n: int, L: int, rows_hint: int) -> str
         if L <= 2048:
             return "sum_copy_waves_kernel<DescSource> (learned: one fragment per wave)"
         return "sum_copy_wg_kernel<DescSource> (learned: two one-row fragments per workgroup)"
+    if not crc and pow2 and 64 <= L <= 1024 and n * L >= 256 * 4096:
+        return (f"sum_row4k_kernel<{L // 16}> (one short-lived 128-thread workgroup per 4 KiB of the message, "
+                f"{4096 // L} fragments each)")
     if pow2 and 64 <= L <= (2048 if crc else 1024) and n * L >= 256 * 4096:
         return f"crc_regular_kernel<{'kSum, ' if not crc else ''}kSub = {L // 64}> (packed rows: {4096 // L} fragments per 4 KiB row)"
     if crc:

@@ -5690,11 +5690,13 @@ hipError_t launch_sum_msg(const uint8_t *base, size_t msg_len, size_t frag_len, 
         return e ? (size_t)std::atoll(e) : (size_t)1024;
     }();
     // fragments of 64 B .. 1 KiB (powers of two): one short-lived workgroup per 4 KiB of the message (sum_row4k_kernel),
-    // the message's last fragments (past its last whole 4 KiB) through the schedules below.  A/B knob LAMPI_SUM_ROW4K=1:
-    // on (not yet measured on the GPU: off in the product library)
+    // the message's last fragments (past its last whole 4 KiB) through the schedules below.  Same box, interleaved
+    // (profiles/r06/sum_row4k_ab.txt), against the packed rows: 1 GiB of 1 KiB (config A's shape) 74.0 -> 83.1%, 512 B
+    // 70.9 -> 81.8%, 256 B 67.7 -> 82.0%, 64 B 61.9 -> 76.8%; 16 GiB of 1 KiB 77.3 -> 84.7%.  A/B knob
+    // LAMPI_SUM_ROW4K=0: off (the packed rows below)
     static const bool row4k = [] {
         const char *e = LAMPI_AB_ENV("LAMPI_SUM_ROW4K");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     if (row4k && frag_len >= 64 && frag_len <= 1024 && (frag_len & (frag_len - 1)) == 0 &&
         msg_len / kRowBytes >= kSumRow4kMinRows && msg_len / kRowBytes <= 0xFFFFFFFFull) {

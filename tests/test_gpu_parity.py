@@ -76,9 +76,10 @@ def test_regular_batches_every_schedule(cuda, oracle, L, mode):
 @pytest.mark.parametrize("L", [64, 128, 256, 512, 1024, 2048])
 def test_packed_row_messages(cuda, oracle, L, mode):
     """Messages of 64 B .. 2 KiB fragments on config B's kernel in packed rows (round 6: 64 / kSub fragments per
-    4 KiB row, crc_regular_kernel<kSub>): whole 8 KiB items through the packed launch, the rest -- a tail of up to
-    two rows' fragments and a short last fragment -- through the other schedules; random registers (CRC), an
-    unaligned base (no packed launch), sizes just at and above the packed minimum (256 rows)."""
+    4 KiB row, crc_regular_kernel<kSub>; SUM up to 1 KiB on sum_row4k_kernel, one short-lived workgroup per 4 KiB):
+    whole 8 KiB items (4 KiB rows) through that launch, the rest -- a tail of up to two rows' fragments and a short
+    last fragment -- through the other schedules; random registers (CRC), unaligned bases, sizes just at and above
+    the minimum (256 rows)."""
     import torch
 
     dv = _dv()

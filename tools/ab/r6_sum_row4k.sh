@@ -1,11 +1,11 @@
 #!/usr/bin/env bash
 # Round 6: SUM messages of 64 B .. 1 KiB fragments on short-lived 128-thread workgroups, one per 4 KiB of the message
-# (sum_row4k_kernel) against the packed rows (LAMPI_SUM_ROW4K=0) -- the GPU tests that cover these messages first
-# (product library), then interleaved bench lines (A/B build).
+# (sum_row4k_kernel, A/B build, LAMPI_SUM_ROW4K=1) against the packed rows (=0) -- the GPU tests that cover these
+# messages first with the switch on, then interleaved bench lines.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -m gpu -v --timeout 120 \
+LAMPI_CSUM_LIB="$PWD/lampi_amd/liblampi_csum_ab.so" LAMPI_SUM_ROW4K=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py -m gpu -v --timeout 120 \
   --timeout-method thread -k "packed_row_messages or config_a_shape or small_fragment or uniform" > gpurun_out/r6_row4k_tests.log 2>&1
 rc=$?; grep -cE "PASSED" gpurun_out/r6_row4k_tests.log; grep -E "FAILED|ERROR" gpurun_out/r6_row4k_tests.log | head; tail -2 gpurun_out/r6_row4k_tests.log; [ $rc -eq 0 ] || exit $rc
 export LAMPI_CSUM_LIB="$PWD/lampi_amd/liblampi_csum_ab.so"
