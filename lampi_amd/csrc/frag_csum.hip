@@ -3686,6 +3686,40 @@ __global__ void __launch_bounds__(128) sum_row4k_kernel(const uint8_t *__restric
     }
 }
 
+// The same over a descriptor batch of equal L-byte fragments (round 6): workgroup b takes fragments b F .. b F + F - 1
+// (F = 4096 / L), each thread loading the descriptors of its two chunks' fragments first and reading its chunks at their
+// own addresses -- a fragment of another length is read as zeros (the table image's zero chunk), not emitted, and its
+// pair listed for sum_pair_leftover_kernel (the pair counters), so nothing outside the batch's fragments is read.
+template <int kG>
+__global__ void __launch_bounds__(128) sum_row4k_desc_kernel(const lampi_frag_desc *__restrict__ d,
+                                                             const uint32_t *__restrict__ img, uint32_t *__restrict__ out,
+                                                             uint32_t *__restrict__ list, uint32_t *left) {
+    constexpr uint32_t L = 16u * kG, F = (uint32_t)kRowBytes / L;
+    static_assert(kG >= 4 && kG <= 64 && (kG & (kG - 1)) == 0, "64 B .. 1 KiB fragments");
+    const uint32_t t = threadIdx.x, j0 = (16u * t) / L, o = 16u * t - j0 * L;  // chunk 0: fragment j0, offset o
+    const size_t f0 = (size_t)blockIdx.x * F;
+    const lampi_frag_desc x0 = d[f0 + j0], x1 = d[f0 + j0 + F / 2];
+    const bool ok0 = x0.length == L, ok1 = x1.length == L;
+    gbyte *zero = (gbyte *)(img + kImgZero);
+    const u32x4 a = ld16u((gu32x4_a1 *)(ok0 ? (gbyte *)(uintptr_t)x0.addr + o : zero));
+    const u32x4 b = ld16u((gu32x4_a1 *)(ok1 ? (gbyte *)(uintptr_t)x1.addr + o : zero));
+    uint32_t s0 = a.x + a.y + a.z + a.w, s1 = b.x + b.y + b.z + b.w;
+    if constexpr (kG == 64) {
+        s0 = wave_add(s0);
+        s1 = wave_add(s1);
+    } else {
+        s0 = group_reduce<kG, true>(s0);
+        s1 = group_reduce<kG, true>(s1);
+    }
+    if ((t & (kG - 1u)) == kG - 1u) {
+        const size_t fa = f0 + j0, fb = fa + F / 2;
+        if (ok0) out[fa] = s0;
+        else list[atomicAdd(left, 1u)] = (uint32_t)(fa >> 1);
+        if (ok1) out[fb] = s1;
+        else list[atomicAdd(left, 1u)] = (uint32_t)(fb >> 1);
+    }
+}
+
 template <class Src, int kT = kSumWgThreads>
 __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
     static_assert(!Src::kPhase, "word-grid sources only (read-only ones: row groups of read-only SUM batches)");
@@ -5102,6 +5136,39 @@ static hipError_t launch_desc_packed(const lampi_frag_desc *d, size_t n, uint32_
     return e;
 }
 
+// SUM descriptor batches of equal 64 B .. 1 KiB fragments (the census saw one contiguous run): sum_row4k_desc_kernel
+// over the whole 4 KiB rows' worth of fragments (*done), the leftovers on sum_pair_leftover_kernel.
+static hipError_t launch_sum_desc_row4k(const lampi_frag_desc *d, size_t n, uint32_t *out, const uint32_t *img,
+                                        hipStream_t s, uint32_t L, size_t *done) {
+    *done = 0;
+    const size_t F = kRowBytes / L, nrow = n / F;
+    if (nrow < kSumRow4kMinRows || nrow > 0xFFFFFFFFull || nrow * F > 0xFFFFFFFFull) return hipSuccess;
+    uint32_t *list = nullptr, *left = nullptr, *next_left = nullptr;
+    bool pooled = false;
+    hipError_t e = stream_scratch(s, (nrow * F + 1) * sizeof(uint32_t), (void **)&list, &pooled);
+    if (e != hipSuccess) return e;
+    e = pair_counters(s, &left, &next_left);
+    if (e != hipSuccess) return scratch_done(s, list, pooled, e);
+    const dim3 g((unsigned)nrow);
+    switch (L) {
+        case 64: hipLaunchKernelGGL(sum_row4k_desc_kernel<4>, g, dim3(128), 0, s, d, img, out, list, left); break;
+        case 128: hipLaunchKernelGGL(sum_row4k_desc_kernel<8>, g, dim3(128), 0, s, d, img, out, list, left); break;
+        case 256: hipLaunchKernelGGL(sum_row4k_desc_kernel<16>, g, dim3(128), 0, s, d, img, out, list, left); break;
+        case 512: hipLaunchKernelGGL(sum_row4k_desc_kernel<32>, g, dim3(128), 0, s, d, img, out, list, left); break;
+        default: hipLaunchKernelGGL(sum_row4k_desc_kernel<64>, g, dim3(128), 0, s, d, img, out, list, left); break;
+    }
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(sum_pair_leftover_kernel, dim3(kLeftoverWgs), dim3(256), 0, s, d, nrow * F, out,
+                           (const uint32_t *)left, next_left, (const uint32_t *)list);
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) reset_pair_counters(s);
+    e = scratch_done(s, list, pooled, e);
+    if (e == hipSuccess) *done = nrow * F;
+    return e;
+}
+
 // Read-only descriptor batches under the learned-shape minimum (kShapeMin fragments) without a rows hint.
 // The lengths are on the device only: the count split gave a whole fragment to one workgroup (16 x 16 MiB
 // 2.3 ms, 1.5% of the roofline; one 64 MiB fragment 3 ms).  Every fragment runs as W row groups instead
@@ -5603,6 +5670,16 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         const char *e = LAMPI_AB_ENV("LAMPI_PACKED_DESC");
         return !(e && e[0] == '0');
     }();
+    static const bool row4k_desc = [] {  // (A/B knob LAMPI_SUM_ROW4K_DESC=1: sum_row4k_desc_kernel; measured first)
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_ROW4K_DESC");
+        return e && e[0] == '1';
+    }();
+    if (img && row4k_desc && rows_hint <= 1 && contig >= 64 && contig <= 1024 && (contig & (contig - 1)) == 0) {
+        size_t done = 0;
+        const hipError_t e = launch_sum_desc_row4k(d, n, out, img, s, contig, &done);
+        if (e != hipSuccess) return e;
+        if (done) return done >= n ? hipSuccess : launch_sum_desc(d + done, n - done, out + done, img, grid, s, false, 1u);
+    }
     if (img && packed_desc && rows_hint <= 1 && contig >= 64 && contig <= 1024 && (contig & (contig - 1)) == 0) {
         size_t done = 0;
         const hipError_t e = launch_desc_packed<true>(d, n, out, img, s, contig, &done);
