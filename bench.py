@@ -380,6 +380,9 @@ def _read_schedule(crc: bool, desc: bool, n: int, L: int, rows_hint: int) -> str
     R = (L + 4095) // 4096
     pow2 = L & (L - 1) == 0
     if desc:
+        if not crc and rows_hint <= 1 and pow2 and 64 <= L <= 1024 and n * L >= 256 * 4096:
+            return (f"sum_row4k_desc_kernel<{L // 16}> (learned: equal fragments -- one short-lived workgroup per "
+                    f"{4096 // L} fragments, each chunk read at its own descriptor's address)")
         if rows_hint <= 1 and pow2 and 64 <= L <= (2048 if crc else 1024) and n * L >= 256 * 4096:
             return (f"crc_regular_kernel<{'kSum, ' if not crc else ''}kSub = {L // 64}> (learned: the descriptors are one "
                     f"contiguous run -- packed rows from d[0].addr, {4096 // L} fragments per 4 KiB row, every "

@@ -5670,9 +5670,11 @@ hipError_t launch_sum_desc(const lampi_frag_desc *d, size_t n, uint32_t *out, co
         const char *e = LAMPI_AB_ENV("LAMPI_PACKED_DESC");
         return !(e && e[0] == '0');
     }();
-    static const bool row4k_desc = [] {  // (A/B knob LAMPI_SUM_ROW4K_DESC=1: sum_row4k_desc_kernel; measured first)
+    // ... on short-lived 4 KiB workgroups (sum_row4k_desc_kernel; profiles/r06/sum_row4k_desc_ab.txt, against the packed
+    // rows: 1 KiB 72.0 -> 79.9%, 256 B 63.6 -> 75.5%, 64 B 50.5-56.0 -> 60.4-64.3%).  A/B knob LAMPI_SUM_ROW4K_DESC=0: off
+    static const bool row4k_desc = [] {
         const char *e = LAMPI_AB_ENV("LAMPI_SUM_ROW4K_DESC");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     if (img && row4k_desc && rows_hint <= 1 && contig >= 64 && contig <= 1024 && (contig & (contig - 1)) == 0) {
         size_t done = 0;
