@@ -3720,6 +3720,33 @@ __global__ void __launch_bounds__(128) sum_row4k_desc_kernel(const lampi_frag_de
     }
 }
 
+// The fused copy of such a message (bcopy_uicsum per fragment, lampi_msg_bcopy): the same workgroups, each chunk
+// also stored (non-temporal) at dst + f * dst_stride + its offset in fragment f.
+template <int kG>
+__global__ void __launch_bounds__(128) sum_row4k_copy_kernel(const uint8_t *__restrict__ base, uint8_t *__restrict__ dst,
+                                                             size_t dst_stride, uint32_t *__restrict__ out) {
+    constexpr uint32_t L = 16u * kG, F = (uint32_t)kRowBytes / L;
+    static_assert(kG >= 4 && kG <= 64 && (kG & (kG - 1)) == 0, "64 B .. 1 KiB fragments");
+    const uint32_t t = threadIdx.x, j0 = (16u * t) / L, o = 16u * t - j0 * L;
+    gbyte *p = (gbyte *)(base + (size_t)blockIdx.x * kRowBytes + 16u * t);
+    const u32x4 a = ld16u((gu32x4_a1 *)p), b = ld16u((gu32x4_a1 *)(p + kRowBytes / 2));
+    const size_t fa = (size_t)blockIdx.x * F + j0, fb = fa + F / 2;
+    st16u((gwu32x4_a1 *)(dst + fa * dst_stride + o), a);
+    st16u((gwu32x4_a1 *)(dst + fb * dst_stride + o), b);
+    uint32_t s0 = a.x + a.y + a.z + a.w, s1 = b.x + b.y + b.z + b.w;
+    if constexpr (kG == 64) {
+        s0 = wave_add(s0);
+        s1 = wave_add(s1);
+    } else {
+        s0 = group_reduce<kG, true>(s0);
+        s1 = group_reduce<kG, true>(s1);
+    }
+    if ((t & (kG - 1u)) == kG - 1u) {
+        out[fa] = s0;
+        out[fb] = s1;
+    }
+}
+
 template <class Src, int kT = kSumWgThreads>
 __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
     static_assert(!Src::kPhase, "word-grid sources only (read-only ones: row groups of read-only SUM batches)");
@@ -5920,6 +5947,29 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
         // ragged or unaligned messages: one wave per fragment on the same tables (any alignment)
         return launch_crc_light_frag_copy(MsgCopySource{base, msg_len, frag_len, partial, dst, dst_stride}, n, img,
                                           out, s);
+    }
+    // SUM copies of 64 B .. 1 KiB fragments (powers of two): one short-lived workgroup per 4 KiB of the message
+    // (sum_row4k_copy_kernel), the fragments past the last whole 4 KiB through the schedules below.  A/B knob
+    // LAMPI_SUM_ROW4K_COPY=1: on (measured first)
+    static const bool row4k_copy = [] {
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_ROW4K_COPY");
+        return e && e[0] == '1';
+    }();
+    if (row4k_copy && mode == LAMPI_CSUM_SUM32 && frag_len >= 64 && frag_len <= 1024 && (frag_len & (frag_len - 1)) == 0 &&
+        msg_len / kRowBytes >= kSumRow4kMinRows && msg_len / kRowBytes <= 0xFFFFFFFFull) {
+        const size_t nrow = msg_len / kRowBytes, done = nrow * (kRowBytes / frag_len);
+        const dim3 g((unsigned)nrow);
+        switch (frag_len) {
+            case 64: hipLaunchKernelGGL(sum_row4k_copy_kernel<4>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+            case 128: hipLaunchKernelGGL(sum_row4k_copy_kernel<8>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+            case 256: hipLaunchKernelGGL(sum_row4k_copy_kernel<16>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+            case 512: hipLaunchKernelGGL(sum_row4k_copy_kernel<32>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+            default: hipLaunchKernelGGL(sum_row4k_copy_kernel<64>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess || done >= n) return e;
+        return launch_msg_bcopy(base + done * frag_len, msg_len - done * frag_len, frag_len, partial,
+                                dst + done * dst_stride, dst_stride, n - done, out + done, mode, img, s);
     }
     const uint64_t rpf = (frag_len + kRowBytes - 1) / kRowBytes;
     const uint32_t W = msg_len != 0 && rpf < 0xFFFFFFFFull ? sum_copy_groups((uint32_t)rpf, frag_len % kRowBytes == 0)

@@ -258,6 +258,11 @@ def test_bcopy_batch_uniform_4k(cuda, oracle):
     # fragments under 2 KiB (SUM: one 128-thread workgroup each, ragged tails)
     (1976 * 5000 + 3, 1976, 2048 + 4, 4),     # shared-memory-sized fragments, ragged tail
     (100 * 3000, 100, 128, 1),                # tiny fragments, byte-misaligned destinations
+    # SUM, 64 B .. 1 KiB fragments over >= 256 whole 4 KiB rows (round 6: sum_row4k_copy_kernel), the tail after them
+    (64 * 20000 + 17, 64, 64, 0),             # contiguous destination, a 17-byte last fragment
+    (256 * 5000 + 100, 256, 256 + 16, 3),     # slots, byte-misaligned destinations
+    (1024 * 1100, 1024, 1024 + 72, 72),       # 1 KiB payloads after a 72-byte header
+    (512 * 2100 + 511, 512, 600, 1),          # a stride that is not a multiple of 16
 ])
 def test_msg_bcopy(cuda, oracle, mode, msg_len, frag_len, stride, dst_off):
     """lampi_msg_bcopy: fragment k -> dst + k*stride with its checksum fused; gap bytes untouched."""
