@@ -5949,11 +5949,12 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                                           out, s);
     }
     // SUM copies of 64 B .. 1 KiB fragments (powers of two): one short-lived workgroup per 4 KiB of the message
-    // (sum_row4k_copy_kernel), the fragments past the last whole 4 KiB through the schedules below.  A/B knob
-    // LAMPI_SUM_ROW4K_COPY=1: on (measured first)
+    // (sum_row4k_copy_kernel), the fragments past the last whole 4 KiB through the schedules below.  Same box,
+    // interleaved (profiles/r06/sum_row4k_copy_ab.txt), against one workgroup per fragment, of read + write: 1 KiB
+    // 56.4 -> 79.3%, 256 B 17.2 -> 78.2%, 64 B 5.0 -> 79.2%.  A/B knob LAMPI_SUM_ROW4K_COPY=0: off
     static const bool row4k_copy = [] {
         const char *e = LAMPI_AB_ENV("LAMPI_SUM_ROW4K_COPY");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     if (row4k_copy && mode == LAMPI_CSUM_SUM32 && frag_len >= 64 && frag_len <= 1024 && (frag_len & (frag_len - 1)) == 0 &&
         msg_len / kRowBytes >= kSumRow4kMinRows && msg_len / kRowBytes <= 0xFFFFFFFFull) {
