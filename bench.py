@@ -1000,7 +1000,11 @@ def run_bcopy(args):
     gm_same = bool(torch.equal(gm_out, dv.msg_csum(gm_msg, gm_L, mode=mode)))
     moved = 2.0 * n * L
     achieved = moved / kern / 1e9
-    kname = ("crc_light_copy_kernel" if mode == dv.CRC32 else "sum_copy_row_kernel")
+    pow2 = L & (L - 1) == 0
+    kname = ("crc_light_copy_kernel" if mode == dv.CRC32 else
+             f"sum_row4k_copy_kernel<{L // 16}> (one short-lived workgroup per 4 KiB of the message)"
+             if pow2 and 64 <= L <= 1024 and n * L >= 256 * 4096 else
+             "sum_copy_row_kernel" if L >= 4096 else "sum_copy_wg_kernel<MsgCopySource> (one fragment per workgroup)")
     print(json.dumps({
         "metric": "device-resident fused copy+checksum GiB/s of payload (bcopy); % of HBM roofline",
         "value": round(n * L / GIB / (wall / args.steps), 2), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
