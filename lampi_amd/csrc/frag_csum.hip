@@ -3747,6 +3747,41 @@ __global__ void __launch_bounds__(128) sum_row4k_copy_kernel(const uint8_t *__re
     }
 }
 
+// Fused copies of a descriptor batch of equal 64 B .. 1 KiB fragments (lampi_frag_bcopy_batch SUM; the census saw equal
+// lengths): the descriptor kernel's workgroups, each chunk read at its fragment's source and stored at its destination;
+// a descriptor of another shape (copylen != L or csumlen > L) is left to sum_copy_list_kernel (its index listed).
+template <int kG>
+__global__ void __launch_bounds__(128) sum_row4k_copy_desc_kernel(const lampi_copy_desc *__restrict__ d,
+                                                                  const uint32_t *__restrict__ img,
+                                                                  uint32_t *__restrict__ out, uint32_t *__restrict__ list,
+                                                                  uint32_t *left) {
+    constexpr uint32_t L = 16u * kG, F = (uint32_t)kRowBytes / L;
+    static_assert(kG >= 4 && kG <= 64 && (kG & (kG - 1)) == 0, "64 B .. 1 KiB fragments");
+    const uint32_t t = threadIdx.x, j0 = (16u * t) / L, o = 16u * t - j0 * L;
+    const size_t fa = (size_t)blockIdx.x * F + j0, fb = fa + F / 2;
+    const lampi_copy_desc x0 = d[fa], x1 = d[fb];
+    const bool ok0 = x0.copylen == L && x0.csumlen <= L, ok1 = x1.copylen == L && x1.csumlen <= L;
+    gbyte *zero = (gbyte *)(img + kImgZero);
+    const u32x4 a = ld16u((gu32x4_a1 *)(ok0 ? (gbyte *)(uintptr_t)x0.src + o : zero));
+    const u32x4 b = ld16u((gu32x4_a1 *)(ok1 ? (gbyte *)(uintptr_t)x1.src + o : zero));
+    if (ok0) st16u((gwu32x4_a1 *)((uint8_t *)(uintptr_t)x0.dst + o), a);
+    if (ok1) st16u((gwu32x4_a1 *)((uint8_t *)(uintptr_t)x1.dst + o), b);
+    uint32_t s0 = a.x + a.y + a.z + a.w, s1 = b.x + b.y + b.z + b.w;
+    if constexpr (kG == 64) {
+        s0 = wave_add(s0);
+        s1 = wave_add(s1);
+    } else {
+        s0 = group_reduce<kG, true>(s0);
+        s1 = group_reduce<kG, true>(s1);
+    }
+    if ((t & (kG - 1u)) == kG - 1u) {
+        if (ok0) out[fa] = s0;
+        else list[atomicAdd(left, 1u)] = (uint32_t)fa;
+        if (ok1) out[fb] = s1;
+        else list[atomicAdd(left, 1u)] = (uint32_t)fb;
+    }
+}
+
 template <class Src, int kT = kSumWgThreads>
 __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint32_t *__restrict__ out) {
     static_assert(!Src::kPhase, "word-grid sources only (read-only ones: row groups of read-only SUM batches)");
@@ -3773,6 +3808,26 @@ __global__ void __launch_bounds__(kT) sum_copy_wg_kernel(Src src, size_t n, uint
             }
         }
     }
+}
+
+// The copy descriptors sum_row4k_copy_desc_kernel listed (list[0 .. *left)): one 128-thread workgroup per entry on a
+// fixed grid (sum_copy_wg_kernel's fragment walk, any length); zeroes the stream's other counter (the pair counters).
+__global__ void __launch_bounds__(128) sum_copy_list_kernel(const lampi_copy_desc *__restrict__ d, const uint32_t *left,
+                                                            uint32_t *next_left, const uint32_t *__restrict__ list,
+                                                            uint32_t *__restrict__ out) {
+    __shared__ uint32_t part[2][2];
+    const uint32_t t = threadIdx.x;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    uint32_t it = 0;
+    for (uint32_t e = blockIdx.x; e < c; e += gridDim.x, it ^= 1u) {
+        const size_t f = list[e];
+        const FragInfo fi = CopySource{d}.get(f);
+        const uint32_t acc = wave_add(sum_copy_frag<128, CopySource>(fi, t));
+        if ((t & 63u) == 0) part[it][t >> 6] = acc;
+        __syncthreads();
+        if (t == 0) out[f] = part[it][0] + part[it][1];
+    }
+    if (blockIdx.x == 0 && t == 0) *next_left = 0u;
 }
 
 // Fragments of at most 2 KiB (IB's payloads; the learned batch shape picks it): one fragment per wave, four
@@ -5568,7 +5623,46 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
         return launch_sum_copy_groups(CopyOnlySource{d}, n, out, s, rows_hint, pairs);
     }
     const bool crc = mode == LAMPI_CSUM_CRC32;
-    rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, &pairs, &nhalf, crc ? kShapeRows : kShapeRowsSum);
+    uint32_t contig = 0;
+    const uint32_t given = rows_hint;
+    rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, &pairs, &nhalf, crc ? kShapeRows : kShapeRowsSum,
+                                  nullptr, nullptr, false, nullptr, nullptr, &contig);
+    // SUM copies of equal 64 B .. 1 KiB fragments: one short-lived workgroup per 4 KiB of them (sum_row4k_copy_desc_kernel;
+    // A/B knob LAMPI_SUM_ROW4K_COPY_DESC=1: on, measured first), the rest after them
+    static const bool row4k_cd = [] {
+        const char *e = LAMPI_AB_ENV("LAMPI_SUM_ROW4K_COPY_DESC");
+        return e && e[0] == '1';
+    }();
+    if (!crc && row4k_cd && given <= 1 && contig >= 64 && contig <= 1024 && (contig & (contig - 1)) == 0) {
+        const size_t F = kRowBytes / contig, nrow = n / F;
+        if (nrow >= kSumRow4kMinRows && nrow * F <= 0xFFFFFFFFull) {
+            uint32_t *list = nullptr, *left = nullptr, *next_left = nullptr;
+            bool pooled = false;
+            hipError_t e = stream_scratch(s, (nrow * F + 1) * sizeof(uint32_t), (void **)&list, &pooled);
+            if (e != hipSuccess) return e;
+            e = pair_counters(s, &left, &next_left);
+            if (e != hipSuccess) return scratch_done(s, list, pooled, e);
+            const dim3 g((unsigned)nrow);
+            switch (contig) {
+                case 64: hipLaunchKernelGGL(sum_row4k_copy_desc_kernel<4>, g, dim3(128), 0, s, d, img, out, list, left); break;
+                case 128: hipLaunchKernelGGL(sum_row4k_copy_desc_kernel<8>, g, dim3(128), 0, s, d, img, out, list, left); break;
+                case 256: hipLaunchKernelGGL(sum_row4k_copy_desc_kernel<16>, g, dim3(128), 0, s, d, img, out, list, left); break;
+                case 512: hipLaunchKernelGGL(sum_row4k_copy_desc_kernel<32>, g, dim3(128), 0, s, d, img, out, list, left); break;
+                default: hipLaunchKernelGGL(sum_row4k_copy_desc_kernel<64>, g, dim3(128), 0, s, d, img, out, list, left); break;
+            }
+            e = hipGetLastError();
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(sum_copy_list_kernel, dim3(kLeftoverWgs), dim3(128), 0, s, d, (const uint32_t *)left,
+                                   next_left, (const uint32_t *)list, out);
+                e = hipGetLastError();
+            }
+            if (e != hipSuccess) reset_pair_counters(s);
+            e = scratch_done(s, list, pooled, e);
+            if (e != hipSuccess) return e;
+            const size_t done = nrow * F;
+            return done >= n ? hipSuccess : launch_bcopy_desc(d + done, n - done, out + done, mode, img, s, 1u);
+        }
+    }
     if (crc && pairs) return launch_crc_light_pair_copy(CopySource{d}, n, img, out, s, nhalf);
     if (crc) return launch_crc_light_frag_copy(CopySource{d}, n, img, out, s, rows_hint);
     return launch_sum_copy_groups(CopySource{d}, n, out, s, rows_hint, pairs);  // (pairs: a wave per fragment)

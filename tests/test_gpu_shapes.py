@@ -549,3 +549,54 @@ def test_learned_ragged_descriptors(cuda, oracle, case):
         m = n - n // 3
         got = dv.as_u32(dv.frag_csum_batch(descs, n=m, mode=dv.CRC32, stream=stream))
         assert np.array_equal(got[:m], prepared["run"][1][:m])
+
+
+@pytest.mark.parametrize("L", [64, 256, 1024])
+def test_learned_small_copy_descriptors_sum(cuda, oracle, L):
+    """Round 6: SUM fused copies of descriptor batches of equal L-byte fragments (a message's fragments into slots) run
+    one short-lived workgroup per 4 KiB of them once the census has seen the shape (sum_row4k_copy_desc_kernel); then,
+    under that shape, descriptors with another copylen (0, 1, L - 1), a csumlen past L (residue checksummed, not
+    copied) or a longer fragment (listed for sum_copy_list_kernel), and a shorter batch -- every sum and every
+    destination byte (slot gaps untouched) vs the oracle."""
+    import torch
+
+    dv = _dv()
+    rng = np.random.default_rng(5100 + L)
+    n = 300 * (4096 // L) + 37
+    stride = L + 48
+    src = torch.empty(n * L + 8192, dtype=torch.uint8, device=cuda)
+    dv.fill_stream(src, seed=5101)
+    hsrc = src.cpu().numpy()
+    so = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    do = np.arange(n, dtype=np.uint64) * np.uint64(stride) + np.uint64(5)
+    cl = np.full(n, L, np.int64)
+    ck = np.full(n, L, np.int64)
+    odd_cl, odd_ck = cl.copy(), ck.copy()
+    pick = rng.choice(n, size=n // 50 + 3, replace=False)
+    odd_cl[pick[0::3]] = rng.choice(np.array([0, 1, L - 1]), size=pick[0::3].size)
+    odd_ck[pick[1::3]] = L + 7
+    odd_cl[pick[2::3]] = L + 16
+    odd_ck[pick[2::3]] = L + 16
+    cases = {"run": (cl, ck), "odd": (odd_cl, odd_ck)}
+    dst_bytes = int(do[-1]) + 2 * L + 64
+    dst = torch.zeros(dst_bytes, dtype=torch.uint8, device=cuda)
+    prepared = {k: dv.make_copy_descs(src, so, dst, do, c, s) for k, (c, s) in cases.items()}
+    descs = prepared["run"].clone()  # one descriptor array: the census keys its shape on it
+    stream = torch.cuda.Stream(device=cuda)
+    seq = ["run"] * 20 + ["odd"] * 2 + ["run"]
+    with torch.cuda.stream(stream):
+        for i, k in enumerate(seq):
+            c, s = cases[k]
+            dst.zero_()
+            descs.copy_(prepared[k])
+            got = dv.as_u32(dv.frag_bcopy_batch(descs, mode=dv.SUM32, stream=stream))
+            want = oracle.desc_batch(hsrc, so, np.maximum(c, s).astype(np.uint32), None, 1)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (L, i, k, bad[:8].tolist())
+            stream.synchronize()
+            hd = dst.cpu().numpy()
+            want_dst = np.zeros(dst_bytes, np.uint8)
+            for j in range(n):
+                a, ln, b = int(so[j]), int(c[j]), int(do[j])
+                want_dst[b:b + ln] = hsrc[a:a + ln]
+            assert np.array_equal(hd, want_dst), (L, i, k)
