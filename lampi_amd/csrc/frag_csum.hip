@@ -5627,11 +5627,13 @@ hipError_t launch_bcopy_desc(const lampi_copy_desc *d, size_t n, uint32_t *out, 
     const uint32_t given = rows_hint;
     rows_hint = learned_rows_hint(CopySource{d}, n, s, 1, rows_hint, &pairs, &nhalf, crc ? kShapeRows : kShapeRowsSum,
                                   nullptr, nullptr, false, nullptr, nullptr, &contig);
-    // SUM copies of equal 64 B .. 1 KiB fragments: one short-lived workgroup per 4 KiB of them (sum_row4k_copy_desc_kernel;
-    // A/B knob LAMPI_SUM_ROW4K_COPY_DESC=1: on, measured first), the rest after them
+    // SUM copies of equal 64 B .. 1 KiB fragments: one short-lived workgroup per 4 KiB of them (sum_row4k_copy_desc_kernel),
+    // the rest after them.  Same box, interleaved (profiles/r06/sum_row4k_cd_ab.txt), of read + write: 1 KiB 69.0 ->
+    // 77.3%, 256 B 23.7 -> 77.7%, 64 B 6.9 -> 63.0% (to + 8 / + 1 destinations 58-74%).  A/B knob
+    // LAMPI_SUM_ROW4K_COPY_DESC=0: off
     static const bool row4k_cd = [] {
         const char *e = LAMPI_AB_ENV("LAMPI_SUM_ROW4K_COPY_DESC");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     if (!crc && row4k_cd && given <= 1 && contig >= 64 && contig <= 1024 && (contig & (contig - 1)) == 0) {
         const size_t F = kRowBytes / contig, nrow = n / F;
