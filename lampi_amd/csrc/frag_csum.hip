@@ -6037,6 +6037,31 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
                          ((uintptr_t)base & 15u) == 0 && ((uintptr_t)dst & 3u) == 0 && dst_stride % 4 == 0 &&
                          n <= 0xFFFFFFFFull;  // dword-aligned dwordx4 stores run at the aligned rate (GM slots)
     if (mode == LAMPI_CSUM_CRC32) {
+        // fragments of 64 B .. 1 KiB (powers of two) over >= 256 whole 4 KiB rows: two passes -- the copy on
+        // sum_row4k_copy_kernel (its sums land in out and are overwritten), then the read-only CRC of the source in
+        // packed rows (launch_crc_msg); the fragments past the last whole 4 KiB through the schedules below.  A/B knob
+        // LAMPI_CRC_COPY_2PASS=1: on (measured first)
+        static const bool two_pass = [] {
+            const char *e = LAMPI_AB_ENV("LAMPI_CRC_COPY_2PASS");
+            return e && e[0] == '1';
+        }();
+        if (two_pass && frag_len >= 64 && frag_len <= 1024 && (frag_len & (frag_len - 1)) == 0 &&
+            msg_len / kRowBytes >= kSumRow4kMinRows && msg_len / kRowBytes <= 0xFFFFFFFFull) {
+            const size_t nrow = msg_len / kRowBytes, done = nrow * (kRowBytes / frag_len);
+            const dim3 g((unsigned)nrow);
+            switch (frag_len) {
+                case 64: hipLaunchKernelGGL(sum_row4k_copy_kernel<4>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+                case 128: hipLaunchKernelGGL(sum_row4k_copy_kernel<8>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+                case 256: hipLaunchKernelGGL(sum_row4k_copy_kernel<16>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+                case 512: hipLaunchKernelGGL(sum_row4k_copy_kernel<32>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+                default: hipLaunchKernelGGL(sum_row4k_copy_kernel<64>, g, dim3(128), 0, s, base, dst, dst_stride, out); break;
+            }
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess) e = launch_crc_msg(base, nrow * kRowBytes, frag_len, partial, done, out, img, 0, s);
+            if (e != hipSuccess || done >= n) return e;
+            return launch_msg_bcopy(base + done * frag_len, msg_len - done * frag_len, frag_len, partial,
+                                    dst + done * dst_stride, dst_stride, n - done, out + done, mode, img, s);
+        }
         if (light_copy_ok(base, msg_len, frag_len, dst, dst_stride, n))
             return launch_crc_light_copy(base, msg_len, frag_len, partial, dst, dst_stride, n, out, img, s);
         if (regular) return launch_crc_regular_copy(base, n, frag_len, partial, dst, dst_stride, out, img, s);
