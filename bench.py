@@ -1001,7 +1001,9 @@ def run_bcopy(args):
     moved = 2.0 * n * L
     achieved = moved / kern / 1e9
     pow2 = L & (L - 1) == 0
-    kname = ("crc_light_copy_kernel" if mode == dv.CRC32 else
+    kname = ((f"sum_row4k_copy_kernel<{L // 16}> (the copy) + crc_regular_kernel<kSub = {L // 64}> (the packed-row CRC "
+              "of the source)" if pow2 and 64 <= L <= 1024 and n * L >= 256 * 4096 else "crc_light_copy_kernel")
+             if mode == dv.CRC32 else
              f"sum_row4k_copy_kernel<{L // 16}> (one short-lived workgroup per 4 KiB of the message)"
              if pow2 and 64 <= L <= 1024 and n * L >= 256 * 4096 else
              "sum_copy_row_kernel" if L >= 4096 else "sum_copy_wg_kernel<MsgCopySource> (one fragment per workgroup)")

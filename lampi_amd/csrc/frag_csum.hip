@@ -6039,11 +6039,12 @@ hipError_t launch_msg_bcopy(const uint8_t *base, size_t msg_len, size_t frag_len
     if (mode == LAMPI_CSUM_CRC32) {
         // fragments of 64 B .. 1 KiB (powers of two) over >= 256 whole 4 KiB rows: two passes -- the copy on
         // sum_row4k_copy_kernel (its sums land in out and are overwritten), then the read-only CRC of the source in
-        // packed rows (launch_crc_msg); the fragments past the last whole 4 KiB through the schedules below.  A/B knob
-        // LAMPI_CRC_COPY_2PASS=1: on (measured first)
+        // packed rows (launch_crc_msg); the fragments past the last whole 4 KiB through the schedules below.  Same box,
+        // interleaved (profiles/r06/crc_copy_2pass_ab.txt), against the one-pass table-light copy, of read + write:
+        // 1 KiB 33.9 -> 52.1%, 256 B 9.0 -> 49.5%, 64 B 2.3 -> 48.4%.  A/B knob LAMPI_CRC_COPY_2PASS=0: off
         static const bool two_pass = [] {
             const char *e = LAMPI_AB_ENV("LAMPI_CRC_COPY_2PASS");
-            return e && e[0] == '1';
+            return !(e && e[0] == '0');
         }();
         if (two_pass && frag_len >= 64 && frag_len <= 1024 && (frag_len & (frag_len - 1)) == 0 &&
             msg_len / kRowBytes >= kSumRow4kMinRows && msg_len / kRowBytes <= 0xFFFFFFFFull) {
